@@ -1,0 +1,89 @@
+/*
+ * tpst.h -- C ABI of the MI355X-native sqrt-PST engine (libtpst.so).
+ *
+ * Drop-in boundary for the BLS12-377 hot path of Testudo's sqrt-PST
+ * polynomial commitment (reference: rosariocannavo/testudo).  The reference
+ * has no FFI of its own; every entry point below replaces one Rust call
+ * site (file:line under the reference tree), see INTEGRATION.md.
+ *
+ * Conventions
+ *  - Field elements are CANONICAL (non-Montgomery) little-endian u64 limbs:
+ *      Fr  = 4 x u64 (value < r),  Fq = 6 x u64 (value < p).
+ *  - G1 affine = x || y (12 u64, 96 bytes); G2 affine = x.c0 || x.c1 ||
+ *    y.c0 || y.c1 (24 u64, 192 bytes).  The point at infinity is all zero
+ *    (x = y = 0 lies on neither curve), i.e. arkworks' Affine with the
+ *    `infinity` flag mapped to (0, 0).
+ *  - GT / Fq12 = 12 Fq in arkworks order c0.c0.c0, c0.c0.c1, c0.c1.c0, ...,
+ *    c1.c2.c1 (72 u64, 576 bytes).
+ *  - Caller owns every host buffer; the library reads inputs and writes
+ *    outputs only.  `_dev` entry points take device pointers (hipMalloc /
+ *    torch allocations on the context's device) and run on the context's
+ *    stream; bases passed to `_dev` calls are in Montgomery form (the same
+ *    bytes as arkworks' in-memory G1Affine x/y), scalars canonical (what
+ *    arkworks' msm_bigint consumes).
+ *  - Return 0 (TPST_OK) or a negative TPST_E_* code; tpst_last_error()
+ *    gives the message.  No exceptions or aborts cross the ABI.  One call
+ *    in flight per context (internally serialised by a mutex).
+ */
+#ifndef TPST_H
+#define TPST_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TPST_OK 0
+#define TPST_E_ARG -1     /* bad length / null pointer / out-of-range value */
+#define TPST_E_NODEV -2   /* no HIP device */
+#define TPST_E_HIP -3     /* HIP runtime failure */
+#define TPST_E_STATE -4   /* e.g. no SRS loaded */
+#define TPST_E_VERIFY -5  /* verification failed */
+
+typedef struct tpst_ctx tpst_ctx;
+
+/* ---- context ---------------------------------------------------------- */
+int tpst_device_count(void);
+int tpst_create(int device, tpst_ctx** out);
+void tpst_destroy(tpst_ctx* ctx);
+const char* tpst_last_error(const tpst_ctx* ctx);
+/* hipStream_t of the context, for callers that order their own work */
+void* tpst_stream(tpst_ctx* ctx);
+int tpst_synchronize(tpst_ctx* ctx);
+
+/* ---- K2: variable-base MSM ---------------------------------------------
+ * sum_i scalars[i] * bases[i] over min(n_bases, n_scalars) terms.
+ * Replaces <G1 as VariableBaseMSM>::msm_unchecked (sqrt_pst.rs:198,
+ * mipp.rs:393 via multiexponentiation mipp.rs:385-394) and msm_bigint inside
+ * MultilinearPC::commit / open. */
+int tpst_g1_msm(tpst_ctx* ctx, const uint64_t* bases, size_t n_bases, const uint64_t* scalars,
+                size_t n_scalars, uint64_t* out);
+int tpst_g2_msm(tpst_ctx* ctx, const uint64_t* bases, size_t n_bases, const uint64_t* scalars,
+                size_t n_scalars, uint64_t* out);
+/* device-resident form: d_bases Montgomery affine (24 u32 each), d_scalars
+ * canonical Fr (8 u32 each), d_out one canonical affine G1 */
+int tpst_g1_msm_dev(tpst_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, void* d_out);
+
+/* ---- K4: multi-pairing ---------------------------------------------------
+ * prod_i e(g1[i], g2[i]) after final exponentiation (ark-ec
+ * Pairing::multi_pairing(...).0; sqrt_pst.rs:143, mipp.rs:397). */
+int tpst_multi_pairing(tpst_ctx* ctx, const uint64_t* g1, const uint64_t* g2, size_t n, uint64_t* out_gt);
+
+/* ---- utilities ----------------------------------------------------------- */
+/* out[i] = scalars[i] * G1 generator (affine, canonical); synthetic bases */
+int tpst_g1_mul_generator(tpst_ctx* ctx, const uint64_t* scalars, size_t n, uint64_t* out);
+int tpst_g2_mul_generator(tpst_ctx* ctx, const uint64_t* scalars, size_t n, uint64_t* out);
+/* device forms: d_out Montgomery (for _dev MSM bases) */
+int tpst_g1_mul_generator_dev(tpst_ctx* ctx, const void* d_scalars, size_t n, void* d_out_mont);
+
+/* Field microbenchmark (measured peak for the roofline's compute column):
+ * kind 0 = Fq Montgomery multiply, 1 = G1 XYZZ mixed add.  Runs `threads`
+ * threads x `iters` dependent ops each; returns kernel milliseconds. */
+int tpst_microbench(tpst_ctx* ctx, int kind, size_t threads, int iters, double* ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TPST_H */

@@ -1,0 +1,201 @@
+"""ctypes loader for the C++ CPU oracle (oracle/cpu/liborc.so).
+
+TEST INFRASTRUCTURE ONLY -- imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg; never by the product.  ``build()`` compiles it
+with the Makefile next to this file (g++ -fopenmp, no GPU).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liborc.so")
+ROOT = os.path.dirname(os.path.dirname(HERE))
+
+_u64p = C.POINTER(C.c_uint64)
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB
+
+
+def _p(a):
+    assert a.dtype == np.uint64 and a.flags["C_CONTIGUOUS"], (a.dtype, a.flags)
+    return a.ctypes.data_as(_u64p)
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB):
+        build()
+    lib = C.CDLL(LIB)
+    sz, vp, i = C.c_size_t, C.c_void_p, C.c_int
+    protos = {
+        "orc_threads": (i, []), "orc_set_threads": (None, [i]),
+        "orc_fr_stream": (C.c_uint64, [C.c_uint64, sz, C.c_uint64, _u64p]),
+        "orc_set_poseidon": (None, [_u64p, _u64p]),
+        "orc_g1_msm": (i, [_u64p, _u64p, sz, _u64p, i]),
+        "orc_g2_msm": (i, [_u64p, _u64p, sz, _u64p, i]),
+        "orc_g1_msm_batch": (i, [_u64p, sz, _u64p, sz, sz, sz, _u64p]),
+        "orc_multi_pairing": (i, [_u64p, _u64p, sz, _u64p]),
+        "orc_g1_mul_gen": (i, [_u64p, sz, _u64p]),
+        "orc_g2_mul_gen": (i, [_u64p, sz, _u64p]),
+        "orc_srs_setup": (vp, [i, C.c_uint64]),
+        "orc_srs_free": (None, [vp]),
+        "orc_srs_export_len": (sz, [vp]),
+        "orc_srs_export": (None, [vp, _u64p]),
+        "orc_pst_eval": (i, [_u64p, i, _u64p, _u64p]),
+        "orc_pst_commit": (i, [vp, _u64p, i, _u64p, _u64p]),
+        "orc_pst_open": (i, [vp, _u64p, i, _u64p, _u64p] + [_u64p] * 7),
+        "orc_pst_verify": (i, [vp, i] + [_u64p] * 10),
+    }
+    for name, (res, args) in protos.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    # Poseidon constants (parameters.rs FR table, canonical Fq limbs)
+    d = json.load(open(os.path.join(ROOT, "testudo_amd", "data", "poseidon_bls12_377.json")))
+    ark = np.zeros((39, 3, 6), dtype=np.uint64)
+    mds = np.zeros((3, 3, 6), dtype=np.uint64)
+    for r, row in enumerate(d["ark"]):
+        for k, v in enumerate(row):
+            ark[r, k] = [(int(v) >> (64 * q)) & (2**64 - 1) for q in range(6)]
+    for r, row in enumerate(d["mds"]):
+        for k, v in enumerate(row):
+            mds[r, k] = [(int(v) >> (64 * q)) & (2**64 - 1) for q in range(6)]
+    lib.orc_set_poseidon(_p(ark), _p(mds))
+    _lib = lib
+    return lib
+
+
+def fr_stream(seed, n, start=0):
+    lib = load()
+    out = np.zeros((n, 4), dtype=np.uint64)
+    nxt = lib.orc_fr_stream(seed, n, start, _p(out))
+    return out, nxt
+
+
+def g1_msm(bases, scalars, parallel=True):
+    lib = load()
+    bases = np.ascontiguousarray(bases, dtype=np.uint64)
+    scalars = np.ascontiguousarray(scalars, dtype=np.uint64)
+    n = min(len(bases), len(scalars))
+    out = np.zeros(12, dtype=np.uint64)
+    lib.orc_g1_msm(_p(bases), _p(scalars), n, _p(out), int(parallel))
+    return out
+
+
+def g2_msm(bases, scalars, parallel=True):
+    lib = load()
+    bases = np.ascontiguousarray(bases, dtype=np.uint64)
+    scalars = np.ascontiguousarray(scalars, dtype=np.uint64)
+    n = min(len(bases), len(scalars))
+    out = np.zeros(24, dtype=np.uint64)
+    lib.orc_g2_msm(_p(bases), _p(scalars), n, _p(out), int(parallel))
+    return out
+
+
+def g1_msm_batch(bases, scalars_flat, rows, row_stride, col_stride):
+    lib = load()
+    bases = np.ascontiguousarray(bases, dtype=np.uint64)
+    scalars_flat = np.ascontiguousarray(scalars_flat, dtype=np.uint64)
+    out = np.zeros((rows, 12), dtype=np.uint64)
+    lib.orc_g1_msm_batch(_p(bases), len(bases), _p(scalars_flat), rows, row_stride, col_stride, _p(out))
+    return out
+
+
+def multi_pairing(g1, g2):
+    lib = load()
+    g1 = np.ascontiguousarray(g1, dtype=np.uint64)
+    g2 = np.ascontiguousarray(g2, dtype=np.uint64)
+    out = np.zeros(72, dtype=np.uint64)
+    lib.orc_multi_pairing(_p(g1), _p(g2), len(g1), _p(out))
+    return out
+
+
+def g1_mul_gen(scalars):
+    lib = load()
+    scalars = np.ascontiguousarray(scalars, dtype=np.uint64)
+    out = np.zeros((len(scalars), 12), dtype=np.uint64)
+    lib.orc_g1_mul_gen(_p(scalars), len(scalars), _p(out))
+    return out
+
+
+def g2_mul_gen(scalars):
+    lib = load()
+    scalars = np.ascontiguousarray(scalars, dtype=np.uint64)
+    out = np.zeros((len(scalars), 24), dtype=np.uint64)
+    lib.orc_g2_mul_gen(_p(scalars), len(scalars), _p(out))
+    return out
+
+
+class SRS:
+    """MultilinearPC setup from the seeded trapdoor; ``export()`` gives the
+    flat layout g | h | (powers_of_g[i] | powers_of_h[i])_i | g_mask | h_mask."""
+
+    def __init__(self, nv, seed):
+        self.lib = load()
+        self.nv = nv
+        self.h = self.lib.orc_srs_setup(nv, seed)
+
+    def export(self):
+        n = self.lib.orc_srs_export_len(self.h)
+        out = np.zeros(n, dtype=np.uint64)
+        self.lib.orc_srs_export(self.h, _p(out))
+        return out
+
+    def __del__(self):
+        try:
+            self.lib.orc_srs_free(self.h)
+        except Exception:
+            pass
+
+
+def pst_eval(Z, n, point):
+    lib = load()
+    out = np.zeros(4, dtype=np.uint64)
+    lib.orc_pst_eval(_p(np.ascontiguousarray(Z)), n, _p(np.ascontiguousarray(point)), _p(out))
+    return out
+
+
+def pst_commit(srs, Z, n):
+    lib = load()
+    m_col = n // 2
+    comms = np.zeros(((1 << m_col), 12), dtype=np.uint64)
+    T = np.zeros(72, dtype=np.uint64)
+    rc = lib.orc_pst_commit(srs.h, _p(np.ascontiguousarray(Z)), n, _p(comms), _p(T))
+    assert rc == 0
+    return comms, T
+
+
+def pst_open(srs, Z, n, point, comms):
+    lib = load()
+    m_col, m_row = n // 2, n - n // 2
+    out = dict(
+        U=np.zeros(12, dtype=np.uint64), pst_proof=np.zeros((m_row, 24), dtype=np.uint64),
+        comms_t=np.zeros((m_col, 2, 72), dtype=np.uint64), comms_u=np.zeros((m_col, 2, 12), dtype=np.uint64),
+        final_a=np.zeros(12, dtype=np.uint64), final_h=np.zeros(24, dtype=np.uint64),
+        pst_proof_h=np.zeros((m_col, 12), dtype=np.uint64))
+    rc = lib.orc_pst_open(srs.h, _p(np.ascontiguousarray(Z)), n, _p(np.ascontiguousarray(point)),
+                          _p(np.ascontiguousarray(comms)), *[_p(out[k]) for k in
+                                                             ("U", "pst_proof", "comms_t", "comms_u", "final_a",
+                                                              "final_h", "pst_proof_h")])
+    assert rc == 0, rc
+    return out
+
+
+def pst_verify(srs, n, point, v, proof, T):
+    lib = load()
+    a = [np.ascontiguousarray(x, dtype=np.uint64) for x in
+         (point, v, proof["U"], proof["pst_proof"], proof["comms_t"], proof["comms_u"], proof["final_a"],
+          proof["final_h"], proof["pst_proof_h"], T)]
+    return lib.orc_pst_verify(srs.h, n, *[_p(x) for x in a]) == 1

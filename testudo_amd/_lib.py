@@ -1,0 +1,57 @@
+"""ctypes binding of libtpst.so (include/tpst.h).
+
+The library is built in-tree by testudo_amd/build.py.  There is no CPU
+fallback: if the shared object is missing or cannot be loaded, importing the
+product path raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtpst.so")
+
+_u64p = C.POINTER(C.c_uint64)
+_vp = C.c_void_p
+_sz = C.c_size_t
+
+# (name, restype, argtypes) -- mirrors include/tpst.h
+PROTOTYPES = [
+    ("tpst_device_count", C.c_int, []),
+    ("tpst_create", C.c_int, [C.c_int, C.POINTER(_vp)]),
+    ("tpst_destroy", None, [_vp]),
+    ("tpst_last_error", C.c_char_p, [_vp]),
+    ("tpst_stream", _vp, [_vp]),
+    ("tpst_synchronize", C.c_int, [_vp]),
+    ("tpst_g1_msm", C.c_int, [_vp, _u64p, _sz, _u64p, _sz, _u64p]),
+    ("tpst_g2_msm", C.c_int, [_vp, _u64p, _sz, _u64p, _sz, _u64p]),
+    ("tpst_g1_msm_dev", C.c_int, [_vp, _vp, _vp, _sz, _vp]),
+    ("tpst_multi_pairing", C.c_int, [_vp, _u64p, _u64p, _sz, _u64p]),
+    ("tpst_g1_mul_generator", C.c_int, [_vp, _u64p, _sz, _u64p]),
+    ("tpst_g2_mul_generator", C.c_int, [_vp, _u64p, _sz, _u64p]),
+    ("tpst_g1_mul_generator_dev", C.c_int, [_vp, _vp, _sz, _vp]),
+    ("tpst_microbench", C.c_int, [_vp, C.c_int, _sz, C.c_int, C.POINTER(C.c_double)]),
+]
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libtpst.so and bind every prototype; raises if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libtpst.so not built (%s); run testudo_amd/build.py" % LIB_PATH)
+    lib = C.CDLL(LIB_PATH)
+    for name, res, args in PROTOTYPES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return [p[0] for p in PROTOTYPES]

@@ -1,0 +1,258 @@
+// C-ABI entry points (include/tpst.h): context management, device
+// primitives (MSM, multi-pairing, generator multiples) and the field
+// microbenchmark.  The sqrt-PST protocol entry points live in pst_api.hip.
+#include <cstring>
+#include "../../include/tpst.h"
+#include "ctx.h"
+#include "device_util.h"
+
+using namespace tpst;
+
+namespace tpst {
+
+int fail(tpst_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+int hip_fail(tpst_ctx* ctx, hipError_t e, const char* where) {
+  return fail(ctx, TPST_E_HIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+}  // namespace tpst
+
+static inline unsigned grid_for(size_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
+
+extern "C" int tpst_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+extern "C" int tpst_create(int device, tpst_ctx** out) {
+  if (!out) return TPST_E_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return TPST_E_NODEV;
+  if (device < 0 || device >= n) return TPST_E_ARG;
+  if (hipSetDevice(device) != hipSuccess) return TPST_E_HIP;
+  tpst_ctx* c = new tpst_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return TPST_E_HIP;
+  }
+  *out = c;
+  return TPST_OK;
+}
+
+extern "C" void tpst_destroy(tpst_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  ctx->arena.release();
+  ctx->io.release();
+  ctx->arena2.release();
+  tpst_release_pst_state(ctx);
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+extern "C" const char* tpst_last_error(const tpst_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+extern "C" void* tpst_stream(tpst_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+extern "C" int tpst_synchronize(tpst_ctx* ctx) {
+  if (!ctx) return TPST_E_ARG;
+  TPST_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return TPST_OK;
+}
+
+// ---------------------------------------------------------------- MSM ----
+template <class F>
+static int msm_host(tpst_ctx* ctx, const uint64_t* bases, size_t nb, const uint64_t* scalars, size_t ns,
+                    uint64_t* out) {
+  if (!ctx || !out || (nb && !bases) || (ns && !scalars)) return fail(ctx, TPST_E_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  const size_t n = nb < ns ? nb : ns;  // msm_unchecked truncates
+  constexpr size_t PW = 2 * Words<F>::n;  // u32 per affine point
+  ctx->io.reset();
+  TPST_HIP(ctx, ctx->io.reserve(Arena::need(n * PW, 4) * 2 + Arena::need(n * 8, 4) + 4096 +
+                                Arena::need(1, sizeof(Xyzz<F>)) + Arena::need(PW, 4)));
+  uint32_t* d_b = ctx->io.take<uint32_t>(n * PW);
+  uint32_t* d_bm = ctx->io.take<uint32_t>(n * PW);
+  uint32_t* d_s = ctx->io.take<uint32_t>(n * 8);
+  Xyzz<F>* d_r = ctx->io.take<Xyzz<F>>(1);
+  uint32_t* d_o = ctx->io.take<uint32_t>(PW);
+  hipStream_t s = ctx->stream;
+  if (n) {
+    TPST_HIP(ctx, hipMemcpyAsync(d_b, bases, n * PW * 4, hipMemcpyHostToDevice, s));
+    TPST_HIP(ctx, hipMemcpyAsync(d_s, scalars, n * 32, hipMemcpyHostToDevice, s));
+    TPST_HIP(ctx, points_to_mont<F>(s, d_b, d_bm, n));
+  }
+  TPST_HIP(ctx, msm_var<F>(ctx->arena, s, d_bm, d_s, n, d_r));
+  TPST_HIP(ctx, xyzz_to_affine_canonical<F>(s, d_r, d_o, 1));
+  TPST_HIP(ctx, hipMemcpyAsync(out, d_o, PW * 4, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipStreamSynchronize(s));
+  return TPST_OK;
+}
+
+extern "C" int tpst_g1_msm(tpst_ctx* ctx, const uint64_t* bases, size_t n_bases, const uint64_t* scalars,
+                           size_t n_scalars, uint64_t* out) {
+  return msm_host<Fq>(ctx, bases, n_bases, scalars, n_scalars, out);
+}
+
+extern "C" int tpst_g2_msm(tpst_ctx* ctx, const uint64_t* bases, size_t n_bases, const uint64_t* scalars,
+                           size_t n_scalars, uint64_t* out) {
+  return msm_host<Fq2>(ctx, bases, n_bases, scalars, n_scalars, out);
+}
+
+extern "C" int tpst_g1_msm_dev(tpst_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, void* d_out) {
+  if (!ctx || !d_out || (n && (!d_bases || !d_scalars))) return fail(ctx, TPST_E_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  ctx->io.reset();
+  TPST_HIP(ctx, ctx->io.reserve(Arena::need(1, sizeof(Xyzz<Fq>)) + 256));
+  Xyzz<Fq>* d_r = ctx->io.take<Xyzz<Fq>>(1);
+  TPST_HIP(ctx, msm_var<Fq>(ctx->arena, ctx->stream, (const uint32_t*)d_bases, (const uint32_t*)d_scalars, n, d_r));
+  TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(ctx->stream, d_r, (uint32_t*)d_out, 1));
+  return TPST_OK;
+}
+
+// ------------------------------------------------------------ pairing ----
+extern "C" int tpst_multi_pairing(tpst_ctx* ctx, const uint64_t* g1, const uint64_t* g2, size_t n,
+                                  uint64_t* out_gt) {
+  if (!ctx || !out_gt || (n && (!g1 || !g2))) return fail(ctx, TPST_E_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  ctx->io.reset();
+  TPST_HIP(ctx, ctx->io.reserve(Arena::need(n * 24, 4) * 2 + Arena::need(n * 48, 4) * 2 +
+                                Arena::need(1, sizeof(Fq12)) + Arena::need(144, 4) + 4096));
+  uint32_t* d1 = ctx->io.take<uint32_t>(n * 24);
+  uint32_t* d1m = ctx->io.take<uint32_t>(n * 24);
+  uint32_t* d2 = ctx->io.take<uint32_t>(n * 48);
+  uint32_t* d2m = ctx->io.take<uint32_t>(n * 48);
+  Fq12* d_f = ctx->io.take<Fq12>(1);
+  uint32_t* d_o = ctx->io.take<uint32_t>(144);
+  if (n) {
+    TPST_HIP(ctx, hipMemcpyAsync(d1, g1, n * 96, hipMemcpyHostToDevice, s));
+    TPST_HIP(ctx, hipMemcpyAsync(d2, g2, n * 192, hipMemcpyHostToDevice, s));
+    TPST_HIP(ctx, points_to_mont<Fq>(s, d1, d1m, n));
+    TPST_HIP(ctx, points_to_mont<Fq2>(s, d2, d2m, n));
+  }
+  TPST_HIP(ctx, multi_pairing(ctx->arena, s, d1m, d2m, 1, n, d_f));
+  TPST_HIP(ctx, fq12_from_mont(s, d_f, d_o, 1));
+  TPST_HIP(ctx, hipMemcpyAsync(out_gt, d_o, 576, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipStreamSynchronize(s));
+  return TPST_OK;
+}
+
+// ------------------------------------------------- generator multiples ----
+template <class F>
+__global__ void k_mul_gen(const uint32_t* __restrict__ scalars, size_t n, uint32_t* __restrict__ out, int canonical) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Affine<F> g;
+  if constexpr (sizeof(F) == sizeof(Fq)) {
+    g = {Fq::from_limbs(params::G1_GEN_X), Fq::from_limbs(params::G1_GEN_Y)};
+  } else {
+    g = {fq2_const(params::G2_GEN_X), fq2_const(params::G2_GEN_Y)};
+  }
+  uint32_t k[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) k[j] = scalars[8 * i + j];
+  Affine<F> a = to_affine(scalar_mul(g, k, 253));
+  if (canonical) {
+    Fq* c = reinterpret_cast<Fq*>(&a);
+#pragma unroll
+    for (int j = 0; j < (int)(sizeof(Affine<F>) / sizeof(Fq)); j++) c[j] = from_mont(c[j]);
+  }
+  store_affine(out, i, a);
+}
+
+template <class F>
+static int mul_gen_host(tpst_ctx* ctx, const uint64_t* scalars, size_t n, uint64_t* out) {
+  if (!ctx || (n && (!scalars || !out))) return fail(ctx, TPST_E_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  if (!n) return TPST_OK;
+  constexpr size_t PW = 2 * Words<F>::n;
+  hipStream_t s = ctx->stream;
+  ctx->io.reset();
+  TPST_HIP(ctx, ctx->io.reserve(Arena::need(n * 8, 4) + Arena::need(n * PW, 4) + 512));
+  uint32_t* d_s = ctx->io.take<uint32_t>(n * 8);
+  uint32_t* d_o = ctx->io.take<uint32_t>(n * PW);
+  TPST_HIP(ctx, hipMemcpyAsync(d_s, scalars, n * 32, hipMemcpyHostToDevice, s));
+  k_mul_gen<F><<<grid_for(n, 64), 64, 0, s>>>(d_s, n, d_o, 1);
+  TPST_HIP(ctx, hipGetLastError());
+  TPST_HIP(ctx, hipMemcpyAsync(out, d_o, n * PW * 4, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipStreamSynchronize(s));
+  return TPST_OK;
+}
+
+extern "C" int tpst_g1_mul_generator(tpst_ctx* ctx, const uint64_t* scalars, size_t n, uint64_t* out) {
+  return mul_gen_host<Fq>(ctx, scalars, n, out);
+}
+
+extern "C" int tpst_g2_mul_generator(tpst_ctx* ctx, const uint64_t* scalars, size_t n, uint64_t* out) {
+  return mul_gen_host<Fq2>(ctx, scalars, n, out);
+}
+
+extern "C" int tpst_g1_mul_generator_dev(tpst_ctx* ctx, const void* d_scalars, size_t n, void* d_out_mont) {
+  if (!ctx || (n && (!d_scalars || !d_out_mont))) return fail(ctx, TPST_E_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  if (!n) return TPST_OK;
+  k_mul_gen<Fq><<<grid_for(n, 64), 64, 0, ctx->stream>>>((const uint32_t*)d_scalars, n, (uint32_t*)d_out_mont, 0);
+  TPST_HIP(ctx, hipGetLastError());
+  return TPST_OK;
+}
+
+// ------------------------------------------------------ microbenchmark ----
+__global__ void k_mb_fqmul(int iters, uint32_t* out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  Fq a = Fq::one(), b = Fq::one();
+  a.v[0] ^= t;
+  b.v[1] ^= t * 7u + 1;
+  for (int i = 0; i < iters; i++) a = mul(a, b);
+  store_f<Fq>(out + 12 * (size_t)t, a);
+}
+
+__global__ void k_mb_madd(int iters, uint32_t* out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  G1A g = {Fq::from_limbs(params::G1_GEN_X), Fq::from_limbs(params::G1_GEN_Y)};
+  Xyzz<Fq> acc = dbl_affine(g);
+  acc.X.v[0] ^= (t & 1);  // keep threads independent of each other's values
+  for (int i = 0; i < iters; i++) acc = add_affine(acc, g);
+  store_f<Fq>(out + 12 * (size_t)t, acc.X);
+}
+
+extern "C" int tpst_microbench(tpst_ctx* ctx, int kind, size_t threads, int iters, double* ms) {
+  if (!ctx || !ms || threads == 0 || iters <= 0) return fail(ctx, TPST_E_ARG, "bad argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  const unsigned bs = threads < 256 ? (unsigned)threads : 256u;
+  const unsigned grid = grid_for(threads, bs);
+  ctx->io.reset();
+  TPST_HIP(ctx, ctx->io.reserve(Arena::need((size_t)grid * bs * 12, 4)));
+  uint32_t* d = ctx->io.take<uint32_t>((size_t)grid * bs * 12);
+  hipEvent_t e0, e1;
+  TPST_HIP(ctx, hipEventCreate(&e0));
+  TPST_HIP(ctx, hipEventCreate(&e1));
+  TPST_HIP(ctx, hipEventRecord(e0, ctx->stream));
+  if (kind == 0)
+    k_mb_fqmul<<<grid, bs, 0, ctx->stream>>>(iters, d);
+  else
+    k_mb_madd<<<grid, bs, 0, ctx->stream>>>(iters, d);
+  TPST_HIP(ctx, hipGetLastError());
+  TPST_HIP(ctx, hipEventRecord(e1, ctx->stream));
+  TPST_HIP(ctx, hipEventSynchronize(e1));
+  float f = 0;
+  TPST_HIP(ctx, hipEventElapsedTime(&f, e0, e1));
+  *ms = f;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return TPST_OK;
+}

@@ -1,0 +1,33 @@
+// Internal state behind the opaque tpst_ctx handle.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <mutex>
+#include <string>
+#include "msm.h"
+#include "pairing_kernels.h"
+
+struct tpst_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  std::string err;
+  tpst::Arena arena;   // kernel scratch (reset per primitive)
+  tpst::Arena io;      // staging for host-pointer entry points
+  tpst::Arena arena2;  // scratch for nested primitives (open / MIPP)
+};
+
+void tpst_release_pst_state(tpst_ctx* ctx);
+
+namespace tpst {
+
+// record an error message and return code
+int fail(tpst_ctx* ctx, int code, const std::string& msg);
+int hip_fail(tpst_ctx* ctx, hipError_t e, const char* where);
+
+}  // namespace tpst
+
+#define TPST_HIP(ctx, x)                                            \
+  do {                                                              \
+    hipError_t _e = (x);                                            \
+    if (_e != hipSuccess) return tpst::hip_fail((ctx), _e, #x);     \
+  } while (0)

@@ -1,0 +1,424 @@
+// BLS12-377 field tower for CDNA4 (gfx950) and host.
+//
+//   Fq  : 377-bit prime field, 12 x u32 limbs, Montgomery R = 2^384
+//   Fr  : 253-bit scalar field,  8 x u32 limbs, Montgomery R = 2^256
+//   Fq2 = Fq[u]/(u^2 + 5), Fq6 = Fq2[v]/(v^3 - u), Fq12 = Fq6[w]/(w^2 - v)
+//
+// The tower and its non-residues are ark-bls12-377 0.4's;
+// the byte layout of an element (12 u32 = 6 u64 little-endian Montgomery
+// limbs) is identical to arkworks' in-memory Fp384, so device buffers and
+// host buffers are interchangeable.
+//
+// Multiplication is the "no-carry" CIOS Montgomery product: both moduli have
+// a top limb < 2^31 - 1, so the running sum never needs an extra word.  Each
+// limb product is one v_mad_u64_u32 on gfx950.  All values are kept fully
+// reduced (< modulus), so equality is limb equality.
+#pragma once
+#include <stdint.h>
+#include "bls12_377_params.h"
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define TPST_HD __host__ __device__ __forceinline__
+#define TPST_NI __host__ __device__ inline __attribute__((noinline))
+#else
+#define TPST_HD inline
+#define TPST_NI inline __attribute__((noinline))
+#endif
+
+namespace tpst {
+
+struct FqCfg {
+  static constexpr int N = 12;
+  static TPST_HD uint32_t p(int i) { return params::FQ_P[i]; }
+  static TPST_HD uint32_t one(int i) { return params::FQ_ONE[i]; }
+  static TPST_HD uint32_t r2(int i) { return params::FQ_R2[i]; }
+  static TPST_HD uint32_t pm2(int i) { return params::FQ_PM2[i]; }
+  static constexpr uint32_t INV = params::FQ_INV;
+};
+
+struct FrCfg {
+  static constexpr int N = 8;
+  static TPST_HD uint32_t p(int i) { return params::FR_P[i]; }
+  static TPST_HD uint32_t one(int i) { return params::FR_ONE[i]; }
+  static TPST_HD uint32_t r2(int i) { return params::FR_R2[i]; }
+  static TPST_HD uint32_t pm2(int i) { return params::FR_PM2[i]; }
+  static constexpr uint32_t INV = params::FR_INV;
+};
+
+template <class C>
+struct Fp {
+  uint32_t v[C::N];
+  static TPST_HD Fp zero() {
+    Fp r;
+#pragma unroll
+    for (int i = 0; i < C::N; i++) r.v[i] = 0;
+    return r;
+  }
+  static TPST_HD Fp one() {
+    Fp r;
+#pragma unroll
+    for (int i = 0; i < C::N; i++) r.v[i] = C::one(i);
+    return r;
+  }
+  static TPST_HD Fp from_limbs(const uint32_t* l) {
+    Fp r;
+#pragma unroll
+    for (int i = 0; i < C::N; i++) r.v[i] = l[i];
+    return r;
+  }
+};
+
+using Fq = Fp<FqCfg>;
+using Fr = Fp<FrCfg>;
+
+// ------------------------------------------------------------ base field --
+template <class C>
+TPST_HD bool is_zero(const Fp<C>& a) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < C::N; i++) acc |= a.v[i];
+  return acc == 0;
+}
+
+template <class C>
+TPST_HD bool eq(const Fp<C>& a, const Fp<C>& b) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < C::N; i++) acc |= a.v[i] ^ b.v[i];
+  return acc == 0;
+}
+
+// r = t - p if t >= p else t   (t < 2p)
+template <class C>
+TPST_HD void reduce_once(Fp<C>& t) {
+  uint32_t s[C::N];
+  int64_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < C::N; i++) {
+    int64_t d = (int64_t)t.v[i] - C::p(i) + borrow;
+    s[i] = (uint32_t)d;
+    borrow = d >> 32;  // 0 or -1
+  }
+  // borrow == 0  <=>  t >= p  -> take s
+  const bool take = (borrow == 0);
+#pragma unroll
+  for (int i = 0; i < C::N; i++) t.v[i] = take ? s[i] : t.v[i];
+}
+
+template <class C>
+TPST_HD Fp<C> add(const Fp<C>& a, const Fp<C>& b) {
+  Fp<C> r;
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < C::N; i++) {
+    c += (uint64_t)a.v[i] + b.v[i];
+    r.v[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  reduce_once(r);
+  return r;
+}
+
+template <class C>
+TPST_HD Fp<C> dbl(const Fp<C>& a) { return add(a, a); }
+
+template <class C>
+TPST_HD Fp<C> sub(const Fp<C>& a, const Fp<C>& b) {
+  Fp<C> r;
+  int64_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < C::N; i++) {
+    int64_t d = (int64_t)a.v[i] - b.v[i] + borrow;
+    r.v[i] = (uint32_t)d;
+    borrow = d >> 32;
+  }
+  // if negative add p back
+  const uint32_t mask = (uint32_t)borrow;  // 0 or 0xffffffff
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < C::N; i++) {
+    c += (uint64_t)r.v[i] + (C::p(i) & mask);
+    r.v[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  return r;
+}
+
+template <class C>
+TPST_HD Fp<C> neg(const Fp<C>& a) { return sub(Fp<C>::zero(), a); }
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// acc(64) + hi(32) += a * b, using v_mad_u64_u32's carry-out into an SGPR
+// pair and one v_addc: 2 VALU ops per limb product, no zero-extension moves.
+__device__ __forceinline__ void mac_vv(uint64_t& acc, uint32_t& hi, uint32_t a, uint32_t b) {
+  uint64_t c;
+  asm("v_mad_u64_u32 %0, %2, %3, %4, %0\n\tv_addc_co_u32_e64 %1, %2, 0, %1, %2"
+      : "+v"(acc), "+v"(hi), "=&s"(c)
+      : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mac_vs(uint64_t& acc, uint32_t& hi, uint32_t a, uint32_t b) {
+  uint64_t c;
+  asm("v_mad_u64_u32 %0, %2, %3, %4, %0\n\tv_addc_co_u32_e64 %1, %2, 0, %1, %2"
+      : "+v"(acc), "+v"(hi), "=&s"(c)
+      : "v"(a), "s"(b));
+}
+
+// Montgomery product a*b*R^-1 mod p, finely-integrated product scanning
+// (column-wise; the reduction word m_k is formed as column k completes).
+template <class C>
+__device__ __forceinline__ Fp<C> mul(const Fp<C>& a, const Fp<C>& b) {
+  constexpr int N = C::N;
+  uint32_t m[N], t[N];
+  uint64_t acc = 0;
+  uint32_t hi = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; k++) {
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < N) mac_vv(acc, hi, a.v[i], b.v[j]);
+    }
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      const int j = k - i;
+      if (i < k && j >= 1 && j < N) mac_vs(acc, hi, m[i], C::p(j));
+    }
+    if (k < N) {
+      m[k] = (uint32_t)acc * C::INV;
+      mac_vs(acc, hi, m[k], C::p(0));
+    } else {
+      t[k - N] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+  t[N - 1] = (uint32_t)acc;
+  Fp<C> r;
+#pragma unroll
+  for (int j = 0; j < N; j++) r.v[j] = t[j];
+  reduce_once(r);
+  return r;
+}
+#else
+// Montgomery product a*b*R^-1 mod p, no-carry CIOS (host build).
+template <class C>
+TPST_HD Fp<C> mul(const Fp<C>& a, const Fp<C>& b) {
+  constexpr int N = C::N;
+  uint32_t t[N];
+  for (int j = 0; j < N; j++) t[j] = 0;
+  for (int i = 0; i < N; i++) {
+    const uint32_t bi = b.v[i];
+    uint64_t s = (uint64_t)a.v[0] * bi + t[0];
+    uint32_t A = (uint32_t)(s >> 32);
+    const uint32_t t0 = (uint32_t)s;
+    const uint32_t m = t0 * C::INV;
+    uint64_t s2 = (uint64_t)m * C::p(0) + t0;
+    uint32_t Cc = (uint32_t)(s2 >> 32);
+    for (int j = 1; j < N; j++) {
+      s = (uint64_t)a.v[j] * bi + t[j] + A;
+      A = (uint32_t)(s >> 32);
+      s2 = (uint64_t)m * C::p(j) + (uint32_t)s + Cc;
+      Cc = (uint32_t)(s2 >> 32);
+      t[j - 1] = (uint32_t)s2;
+    }
+    t[N - 1] = Cc + A;
+  }
+  Fp<C> r;
+  for (int j = 0; j < N; j++) r.v[j] = t[j];
+  reduce_once(r);
+  return r;
+}
+#endif
+
+template <class C>
+TPST_HD Fp<C> sqr(const Fp<C>& a) { return mul(a, a); }
+
+template <class C>
+TPST_HD Fp<C> to_mont(const Fp<C>& a) {  // canonical -> Montgomery
+  Fp<C> r2;
+#pragma unroll
+  for (int i = 0; i < C::N; i++) r2.v[i] = C::r2(i);
+  return mul(a, r2);
+}
+
+template <class C>
+TPST_HD Fp<C> from_mont(const Fp<C>& a) {  // Montgomery -> canonical
+  Fp<C> one = Fp<C>::zero();
+  one.v[0] = 1;
+  return mul(a, one);
+}
+
+// a^(p-2) (Fermat); a == 0 -> 0
+template <class C>
+TPST_NI Fp<C> inv(const Fp<C>& a) {
+  Fp<C> r = Fp<C>::one();
+  for (int i = C::N - 1; i >= 0; i--) {
+    const uint32_t e = C::pm2(i);
+    for (int b = 31; b >= 0; b--) {
+      r = sqr(r);
+      if ((e >> b) & 1) r = mul(r, a);
+    }
+  }
+  return r;
+}
+
+// small constant multiples
+template <class C>
+TPST_HD Fp<C> mul3(const Fp<C>& a) { return add(dbl(a), a); }
+
+// ------------------------------------------------------------------ Fq2 ---
+struct Fq2 {
+  Fq c0, c1;
+  static TPST_HD Fq2 zero() { return {Fq::zero(), Fq::zero()}; }
+  static TPST_HD Fq2 one() { return {Fq::one(), Fq::zero()}; }
+};
+
+TPST_HD bool is_zero(const Fq2& a) { return is_zero(a.c0) && is_zero(a.c1); }
+TPST_HD bool eq(const Fq2& a, const Fq2& b) { return eq(a.c0, b.c0) && eq(a.c1, b.c1); }
+TPST_HD Fq2 add(const Fq2& a, const Fq2& b) { return {add(a.c0, b.c0), add(a.c1, b.c1)}; }
+TPST_HD Fq2 sub(const Fq2& a, const Fq2& b) { return {sub(a.c0, b.c0), sub(a.c1, b.c1)}; }
+TPST_HD Fq2 dbl(const Fq2& a) { return {dbl(a.c0), dbl(a.c1)}; }
+TPST_HD Fq2 neg(const Fq2& a) { return {neg(a.c0), neg(a.c1)}; }
+TPST_HD Fq2 mul3(const Fq2& a) { return {mul3(a.c0), mul3(a.c1)}; }
+TPST_HD Fq mul5(const Fq& a) { return add(dbl(dbl(a)), a); }
+TPST_HD Fq2 conj(const Fq2& a) { return {a.c0, neg(a.c1)}; }
+
+TPST_HD Fq2 mul(const Fq2& a, const Fq2& b) {
+  const Fq v0 = mul(a.c0, b.c0);
+  const Fq v1 = mul(a.c1, b.c1);
+  const Fq s = mul(add(a.c0, a.c1), add(b.c0, b.c1));
+  return {sub(v0, mul5(v1)), sub(sub(s, v0), v1)};
+}
+
+TPST_HD Fq2 sqr(const Fq2& a) {
+  // (a0 + a1 u)^2 = a0^2 - 5 a1^2 + 2 a0 a1 u
+  const Fq v0 = mul(a.c0, a.c1);
+  // (a0 + a1)(a0 - 5 a1) = a0^2 - 5a1^2 - 4 a0 a1
+  const Fq t = mul(add(a.c0, a.c1), sub(a.c0, mul5(a.c1)));
+  const Fq c0 = add(t, dbl(dbl(v0)));
+  return {c0, dbl(v0)};
+}
+
+TPST_HD Fq2 mul_fq(const Fq2& a, const Fq& s) { return {mul(a.c0, s), mul(a.c1, s)}; }
+
+TPST_NI Fq2 inv(const Fq2& a) {
+  const Fq n = add(sqr(a.c0), mul5(sqr(a.c1)));
+  const Fq ni = inv(n);
+  return {mul(a.c0, ni), neg(mul(a.c1, ni))};
+}
+
+// times the Fq6 non-residue u:  (x0 + x1 u) u = -5 x1 + x0 u
+TPST_HD Fq2 mul_by_u(const Fq2& a) { return {neg(mul5(a.c1)), a.c0}; }
+
+TPST_HD Fq2 fq2_const(const uint32_t (*c)[12]) {
+  return {Fq::from_limbs(c[0]), Fq::from_limbs(c[1])};
+}
+
+// ------------------------------------------------------------------ Fq6 ---
+struct Fq6 {
+  Fq2 c0, c1, c2;
+  static TPST_HD Fq6 zero() { return {Fq2::zero(), Fq2::zero(), Fq2::zero()}; }
+  static TPST_HD Fq6 one() { return {Fq2::one(), Fq2::zero(), Fq2::zero()}; }
+};
+
+TPST_HD Fq6 add(const Fq6& a, const Fq6& b) { return {add(a.c0, b.c0), add(a.c1, b.c1), add(a.c2, b.c2)}; }
+TPST_HD Fq6 sub(const Fq6& a, const Fq6& b) { return {sub(a.c0, b.c0), sub(a.c1, b.c1), sub(a.c2, b.c2)}; }
+TPST_HD Fq6 neg(const Fq6& a) { return {neg(a.c0), neg(a.c1), neg(a.c2)}; }
+TPST_HD Fq6 dbl(const Fq6& a) { return {dbl(a.c0), dbl(a.c1), dbl(a.c2)}; }
+TPST_HD bool eq(const Fq6& a, const Fq6& b) { return eq(a.c0, b.c0) && eq(a.c1, b.c1) && eq(a.c2, b.c2); }
+TPST_HD bool is_zero(const Fq6& a) { return is_zero(a.c0) && is_zero(a.c1) && is_zero(a.c2); }
+
+TPST_NI Fq6 mul(const Fq6& a, const Fq6& b) {
+  const Fq2 v0 = mul(a.c0, b.c0);
+  const Fq2 v1 = mul(a.c1, b.c1);
+  const Fq2 v2 = mul(a.c2, b.c2);
+  const Fq2 c0 = add(mul_by_u(sub(sub(mul(add(a.c1, a.c2), add(b.c1, b.c2)), v1), v2)), v0);
+  const Fq2 c1 = add(sub(sub(mul(add(a.c0, a.c1), add(b.c0, b.c1)), v0), v1), mul_by_u(v2));
+  const Fq2 c2 = add(sub(sub(mul(add(a.c0, a.c2), add(b.c0, b.c2)), v0), v2), v1);
+  return {c0, c1, c2};
+}
+
+TPST_HD Fq6 sqr(const Fq6& a) { return mul(a, a); }
+
+// times the Fq12 non-residue v: (x0 + x1 v + x2 v^2) v = u x2 + x0 v + x1 v^2
+TPST_HD Fq6 mul_by_v(const Fq6& a) { return {mul_by_u(a.c2), a.c0, a.c1}; }
+
+// (a0 + a1 v + a2 v^2)(b0 + b1 v)      ark Fp6::mul_by_01
+TPST_NI Fq6 mul_by_01(const Fq6& a, const Fq2& b0, const Fq2& b1) {
+  const Fq2 v0 = mul(a.c0, b0);
+  const Fq2 v1 = mul(a.c1, b1);
+  const Fq2 t1 = add(mul_by_u(sub(mul(add(a.c1, a.c2), b1), v1)), v0);
+  const Fq2 t3 = add(sub(mul(add(a.c0, a.c2), b0), v0), v1);
+  const Fq2 t2 = sub(sub(mul(add(b0, b1), add(a.c0, a.c1)), v0), v1);
+  return {t1, t2, t3};
+}
+
+TPST_NI Fq6 inv(const Fq6& a) {
+  // standard: c0 = a0^2 - u a1 a2, c1 = u a2^2 - a0 a1, c2 = a1^2 - a0 a2
+  const Fq2 c0 = sub(sqr(a.c0), mul_by_u(mul(a.c1, a.c2)));
+  const Fq2 c1 = sub(mul_by_u(sqr(a.c2)), mul(a.c0, a.c1));
+  const Fq2 c2 = sub(sqr(a.c1), mul(a.c0, a.c2));
+  const Fq2 t = add(mul(a.c0, c0), mul_by_u(add(mul(a.c2, c1), mul(a.c1, c2))));
+  const Fq2 ti = inv(t);
+  return {mul(c0, ti), mul(c1, ti), mul(c2, ti)};
+}
+
+// ----------------------------------------------------------------- Fq12 ---
+struct Fq12 {
+  Fq6 c0, c1;
+  static TPST_HD Fq12 one() { return {Fq6::one(), Fq6::zero()}; }
+};
+
+TPST_HD bool eq(const Fq12& a, const Fq12& b) { return eq(a.c0, b.c0) && eq(a.c1, b.c1); }
+
+TPST_NI Fq12 mul(const Fq12& a, const Fq12& b) {
+  const Fq6 v0 = mul(a.c0, b.c0);
+  const Fq6 v1 = mul(a.c1, b.c1);
+  const Fq6 c1 = sub(sub(mul(add(a.c0, a.c1), add(b.c0, b.c1)), v0), v1);
+  return {add(v0, mul_by_v(v1)), c1};
+}
+
+TPST_NI Fq12 sqr(const Fq12& a) {
+  // complex squaring
+  const Fq6 ab = mul(a.c0, a.c1);
+  const Fq6 t = mul(add(a.c0, a.c1), add(a.c0, mul_by_v(a.c1)));
+  const Fq6 c0 = sub(sub(t, ab), mul_by_v(ab));
+  return {c0, dbl(ab)};
+}
+
+TPST_HD Fq12 conj(const Fq12& a) { return {a.c0, neg(a.c1)}; }
+
+TPST_NI Fq12 inv(const Fq12& a) {
+  const Fq6 t = sub(sqr(a.c0), mul_by_v(sqr(a.c1)));
+  const Fq6 ti = inv(t);
+  return {mul(a.c0, ti), neg(mul(a.c1, ti))};
+}
+
+// f *= (c0 + c3 w + c4 v w)                 ark Fp12::mul_by_034
+TPST_NI Fq12 mul_by_034(const Fq12& f, const Fq2& c0, const Fq2& c3, const Fq2& c4) {
+  const Fq6 a = {mul(f.c0.c0, c0), mul(f.c0.c1, c0), mul(f.c0.c2, c0)};
+  const Fq6 b = mul_by_01(f.c1, c3, c4);
+  const Fq6 e = mul_by_01(add(f.c0, f.c1), add(c0, c3), c4);
+  return {add(a, mul_by_v(b)), sub(e, add(a, b))};
+}
+
+TPST_HD Fq2 frob2(const Fq2& a, int k) { return (k & 1) ? conj(a) : a; }
+
+// Frobenius x -> x^(p^k), k in {1,2,3}
+TPST_NI Fq12 frobenius(const Fq12& a, int k) {
+  Fq2 c61, c62, c12;
+  if (k == 1) {
+    c61 = fq2_const(params::FROB6_C1_1); c62 = fq2_const(params::FROB6_C2_1); c12 = fq2_const(params::FROB12_C1_1);
+  } else if (k == 2) {
+    c61 = fq2_const(params::FROB6_C1_2); c62 = fq2_const(params::FROB6_C2_2); c12 = fq2_const(params::FROB12_C1_2);
+  } else {
+    c61 = fq2_const(params::FROB6_C1_3); c62 = fq2_const(params::FROB6_C2_3); c12 = fq2_const(params::FROB12_C1_3);
+  }
+  Fq6 x0 = {frob2(a.c0.c0, k), mul(frob2(a.c0.c1, k), c61), mul(frob2(a.c0.c2, k), c62)};
+  Fq6 x1 = {frob2(a.c1.c0, k), mul(frob2(a.c1.c1, k), c61), mul(frob2(a.c1.c2, k), c62)};
+  x1 = {mul(x1.c0, c12), mul(x1.c1, c12), mul(x1.c2, c12)};
+  return {x0, x1};
+}
+
+}  // namespace tpst

@@ -1,0 +1,77 @@
+// Pippenger multi-scalar multiplication engine for CDNA4 (host-side API of
+// msm.hip).  Two shapes, matching the reference hot loops:
+//
+//  K2  variable-base MSM  sum_i s_i * P_i            (sqrt_pst.rs:198,
+//      mipp.rs:393, config 2 of BASELINE.json)
+//  K1  batched shared-base MSM  C_r = sum_j Z[r][j] * B_j  over R rows with
+//      one SRS-fixed base vector (sqrt_pst.rs:121-125 par_iter of
+//      MultilinearPC::commit), using precomputed window tables
+//      T[w][j] = 2^(c w) B_j so every row is ONE bucket set.
+//
+// Both run the same pipeline of kernels:
+//   signed-digit decomposition -> (bucket key, point index|sign) pairs
+//   -> radix sort by key -> bucket bounds -> bucket accumulation (XYZZ
+//   mixed adds, one thread per bucket) -> segmented weighted bucket
+//   reduction -> per-group (window / row) tree reduction -> combine.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+#include "curve.h"
+
+namespace tpst {
+
+// grow-only device scratch arena; reset() per call, never freed mid-call
+struct Arena {
+  char* base = nullptr;
+  size_t cap = 0;
+  size_t off = 0;
+  hipError_t reserve(size_t bytes);
+  void reset() { off = 0; }
+  template <class T>
+  T* take(size_t count) {
+    size_t bytes = (count * sizeof(T) + 255) & ~size_t(255);
+    T* p = reinterpret_cast<T*>(base + off);
+    off += bytes;
+    return p;
+  }
+  static size_t need(size_t count, size_t elem) { return (count * elem + 255) & ~size_t(255); }
+  void release();
+};
+
+// window size used for a variable-base MSM of n points
+int msm_window_bits(size_t n);
+
+// Variable-base MSM over device buffers.  bases: n affine points,
+// Montgomery form (24 / 48 u32 each); scalars: n canonical Fr (8 u32 each).
+// Writes one XYZZ point to d_out.  Returns hipSuccess or the first error.
+template <class F>
+hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint32_t* d_scalars,
+                   size_t n, Xyzz<F>* d_out);
+
+// Fixed-base tables for K1: T[w][j] = 2^(c w) * B_j (affine, Montgomery).
+struct BatchTables {
+  uint32_t* d_table = nullptr;  // W * N affine G1 points
+  size_t N = 0;
+  int c = 0;
+  int W = 0;
+};
+
+hipError_t batch_tables_build(hipStream_t s, const uint32_t* d_bases, size_t N, int c, BatchTables& t);
+void batch_tables_free(BatchTables& t);
+int batch_window_bits(size_t N);
+
+// K1: rows x N scalar matrix; scalar (r, j) is at d_scalars + 8*(r*row_stride + j*col_stride)
+// (canonical Fr).  Writes `rows` XYZZ points.
+hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint32_t* d_scalars,
+                     size_t rows, size_t row_stride, size_t col_stride, Xyzz<Fq>* d_out);
+
+// elementwise helpers
+template <class F>
+hipError_t points_to_mont(hipStream_t s, const uint32_t* d_in, uint32_t* d_out, size_t n);
+template <class F>
+hipError_t xyzz_to_affine_canonical(hipStream_t s, const Xyzz<F>* d_in, uint32_t* d_out, size_t n);
+template <class F>
+hipError_t affine_from_mont(hipStream_t s, const uint32_t* d_in, uint32_t* d_out, size_t n);
+
+}  // namespace tpst

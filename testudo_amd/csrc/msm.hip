@@ -1,0 +1,450 @@
+// Pippenger MSM kernels for gfx950 (see msm.h for the pipeline).
+#include <hipcub/hipcub.hpp>
+#include "device_util.h"
+#include "msm.h"
+
+namespace tpst {
+
+#define TPST_TRY(x)                          \
+  do {                                       \
+    hipError_t _e = (x);                     \
+    if (_e != hipSuccess) return _e;         \
+  } while (0)
+
+hipError_t Arena::reserve(size_t bytes) {
+  if (bytes <= cap) return hipSuccess;
+  if (base) {
+    hipError_t e = hipFree(base);
+    if (e != hipSuccess) return e;
+    base = nullptr;
+    cap = 0;
+  }
+  size_t want = bytes + (bytes >> 3);
+  hipError_t e = hipMalloc(&base, want);
+  if (e != hipSuccess) return e;
+  cap = want;
+  return hipSuccess;
+}
+
+void Arena::release() {
+  if (base) (void)hipFree(base);
+  base = nullptr;
+  cap = off = 0;
+}
+
+static inline unsigned grid_for(size_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
+
+static inline int bit_length(uint64_t v) {
+  int b = 0;
+  while (v) {
+    b++;
+    v >>= 1;
+  }
+  return b;
+}
+
+int msm_window_bits(size_t n) {
+  // 16-bit signed windows are the sweet spot for ~2^18..2^22 points; smaller
+  // inputs use smaller windows so buckets stay populated.
+  int lg = bit_length(n ? n - 1 : 0);
+  if (lg >= 20) return 16;
+  if (lg >= 16) return 13;
+  if (lg >= 12) return 10;
+  if (lg >= 8) return 7;
+  return 4;
+}
+
+int batch_window_bits(size_t N) {
+  int lg = bit_length(N ? N - 1 : 0);
+  if (lg >= 12) return 12;
+  if (lg >= 10) return 10;
+  if (lg >= 6) return 7;
+  return 4;
+}
+
+// number of signed-digit windows: ceil(254 / c) keeps the top digit < 2^(c-1)
+static inline int num_windows(int c) { return (254 + c - 1) / c; }
+
+// c-bit window of an 8-word canonical scalar starting at bit `off`
+__device__ __forceinline__ uint32_t window_bits(const uint32_t* s, int off, int c) {
+  const int w = off >> 5, b = off & 31;
+  const uint64_t lo = (w < 8) ? s[w] : 0u;
+  const uint64_t hi = (w + 1 < 8) ? s[w + 1] : 0u;
+  return (uint32_t)(((lo | (hi << 32)) >> b) & ((1ull << c) - 1));
+}
+
+// signed digit of window w given the running carry (arkworks make_digits,
+// except the top window keeps its carry instead of recentering)
+__device__ __forceinline__ int signed_digit(const uint32_t* s, int w, int c, int W, uint32_t& carry) {
+  const uint32_t coef = window_bits(s, w * c, c) + carry;
+  if (w == W - 1) {
+    carry = 0;
+    return (int)coef;
+  }
+  carry = (coef + (1u << (c - 1))) >> c;
+  return (int)coef - (int)(carry << c);
+}
+
+__device__ __forceinline__ void load_scalar(const uint32_t* p, uint32_t* s) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  const uint4 a = q[0], b = q[1];
+  s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w;
+  s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
+}
+
+// ------------------------------------------------------ K2 decomposition --
+__global__ void k_decompose_var(const uint32_t* __restrict__ scalars, size_t n, int c, int W,
+                                uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t s[8];
+  load_scalar(scalars + 8 * i, s);
+  const uint32_t nb = 1u << (c - 1);
+  const uint32_t sent = (uint32_t)W * nb;
+  uint32_t carry = 0;
+  for (int w = 0; w < W; w++) {
+    const int d = signed_digit(s, w, c, W, carry);
+    uint32_t key = sent, val = 0;
+    if (d != 0) {
+      key = (uint32_t)w * nb + (uint32_t)(abs(d) - 1);
+      val = (uint32_t)i | (d < 0 ? 0x80000000u : 0u);
+    }
+    keys[(size_t)w * n + i] = key;
+    vals[(size_t)w * n + i] = val;
+  }
+}
+
+__global__ void k_bucket_bounds(const uint32_t* __restrict__ keys, size_t m, uint32_t sent,
+                                uint32_t* __restrict__ bstart, uint32_t* __restrict__ bend) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const uint32_t k = keys[i];
+  if (k >= sent) return;
+  if (i == 0 || keys[i - 1] != k) bstart[k] = (uint32_t)i;
+  if (i == m - 1 || keys[i + 1] != k) bend[k] = (uint32_t)i + 1;
+}
+
+// one thread per bucket: sum its (signed) points with XYZZ mixed additions
+template <class F>
+__global__ void k_bucket_acc(const uint32_t* __restrict__ vals, const uint32_t* __restrict__ bstart,
+                             const uint32_t* __restrict__ bend, const uint32_t* __restrict__ bases,
+                             size_t nbk, Xyzz<F>* __restrict__ out) {
+  const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nbk) return;
+  const uint32_t e0 = bstart[b], e1 = bend[b];
+  Xyzz<F> acc = Xyzz<F>::inf();
+  for (uint32_t e = e0; e < e1; e++) {
+    const uint32_t v = vals[e];
+    Affine<F> p = load_affine<F>(bases, v & 0x7fffffffu);
+    if (v >> 31) p.y = neg(p.y);
+    acc = add_affine(acc, p);
+  }
+  store_xyzz(out, b, acc);
+}
+
+// segment t of group g: sum_{b in seg} (b+1) * S_b with b the bucket index
+// inside the group (bucket b holds digit value b+1)
+template <class F>
+__global__ void k_seg_reduce(const Xyzz<F>* __restrict__ buckets, uint32_t nb, uint32_t L, size_t nseg,
+                             Xyzz<F>* __restrict__ seg_out) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nseg) return;
+  const uint32_t S = nb / L;
+  const size_t g = t / S;
+  const uint32_t k = (uint32_t)(t % S);
+  const size_t base = g * nb + (size_t)k * L;
+  Xyzz<F> acc = Xyzz<F>::inf(), sum = Xyzz<F>::inf();
+  for (int b = (int)L - 1; b >= 0; b--) {
+    acc = add(acc, load_xyzz(buckets, base + b));
+    sum = add(sum, acc);
+  }
+  const uint32_t s0 = k * L;
+  if (s0 != 0 && !is_inf(acc)) {
+    uint32_t sc[1] = {s0};
+    int nbits = 32 - __builtin_clz(s0);
+    sum = add(sum, scalar_mul_xyzz(acc, sc, nbits));
+  }
+  store_xyzz(seg_out, t, sum);
+}
+
+// one workgroup per group: sum its S segment results
+template <class F, int BS>
+__global__ void __launch_bounds__(BS) k_group_reduce(const Xyzz<F>* __restrict__ seg, uint32_t S,
+                                                     Xyzz<F>* __restrict__ out) {
+  __shared__ Xyzz<F> sh[BS];
+  const size_t g = blockIdx.x;
+  Xyzz<F> acc = Xyzz<F>::inf();
+  for (uint32_t k = threadIdx.x; k < S; k += BS) acc = add(acc, load_xyzz(seg, g * S + k));
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int h = BS / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) sh[threadIdx.x] = add(sh[threadIdx.x], sh[threadIdx.x + h]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) store_xyzz(out, g, sh[0]);
+}
+
+// Horner over windows: sum_w 2^(c w) G_w
+template <class F>
+__global__ void k_window_combine(const Xyzz<F>* __restrict__ win, int W, int c, Xyzz<F>* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  Xyzz<F> acc = load_xyzz(win, W - 1);
+  for (int w = W - 2; w >= 0; w--) {
+    for (int i = 0; i < c; i++) acc = dbl(acc);
+    acc = add(acc, load_xyzz(win, w));
+  }
+  store_xyzz(out, 0, acc);
+}
+
+template <class F>
+__global__ void k_points_to_mont(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Affine<F> a = load_affine<F>(in, i);
+  Fq* c = reinterpret_cast<Fq*>(&a);
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(Affine<F>) / sizeof(Fq)); k++) c[k] = to_mont(c[k]);
+  store_affine(out, i, a);
+}
+
+template <class F>
+__global__ void k_affine_from_mont(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Affine<F> a = load_affine<F>(in, i);
+  Fq* c = reinterpret_cast<Fq*>(&a);
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(Affine<F>) / sizeof(Fq)); k++) c[k] = from_mont(c[k]);
+  store_affine(out, i, a);
+}
+
+template <class F>
+__global__ void k_xyzz_to_affine_canonical(const Xyzz<F>* __restrict__ in, uint32_t* __restrict__ out, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Affine<F> a = to_affine(load_xyzz(in, i));
+  Fq* c = reinterpret_cast<Fq*>(&a);
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(Affine<F>) / sizeof(Fq)); k++) c[k] = from_mont(c[k]);
+  store_affine(out, i, a);
+}
+
+template <class F>
+hipError_t points_to_mont(hipStream_t s, const uint32_t* d_in, uint32_t* d_out, size_t n) {
+  if (!n) return hipSuccess;
+  k_points_to_mont<F><<<grid_for(n, 256), 256, 0, s>>>(d_in, d_out, n);
+  return hipGetLastError();
+}
+
+template <class F>
+hipError_t affine_from_mont(hipStream_t s, const uint32_t* d_in, uint32_t* d_out, size_t n) {
+  if (!n) return hipSuccess;
+  k_affine_from_mont<F><<<grid_for(n, 256), 256, 0, s>>>(d_in, d_out, n);
+  return hipGetLastError();
+}
+
+template <class F>
+hipError_t xyzz_to_affine_canonical(hipStream_t s, const Xyzz<F>* d_in, uint32_t* d_out, size_t n) {
+  if (!n) return hipSuccess;
+  k_xyzz_to_affine_canonical<F><<<grid_for(n, 64), 64, 0, s>>>(d_in, d_out, n);
+  return hipGetLastError();
+}
+
+// reduce `groups` bucket sets of nb buckets each into one point per group
+template <class F>
+static hipError_t reduce_buckets(Arena& ar, hipStream_t s, const Xyzz<F>* d_buckets, size_t groups, uint32_t nb,
+                                 Xyzz<F>* d_group_out) {
+  uint32_t L = nb >= 32 ? 32 : nb;
+  const uint32_t S = nb / L;
+  const size_t nseg = groups * S;
+  Xyzz<F>* seg = ar.take<Xyzz<F>>(nseg);
+  k_seg_reduce<F><<<grid_for(nseg, 64), 64, 0, s>>>(d_buckets, nb, L, nseg, seg);
+  TPST_TRY(hipGetLastError());
+  k_group_reduce<F, 64><<<(unsigned)groups, 64, 0, s>>>(seg, S, d_group_out);
+  return hipGetLastError();
+}
+
+template <class F>
+hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint32_t* d_scalars, size_t n,
+                   Xyzz<F>* d_out) {
+  if (n == 0) {
+    Xyzz<F> inf = Xyzz<F>::inf();
+    return hipMemcpyAsync(d_out, &inf, sizeof(inf), hipMemcpyHostToDevice, s);
+  }
+  const int c = msm_window_bits(n);
+  const int W = num_windows(c);
+  const uint32_t nb = 1u << (c - 1);
+  const size_t m = (size_t)W * n;
+  const size_t nbk = (size_t)W * nb;
+  const uint32_t sent = (uint32_t)nbk;
+  const int end_bit = bit_length(sent);
+
+  size_t sort_bytes = 0;
+  TPST_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                              (uint32_t*)nullptr, (uint32_t*)nullptr, (int)m, 0, end_bit, s));
+  const uint32_t L = nb >= 32 ? 32 : nb;
+  size_t need = Arena::need(m, 4) * 4 + Arena::need(nbk, 4) * 2 + Arena::need(nbk, sizeof(Xyzz<F>)) +
+                Arena::need((size_t)W * (nb / L), sizeof(Xyzz<F>)) + Arena::need(W, sizeof(Xyzz<F>)) +
+                Arena::need(sort_bytes, 1) + 4096;
+  ar.reset();
+  TPST_TRY(ar.reserve(need));
+  uint32_t* keys = ar.take<uint32_t>(m);
+  uint32_t* vals = ar.take<uint32_t>(m);
+  uint32_t* keys2 = ar.take<uint32_t>(m);
+  uint32_t* vals2 = ar.take<uint32_t>(m);
+  uint32_t* bstart = ar.take<uint32_t>(nbk);
+  uint32_t* bend = ar.take<uint32_t>(nbk);
+  Xyzz<F>* buckets = ar.take<Xyzz<F>>(nbk);
+  Xyzz<F>* win = ar.take<Xyzz<F>>(W);
+  void* tmp = ar.take<char>(sort_bytes);
+
+  k_decompose_var<<<grid_for(n, 256), 256, 0, s>>>(d_scalars, n, c, W, keys, vals);
+  TPST_TRY(hipGetLastError());
+  TPST_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, sort_bytes, keys, keys2, vals, vals2, (int)m, 0, end_bit, s));
+  TPST_TRY(hipMemsetAsync(bstart, 0, nbk * 4, s));
+  TPST_TRY(hipMemsetAsync(bend, 0, nbk * 4, s));
+  k_bucket_bounds<<<grid_for(m, 256), 256, 0, s>>>(keys2, m, sent, bstart, bend);
+  TPST_TRY(hipGetLastError());
+  k_bucket_acc<F><<<grid_for(nbk, 64), 64, 0, s>>>(vals2, bstart, bend, d_bases, nbk, buckets);
+  TPST_TRY(hipGetLastError());
+  TPST_TRY(reduce_buckets<F>(ar, s, buckets, W, nb, win));
+  k_window_combine<F><<<1, 64, 0, s>>>(win, W, c, d_out);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ K1 ---
+// T[w][j] = 2^(c w) B_j, one thread per base
+__global__ void k_build_tables(const uint32_t* __restrict__ bases, size_t N, int c, int W, uint32_t* __restrict__ table) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= N) return;
+  G1A p = load_affine<Fq>(bases, j);
+  for (int w = 0; w < W; w++) {
+    store_affine(table, (size_t)w * N + j, p);
+    if (w + 1 < W) {
+      Xyzz<Fq> x = to_xyzz(p);
+      for (int i = 0; i < c; i++) x = dbl(x);
+      p = to_affine(x);
+    }
+  }
+}
+
+hipError_t batch_tables_build(hipStream_t s, const uint32_t* d_bases, size_t N, int c, BatchTables& t) {
+  batch_tables_free(t);
+  t.N = N;
+  t.c = c;
+  t.W = num_windows(c);
+  TPST_TRY(hipMalloc(&t.d_table, (size_t)t.W * N * 24 * sizeof(uint32_t)));
+  k_build_tables<<<grid_for(N, 64), 64, 0, s>>>(d_bases, N, c, t.W, t.d_table);
+  return hipGetLastError();
+}
+
+void batch_tables_free(BatchTables& t) {
+  if (t.d_table) (void)hipFree(t.d_table);
+  t.d_table = nullptr;
+  t.N = 0;
+}
+
+// one workgroup per row: LDS counting sort of the row's N*W signed digits
+// by bucket; writes the row's entries and bucket bounds.
+__global__ void __launch_bounds__(256) k_batch_sort(const uint32_t* __restrict__ scalars, size_t rows, size_t N,
+                                                    size_t row_stride, size_t col_stride, int c, int W,
+                                                    uint32_t* __restrict__ entries, uint32_t* __restrict__ bstart,
+                                                    uint32_t* __restrict__ bend) {
+  extern __shared__ uint32_t cnt[];  // nb counters
+  // XCD-aware: consecutive rows on the same XCD (blocks b, b+8, ... share one)
+  const size_t nblk = gridDim.x;
+  size_t r = blockIdx.x;
+  if (nblk % 8 == 0) r = (blockIdx.x % 8) * (nblk / 8) + blockIdx.x / 8;
+  if (r >= rows) return;
+  const uint32_t nb = 1u << (c - 1);
+  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) cnt[b] = 0;
+  __syncthreads();
+  for (size_t j = threadIdx.x; j < N; j += blockDim.x) {
+    uint32_t s[8];
+    load_scalar(scalars + 8 * (r * row_stride + j * col_stride), s);
+    uint32_t carry = 0;
+    for (int w = 0; w < W; w++) {
+      const int d = signed_digit(s, w, c, W, carry);
+      if (d) atomicAdd(&cnt[abs(d) - 1], 1u);
+    }
+  }
+  __syncthreads();
+  // exclusive scan of nb counters: thread t owns a contiguous slice
+  __shared__ uint32_t part[256];
+  const uint32_t per = (nb + blockDim.x - 1) / blockDim.x;
+  const uint32_t b0 = threadIdx.x * per;
+  uint32_t local = 0;
+  for (uint32_t b = b0; b < b0 + per && b < nb; b++) local += cnt[b];
+  part[threadIdx.x] = local;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+    for (unsigned t = 0; t < blockDim.x; t++) {
+      const uint32_t v = part[t];
+      part[t] = run;
+      run += v;
+    }
+  }
+  __syncthreads();
+  const size_t rowbase = r * N * (size_t)W;
+  uint32_t run = part[threadIdx.x];
+  for (uint32_t b = b0; b < b0 + per && b < nb; b++) {
+    const uint32_t v = cnt[b];
+    bstart[r * nb + b] = (uint32_t)(rowbase + run);
+    bend[r * nb + b] = (uint32_t)(rowbase + run + v);
+    cnt[b] = run;
+    run += v;
+  }
+  __syncthreads();
+  for (size_t j = threadIdx.x; j < N; j += blockDim.x) {
+    uint32_t s[8];
+    load_scalar(scalars + 8 * (r * row_stride + j * col_stride), s);
+    uint32_t carry = 0;
+    for (int w = 0; w < W; w++) {
+      const int d = signed_digit(s, w, c, W, carry);
+      if (d) {
+        const uint32_t pos = atomicAdd(&cnt[abs(d) - 1], 1u);
+        entries[rowbase + pos] = (uint32_t)(w * N + j) | (d < 0 ? 0x80000000u : 0u);
+      }
+    }
+  }
+}
+
+hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint32_t* d_scalars, size_t rows,
+                     size_t row_stride, size_t col_stride, Xyzz<Fq>* d_out) {
+  if (rows == 0) return hipSuccess;
+  const int c = t.c, W = t.W;
+  const size_t N = t.N;
+  const uint32_t nb = 1u << (c - 1);
+  const size_t m = rows * N * (size_t)W;
+  if (m >= (1ull << 32)) return hipErrorInvalidValue;  // entry offsets are u32
+  const size_t nbk = rows * nb;
+  const uint32_t L = nb >= 32 ? 32 : nb;
+  size_t need = Arena::need(m, 4) + 2 * Arena::need(nbk, 4) + Arena::need(nbk, sizeof(Xyzz<Fq>)) +
+                Arena::need(rows * (nb / L), sizeof(Xyzz<Fq>)) + 4096;
+  ar.reset();
+  TPST_TRY(ar.reserve(need));
+  uint32_t* entries = ar.take<uint32_t>(m);
+  uint32_t* bstart = ar.take<uint32_t>(nbk);
+  uint32_t* bend = ar.take<uint32_t>(nbk);
+  Xyzz<Fq>* buckets = ar.take<Xyzz<Fq>>(nbk);
+  unsigned nblk = (unsigned)rows;
+  k_batch_sort<<<nblk, 256, nb * sizeof(uint32_t), s>>>(d_scalars, rows, N, row_stride, col_stride, c, W, entries,
+                                                        bstart, bend);
+  TPST_TRY(hipGetLastError());
+  k_bucket_acc<Fq><<<grid_for(nbk, 64), 64, 0, s>>>(entries, bstart, bend, t.d_table, nbk, buckets);
+  TPST_TRY(hipGetLastError());
+  return reduce_buckets<Fq>(ar, s, buckets, rows, nb, d_out);
+}
+
+// explicit instantiations
+template hipError_t msm_var<Fq>(Arena&, hipStream_t, const uint32_t*, const uint32_t*, size_t, Xyzz<Fq>*);
+template hipError_t msm_var<Fq2>(Arena&, hipStream_t, const uint32_t*, const uint32_t*, size_t, Xyzz<Fq2>*);
+template hipError_t points_to_mont<Fq>(hipStream_t, const uint32_t*, uint32_t*, size_t);
+template hipError_t points_to_mont<Fq2>(hipStream_t, const uint32_t*, uint32_t*, size_t);
+template hipError_t affine_from_mont<Fq>(hipStream_t, const uint32_t*, uint32_t*, size_t);
+template hipError_t affine_from_mont<Fq2>(hipStream_t, const uint32_t*, uint32_t*, size_t);
+template hipError_t xyzz_to_affine_canonical<Fq>(hipStream_t, const Xyzz<Fq>*, uint32_t*, size_t);
+template hipError_t xyzz_to_affine_canonical<Fq2>(hipStream_t, const Xyzz<Fq2>*, uint32_t*, size_t);
+
+}  // namespace tpst

@@ -1,0 +1,28 @@
+// Host-side API of pairing.hip (K4): batched multi-Miller loop, Fq12 tree
+// product and final exponentiation on the device.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "msm.h"
+#include "pairing.h"
+
+namespace tpst {
+
+// G2Prepared for n points: coeffs laid out coefficient-major,
+// d_coeffs[idx * n + i] (idx < 69).  Infinity points get no use (the Miller
+// kernel skips pairs whose G1 or G2 point is infinity).
+hipError_t g2_prepare_batch(hipStream_t s, const uint32_t* d_g2, size_t n, LineCoeff* d_coeffs);
+
+// groups x n pairs -> groups GT elements (after final exponentiation).
+// d_g1: groups*n affine G1 (Montgomery); d_coeffs: prepared G2 of the same
+// pairs, coefficient-major with row length groups*n; d_g2 only for the
+// infinity test.  Output Montgomery Fq12 per group.
+hipError_t multi_pairing_prepared(Arena& ar, hipStream_t s, const uint32_t* d_g1, const uint32_t* d_g2,
+                                  const LineCoeff* d_coeffs, size_t groups, size_t n, Fq12* d_out);
+
+// convenience: prepare + pair
+hipError_t multi_pairing(Arena& ar, hipStream_t s, const uint32_t* d_g1, const uint32_t* d_g2, size_t groups,
+                         size_t n, Fq12* d_out);
+
+hipError_t fq12_from_mont(hipStream_t s, const Fq12* d_in, uint32_t* d_out, size_t n);
+
+}  // namespace tpst

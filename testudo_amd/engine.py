@@ -1,0 +1,88 @@
+"""Python handle on a libtpst context (one per GPU / process).
+
+Thin, typed wrappers over the C-ABI primitives; every call goes to the HIP
+library.  Errors raise ``TpstError`` with the library's message.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from .encoding import ptr
+
+
+class TpstError(RuntimeError):
+    pass
+
+
+class Context:
+    def __init__(self, device: int = 0):
+        self.lib = _lib.load()
+        h = C.c_void_p()
+        rc = self.lib.tpst_create(device, C.byref(h))
+        if rc != 0:
+            raise TpstError("tpst_create(%d) failed: %d" % (device, rc))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            self.lib.tpst_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, rc: int, what: str):
+        if rc != 0:
+            msg = self.lib.tpst_last_error(self.h)
+            raise TpstError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else ""))
+
+    # ------------------------------------------------------------ MSM ----
+    def g1_msm(self, bases: np.ndarray, scalars: np.ndarray) -> np.ndarray:
+        bases = np.ascontiguousarray(bases, dtype=np.uint64).reshape(-1, 12)
+        scalars = np.ascontiguousarray(scalars, dtype=np.uint64).reshape(-1, 4)
+        out = np.zeros(12, dtype=np.uint64)
+        self.check(self.lib.tpst_g1_msm(self.h, ptr(bases), len(bases), ptr(scalars), len(scalars), ptr(out)),
+                   "tpst_g1_msm")
+        return out
+
+    def g2_msm(self, bases: np.ndarray, scalars: np.ndarray) -> np.ndarray:
+        bases = np.ascontiguousarray(bases, dtype=np.uint64).reshape(-1, 24)
+        scalars = np.ascontiguousarray(scalars, dtype=np.uint64).reshape(-1, 4)
+        out = np.zeros(24, dtype=np.uint64)
+        self.check(self.lib.tpst_g2_msm(self.h, ptr(bases), len(bases), ptr(scalars), len(scalars), ptr(out)),
+                   "tpst_g2_msm")
+        return out
+
+    def multi_pairing(self, g1: np.ndarray, g2: np.ndarray) -> np.ndarray:
+        g1 = np.ascontiguousarray(g1, dtype=np.uint64).reshape(-1, 12)
+        g2 = np.ascontiguousarray(g2, dtype=np.uint64).reshape(-1, 24)
+        assert len(g1) == len(g2)
+        out = np.zeros(72, dtype=np.uint64)
+        self.check(self.lib.tpst_multi_pairing(self.h, ptr(g1), ptr(g2), len(g1), ptr(out)), "tpst_multi_pairing")
+        return out
+
+    def g1_mul_generator(self, scalars: np.ndarray) -> np.ndarray:
+        scalars = np.ascontiguousarray(scalars, dtype=np.uint64).reshape(-1, 4)
+        out = np.zeros((len(scalars), 12), dtype=np.uint64)
+        self.check(self.lib.tpst_g1_mul_generator(self.h, ptr(scalars), len(scalars), ptr(out)),
+                   "tpst_g1_mul_generator")
+        return out
+
+    def g2_mul_generator(self, scalars: np.ndarray) -> np.ndarray:
+        scalars = np.ascontiguousarray(scalars, dtype=np.uint64).reshape(-1, 4)
+        out = np.zeros((len(scalars), 24), dtype=np.uint64)
+        self.check(self.lib.tpst_g2_mul_generator(self.h, ptr(scalars), len(scalars), ptr(out)),
+                   "tpst_g2_mul_generator")
+        return out
+
+    def microbench(self, kind: int, threads: int, iters: int) -> float:
+        ms = C.c_double()
+        self.check(self.lib.tpst_microbench(self.h, kind, threads, iters, C.byref(ms)), "tpst_microbench")
+        return ms.value
