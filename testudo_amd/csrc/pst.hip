@@ -1,0 +1,219 @@
+// sqrt-PST protocol kernels for gfx950 (see pst_kernels.h).
+#include "device_util.h"
+#include "pst_kernels.h"
+
+namespace tpst {
+
+static inline unsigned grid_for(size_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
+
+__global__ void k_fr_conv(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, size_t n, int to_mont_flag) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Fr a = load_f<Fr>(in + 8 * i);
+  store_f<Fr>(out + 8 * i, to_mont_flag ? to_mont(a) : from_mont(a));
+}
+
+hipError_t fr_to_mont(hipStream_t s, const uint32_t* in, uint32_t* out, size_t n) {
+  if (!n) return hipSuccess;
+  k_fr_conv<<<grid_for(n, 256), 256, 0, s>>>(in, out, n, 1);
+  return hipGetLastError();
+}
+
+hipError_t fr_from_mont(hipStream_t s, const uint32_t* in, uint32_t* out, size_t n) {
+  if (!n) return hipSuccess;
+  k_fr_conv<<<grid_for(n, 256), 256, 0, s>>>(in, out, n, 0);
+  return hipGetLastError();
+}
+
+__global__ void k_chi(const uint32_t* __restrict__ b, int m, uint32_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ((size_t)1 << m)) return;
+  Fr prod = Fr::one();
+  for (int j = 0; j < m; j++) {
+    const Fr bj = load_f<Fr>(b + 8 * j);
+    prod = mul(prod, ((i >> (m - j - 1)) & 1) ? bj : sub(Fr::one(), bj));
+  }
+  store_f<Fr>(out + 8 * i, prod);
+}
+
+hipError_t chi_table(hipStream_t s, const uint32_t* d_b, int m, uint32_t* d_out) {
+  const size_t n = (size_t)1 << m;
+  k_chi<<<grid_for(n, 256), 256, 0, s>>>(d_b, m, d_out);
+  return hipGetLastError();
+}
+
+// one workgroup per output j: the row Z[j*C .. j*C+C) is contiguous, read coalesced
+template <int BS>
+__global__ void __launch_bounds__(BS) k_get_q(const uint32_t* __restrict__ Z, int m_col, const uint32_t* __restrict__ chis,
+                                              uint32_t* __restrict__ q) {
+  __shared__ Fr sh[BS];
+  const size_t j = blockIdx.x;
+  const size_t C = (size_t)1 << m_col;
+  Fr acc = Fr::zero();
+  for (size_t i = threadIdx.x; i < C; i += BS) {
+    const Fr z = to_mont(load_f<Fr>(Z + 8 * ((j << m_col) | i)));
+    acc = add(acc, mul(z, load_f<Fr>(chis + 8 * i)));
+  }
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int h = BS / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) sh[threadIdx.x] = add(sh[threadIdx.x], sh[threadIdx.x + h]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) store_f<Fr>(q + 8 * j, sh[0]);
+}
+
+hipError_t get_q(hipStream_t s, const uint32_t* d_Z, int m_col, int m_row, const uint32_t* d_chis, uint32_t* d_q) {
+  k_get_q<256><<<(unsigned)((size_t)1 << m_row), 256, 0, s>>>(d_Z, m_col, d_chis, d_q);
+  return hipGetLastError();
+}
+
+template <int BS>
+__global__ void __launch_bounds__(BS) k_fr_dot(const uint32_t* __restrict__ x, const uint32_t* __restrict__ y, size_t n,
+                                               uint32_t* __restrict__ v) {
+  __shared__ Fr sh[BS];
+  Fr acc = Fr::zero();
+  for (size_t i = threadIdx.x; i < n; i += BS) acc = add(acc, mul(load_f<Fr>(x + 8 * i), load_f<Fr>(y + 8 * i)));
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int h = BS / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) sh[threadIdx.x] = add(sh[threadIdx.x], sh[threadIdx.x + h]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) store_f<Fr>(v, sh[0]);
+}
+
+hipError_t fr_dot(hipStream_t s, const uint32_t* d_x, const uint32_t* d_y, size_t n, uint32_t* d_v) {
+  k_fr_dot<256><<<1, 256, 0, s>>>(d_x, d_y, n, d_v);
+  return hipGetLastError();
+}
+
+__global__ void k_pst_step(const uint32_t* __restrict__ r, size_t half, const uint32_t* __restrict__ pt,
+                           uint32_t* __restrict__ qcan, uint32_t* __restrict__ rnext) {
+  const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= half) return;
+  const Fr p = load_f<Fr>(pt);
+  const Fr r0 = load_f<Fr>(r + 16 * b), r1 = load_f<Fr>(r + 16 * b + 8);
+  const Fr d = sub(r1, r0);
+  store_f<Fr>(qcan + 8 * b, from_mont(d));
+  store_f<Fr>(rnext + 8 * b, add(r0, mul(d, p)));  // r0(1-p) + r1 p
+}
+
+hipError_t pst_step(hipStream_t s, const uint32_t* d_r, size_t half, const uint32_t* d_pt, uint32_t* d_qcan,
+                    uint32_t* d_rnext) {
+  if (!half) return hipSuccess;
+  k_pst_step<<<grid_for(half, 256), 256, 0, s>>>(d_r, half, d_pt, d_qcan, d_rnext);
+  return hipGetLastError();
+}
+
+template <class F>
+__global__ void k_compress(uint32_t* __restrict__ v, size_t split, const uint32_t* __restrict__ k) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= split) return;
+  uint32_t sc[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) sc[j] = k[j];
+  const Affine<F> l = load_affine<F>(v, i), r = load_affine<F>(v, i + split);
+  Xyzz<F> acc = scalar_mul(r, sc, 253);
+  acc = add_affine(acc, l);
+  store_affine(v, i, to_affine(acc));
+}
+
+template <class F>
+hipError_t compress_points(hipStream_t s, uint32_t* d_v, size_t split, const uint32_t* d_k) {
+  if (!split) return hipSuccess;
+  k_compress<F><<<grid_for(split, 64), 64, 0, s>>>(d_v, split, d_k);
+  return hipGetLastError();
+}
+
+__global__ void k_compress_fr(uint32_t* __restrict__ y, size_t split, const uint32_t* __restrict__ k) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= split) return;
+  const Fr c = load_f<Fr>(k);
+  store_f<Fr>(y + 8 * i, add(load_f<Fr>(y + 8 * i), mul(load_f<Fr>(y + 8 * (i + split)), c)));
+}
+
+hipError_t compress_fr(hipStream_t s, uint32_t* d_y, size_t split, const uint32_t* d_kmont) {
+  if (!split) return hipSuccess;
+  k_compress_fr<<<grid_for(split, 256), 256, 0, s>>>(d_y, split, d_kmont);
+  return hipGetLastError();
+}
+
+template <class F>
+__global__ void k_fixed_base(const uint32_t* __restrict__ p, const uint32_t* __restrict__ scalars, size_t n,
+                             uint32_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Affine<F> P = load_affine<F>(p, 0);
+  uint32_t k[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) k[j] = scalars[8 * i + j];
+  store_affine(out, i, to_affine(scalar_mul(P, k, 253)));
+}
+
+template <class F>
+hipError_t fixed_base_mul(hipStream_t s, const uint32_t* d_p, const uint32_t* d_scalars, size_t n, uint32_t* d_out) {
+  if (!n) return hipSuccess;
+  k_fixed_base<F><<<grid_for(n, 64), 64, 0, s>>>(d_p, d_scalars, n, d_out);
+  return hipGetLastError();
+}
+
+template <class F>
+__global__ void k_pair_sum(const uint32_t* __restrict__ in, size_t half, uint32_t* __restrict__ out) {
+  const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= half) return;
+  Xyzz<F> a = to_xyzz(load_affine<F>(in, 2 * b));
+  a = add_affine(a, load_affine<F>(in, 2 * b + 1));
+  store_affine(out, b, to_affine(a));
+}
+
+template <class F>
+hipError_t pair_sum(hipStream_t s, const uint32_t* d_in, size_t half, uint32_t* d_out) {
+  if (!half) return hipSuccess;
+  k_pair_sum<F><<<grid_for(half, 64), 64, 0, s>>>(d_in, half, d_out);
+  return hipGetLastError();
+}
+
+template <class F>
+__global__ void k_xyzz_to_affine_mont(const Xyzz<F>* __restrict__ in, uint32_t* __restrict__ out, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  store_affine(out, i, to_affine(load_xyzz(in, i)));
+}
+
+template <class F>
+hipError_t xyzz_to_affine_mont(hipStream_t s, const Xyzz<F>* d_in, uint32_t* d_out, size_t n) {
+  if (!n) return hipSuccess;
+  k_xyzz_to_affine_mont<F><<<grid_for(n, 64), 64, 0, s>>>(d_in, d_out, n);
+  return hipGetLastError();
+}
+
+__global__ void k_gt_pow(const Fq12* __restrict__ base, const uint32_t* __restrict__ exps, size_t n,
+                         Fq12* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Fq12 b = base[i];
+  Fq12 r = Fq12::one();
+  for (int bit = 252; bit >= 0; bit--) {
+    r = sqr(r);
+    if ((exps[8 * i + (bit >> 5)] >> (bit & 31)) & 1) r = mul(r, b);
+  }
+  out[i] = r;
+}
+
+hipError_t gt_pow(hipStream_t s, const Fq12* d_base, const uint32_t* d_exps, size_t n, Fq12* d_out) {
+  if (!n) return hipSuccess;
+  k_gt_pow<<<grid_for(n, 32), 32, 0, s>>>(d_base, d_exps, n, d_out);
+  return hipGetLastError();
+}
+
+template hipError_t compress_points<Fq>(hipStream_t, uint32_t*, size_t, const uint32_t*);
+template hipError_t compress_points<Fq2>(hipStream_t, uint32_t*, size_t, const uint32_t*);
+template hipError_t fixed_base_mul<Fq>(hipStream_t, const uint32_t*, const uint32_t*, size_t, uint32_t*);
+template hipError_t fixed_base_mul<Fq2>(hipStream_t, const uint32_t*, const uint32_t*, size_t, uint32_t*);
+template hipError_t pair_sum<Fq>(hipStream_t, const uint32_t*, size_t, uint32_t*);
+template hipError_t pair_sum<Fq2>(hipStream_t, const uint32_t*, size_t, uint32_t*);
+template hipError_t xyzz_to_affine_mont<Fq>(hipStream_t, const Xyzz<Fq>*, uint32_t*, size_t);
+template hipError_t xyzz_to_affine_mont<Fq2>(hipStream_t, const Xyzz<Fq2>*, uint32_t*, size_t);
+
+}  // namespace tpst

@@ -1,5 +1,1008 @@
-// sqrt-PST protocol entry points (commit / open / verify) -- filled in below.
+// sqrt-PST protocol layer of libtpst (include/tpst.h): SRS (MultilinearPC
+// keys), the Polynomial handle (sqrt_pst.rs:14-265), MIPP prover/verifier
+// (mipp.rs:31-320) and the Poseidon transcript (poseidon_transcript.rs).
+//
+// Everything heavy runs on the device (K1 row MSMs, K2 MSMs, K3 G2 MSMs, K4
+// pairings, MIPP folds, Fr kernels); the host keeps the Fiat-Shamir
+// transcript, which is inherently sequential and only absorbs a few KB per
+// round.
+#include <cstring>
+#include <memory>
+#include <vector>
+
 #include "../../include/tpst.h"
 #include "ctx.h"
+#include "device_util.h"
+#include "pst_kernels.h"
 
-void tpst_release_pst_state(tpst_ctx*) {}
+using namespace tpst;
+
+#include "poseidon_constants.inc"
+
+// =================================================================== host ==
+namespace {
+
+Fq fq_canon(const uint64_t* c) {  // canonical u64 limbs -> Montgomery
+  Fq a;
+  memcpy(a.v, c, 48);
+  return to_mont(a);
+}
+void fq_out(const Fq& a, uint64_t* c) {
+  Fq r = from_mont(a);
+  memcpy(c, r.v, 48);
+}
+Fr fr_canon(const uint64_t* c) {
+  Fr a;
+  memcpy(a.v, c, 32);
+  return to_mont(a);
+}
+void fr_out(const Fr& a, uint64_t* c) {
+  Fr r = from_mont(a);
+  memcpy(c, r.v, 32);
+}
+
+// ------------------------------------------------------------ Poseidon ----
+struct PoseidonParams {
+  Fq ark[39][3];
+  Fq mds[3][3];
+  PoseidonParams() {
+    for (int r = 0; r < 39; r++)
+      for (int i = 0; i < 3; i++) ark[r][i] = fq_canon(POSEIDON_ARK[r][i]);
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) mds[i][j] = fq_canon(POSEIDON_MDS[i][j]);
+  }
+};
+const PoseidonParams& pparams() {
+  static PoseidonParams p;
+  return p;
+}
+
+// ark-crypto-primitives PoseidonSponge<Fq>: rate 2, capacity 1, alpha 17,
+// 8 full + 31 partial rounds (parameters.rs:309-338)
+struct Sponge {
+  Fq st[3];
+  bool squeezing;
+  int idx;
+  void load(const tpst_transcript* t) {
+    for (int i = 0; i < 3; i++) st[i] = fq_canon(t->state[i]);
+    squeezing = t->squeezing != 0;
+    idx = (int)t->index;
+  }
+  void store(tpst_transcript* t) const {
+    for (int i = 0; i < 3; i++) fq_out(st[i], t->state[i]);
+    t->squeezing = squeezing ? 1 : 0;
+    t->index = (uint32_t)idx;
+  }
+  void permute() {
+    const PoseidonParams& P = pparams();
+    for (int r = 0; r < 39; r++) {
+      for (int i = 0; i < 3; i++) st[i] = add(st[i], P.ark[r][i]);
+      const bool full = r < 4 || r >= 35;
+      for (int i = 0; i < (full ? 3 : 1); i++) {
+        const Fq x = st[i], x2 = sqr(x), x4 = sqr(x2), x8 = sqr(x4), x16 = sqr(x8);
+        st[i] = mul(x16, x);
+      }
+      Fq ns[3];
+      for (int i = 0; i < 3; i++)
+        ns[i] = add(add(mul(P.mds[i][0], st[0]), mul(P.mds[i][1], st[1])), mul(P.mds[i][2], st[2]));
+      for (int i = 0; i < 3; i++) st[i] = ns[i];
+    }
+  }
+  void absorb(const std::vector<Fq>& e) {
+    if (e.empty()) return;
+    int i0;
+    if (!squeezing) {
+      i0 = idx;
+      if (i0 == 2) {
+        permute();
+        i0 = 0;
+      }
+    } else {
+      permute();
+      i0 = 0;
+    }
+    size_t k = 0;
+    for (;;) {
+      const size_t rem = e.size() - k;
+      if (i0 + rem <= 2) {
+        for (size_t j = 0; j < rem; j++) st[1 + i0 + j] = add(st[1 + i0 + j], e[k + j]);
+        squeezing = false;
+        idx = i0 + (int)rem;
+        return;
+      }
+      const int take = 2 - i0;
+      for (int j = 0; j < take; j++) st[1 + i0 + j] = add(st[1 + i0 + j], e[k + j]);
+      permute();
+      k += take;
+      i0 = 0;
+    }
+  }
+  // Absorb for Vec<u8>: u64 LE length prefix, 47-byte chunks -> Fq
+  void absorb_bytes(const uint8_t* d, size_t n) {
+    std::vector<uint8_t> buf(8 + n);
+    const uint64_t len = n;
+    memcpy(buf.data(), &len, 8);
+    memcpy(buf.data() + 8, d, n);
+    std::vector<Fq> e;
+    for (size_t o = 0; o < buf.size(); o += 47) {
+      uint64_t l[6] = {0, 0, 0, 0, 0, 0};
+      const size_t m = buf.size() - o < 47 ? buf.size() - o : 47;
+      memcpy(l, buf.data() + o, m);
+      e.push_back(fq_canon(l));
+    }
+    absorb(e);
+  }
+  Fq squeeze1() {
+    int i0;
+    if (!squeezing) {
+      permute();
+      i0 = 0;
+    } else {
+      i0 = idx;
+      if (i0 == 2) {
+        permute();
+        i0 = 0;
+      }
+    }
+    const Fq out = st[1 + i0];
+    squeezing = true;
+    idx = i0 + 1;
+    return out;
+  }
+  // non-native squeeze_field_elements::<Fr>(1): low 252 bits of one Fq
+  void challenge(uint64_t* fr_canon_out) {
+    uint64_t c[6];
+    fq_out(squeeze1(), c);
+    fr_canon_out[0] = c[0];
+    fr_canon_out[1] = c[1];
+    fr_canon_out[2] = c[2];
+    fr_canon_out[3] = c[3] & ((1ull << 60) - 1);
+  }
+};
+
+// y > -y on canonical limbs  <=>  2y > p
+bool y_is_negative(const uint64_t* y) {
+  // compare y with p - y
+  uint64_t ny[6];
+  unsigned __int128 br = 0;
+  const uint32_t* p32 = params::FQ_P;
+  for (int i = 0; i < 6; i++) {
+    const uint64_t pi = (uint64_t)p32[2 * i] | ((uint64_t)p32[2 * i + 1] << 32);
+    unsigned __int128 d = (unsigned __int128)pi - y[i] - (uint64_t)br;
+    ny[i] = (uint64_t)d;
+    br = (d >> 64) & 1;
+  }
+  for (int i = 5; i >= 0; i--)
+    if (y[i] != ny[i]) return y[i] > ny[i];
+  return false;
+}
+
+void g1_bytes(const uint64_t* p, uint8_t* b) {  // ark serialize Compress::No
+  bool inf = true;
+  for (int i = 0; i < 12; i++) inf &= p[i] == 0;
+  memcpy(b, p, 96);
+  if (inf)
+    b[95] |= 0x40;
+  else if (y_is_negative(p + 6))
+    b[95] |= 0x80;
+}
+
+// host Fr helpers
+Fr fr_inv(const Fr& a) { return inv(a); }
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  hipError_t alloc(size_t b) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = b;
+    return b ? hipMalloc(&p, b) : hipSuccess;
+  }
+  uint32_t* u() const { return (uint32_t*)p; }
+};
+
+}  // namespace
+
+// ================================================================ state ==
+struct SrsState {
+  int nv = 0;
+  DevBuf g, h;                    // affine Montgomery
+  std::vector<std::unique_ptr<DevBuf>> pg, ph, pg_pair, ph_pair;
+  DevBuf gmask, hmask;
+  BatchTables tables;             // K1 tables over powers_of_g[0]
+  DevBuf hprep[2];                // G2Prepared of powers_of_h[odd], odd = 0/1
+  std::vector<uint64_t> flat;     // canonical export
+  ~SrsState() { batch_tables_free(tables); }
+};
+
+struct tpst_poly {
+  tpst_ctx* ctx;
+  int n, m_col, m_row, odd;
+  DevBuf Zown;
+  const uint32_t* d_Z = nullptr;  // canonical Fr
+  DevBuf q, chis;                 // Montgomery
+  bool has_q = false;
+};
+
+static std::unique_ptr<SrsState>& srs_slot(tpst_ctx* ctx) {
+  static std::mutex mu;
+  static std::vector<std::pair<tpst_ctx*, std::unique_ptr<SrsState>>> slots;
+  std::lock_guard<std::mutex> lk(mu);
+  for (auto& s : slots)
+    if (s.first == ctx) return s.second;
+  slots.emplace_back(ctx, nullptr);
+  return slots.back().second;
+}
+
+void tpst_release_pst_state(tpst_ctx* ctx) { srs_slot(ctx).reset(); }
+
+extern "C" size_t tpst_srs_flat_len(int nv) {
+  size_t n = 12 + 24;
+  for (int i = 0; i < nv; i++) n += ((size_t)1 << (nv - i)) * 36;
+  return n + (size_t)nv * 36;
+}
+
+// upload the flat canonical SRS and build every derived device table
+static int srs_install(tpst_ctx* ctx, int nv, const uint64_t* flat) {
+  auto st = std::make_unique<SrsState>();
+  st->nv = nv;
+  st->flat.assign(flat, flat + tpst_srs_flat_len(nv));
+  hipStream_t s = ctx->stream;
+  DevBuf stage;
+  TPST_HIP(ctx, stage.alloc(st->flat.size() * 8));
+  TPST_HIP(ctx, hipMemcpyAsync(stage.p, flat, st->flat.size() * 8, hipMemcpyHostToDevice, s));
+  const uint32_t* src = stage.u();
+  auto take = [&](DevBuf& dst, size_t npts, int words) -> hipError_t {
+    hipError_t e = dst.alloc(npts * words * 4);
+    if (e != hipSuccess) return e;
+    e = words == 24 ? points_to_mont<Fq>(s, src, dst.u(), npts) : points_to_mont<Fq2>(s, src, dst.u(), npts);
+    src += npts * words;
+    return e;
+  };
+  TPST_HIP(ctx, take(st->g, 1, 24));
+  TPST_HIP(ctx, take(st->h, 1, 48));
+  for (int i = 0; i < nv; i++) {
+    const size_t m = (size_t)1 << (nv - i);
+    st->pg.emplace_back(new DevBuf());
+    st->ph.emplace_back(new DevBuf());
+    TPST_HIP(ctx, take(*st->pg.back(), m, 24));
+    TPST_HIP(ctx, take(*st->ph.back(), m, 48));
+    st->pg_pair.emplace_back(new DevBuf());
+    st->ph_pair.emplace_back(new DevBuf());
+    TPST_HIP(ctx, st->pg_pair.back()->alloc(m / 2 * 96));
+    TPST_HIP(ctx, st->ph_pair.back()->alloc(m / 2 * 192));
+    TPST_HIP(ctx, pair_sum<Fq>(s, st->pg.back()->u(), m / 2, st->pg_pair.back()->u()));
+    TPST_HIP(ctx, pair_sum<Fq2>(s, st->ph.back()->u(), m / 2, st->ph_pair.back()->u()));
+  }
+  TPST_HIP(ctx, take(st->gmask, nv, 24));
+  TPST_HIP(ctx, take(st->hmask, nv, 48));
+  const size_t N = (size_t)1 << nv;
+  TPST_HIP(ctx, batch_tables_build(s, st->pg[0]->u(), N, batch_window_bits(N), st->tables));
+  for (int odd = 0; odd < 2 && odd < nv; odd++) {
+    const size_t m = (size_t)1 << (nv - odd);
+    TPST_HIP(ctx, st->hprep[odd].alloc(m * N_LINE_COEFFS * sizeof(LineCoeff)));
+    TPST_HIP(ctx, g2_prepare_batch(s, st->ph[odd]->u(), m, (LineCoeff*)st->hprep[odd].p));
+  }
+  TPST_HIP(ctx, hipStreamSynchronize(s));
+  srs_slot(ctx) = std::move(st);
+  return TPST_OK;
+}
+
+static SrsState* srs_of(tpst_ctx* ctx) { return srs_slot(ctx).get(); }
+
+// SplitMix64 Fr stream (same definition as the bench / oracle generators)
+static uint64_t splitmix(uint64_t seed, uint64_t i) {
+  uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+extern "C" uint64_t tpst_fr_stream(uint64_t seed, size_t n, uint64_t start, uint64_t* out) {
+  const uint32_t* r = params::FR_P;
+  uint64_t k = start;
+  size_t got = 0;
+  while (got < n) {
+    uint64_t v[4];
+    for (int j = 0; j < 4; j++) v[j] = splitmix(seed, 4 * k + j);
+    v[3] &= (1ull << 61) - 1;
+    k++;
+    bool lt = false;
+    for (int i = 3; i >= 0; i--) {
+      const uint64_t ri = (uint64_t)r[2 * i] | ((uint64_t)r[2 * i + 1] << 32);
+      if (v[i] != ri) {
+        lt = v[i] < ri;
+        break;
+      }
+    }
+    if (lt) {
+      memcpy(out + 4 * got, v, 32);
+      got++;
+    }
+  }
+  return k;
+}
+
+// MultilinearPC::setup semantics from a seeded trapdoor: g = k_g G1, h = k_h G2,
+// powers_of_g[i][x] = g^{eq(t[i..], x)} (LSB-first), g_mask[i] = g^{t_i}
+extern "C" int tpst_srs_setup(tpst_ctx* ctx, int nv, uint64_t seed) {
+  if (!ctx || nv <= 0 || nv > 28) return fail(ctx, TPST_E_ARG, "bad nv");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  std::vector<uint64_t> vals(4 * (nv + 2));
+  tpst_fr_stream(seed, nv + 2, 0, vals.data());
+  std::vector<Fr> t(nv);
+  for (int i = 0; i < nv; i++) t[i] = fr_canon(&vals[4 * (2 + i)]);
+  // all scalars: [k_g], [k_h] handled by generator muls; then eq tables and t
+  std::vector<uint64_t> sc;  // canonical: for i: eq(t[i..]) ; then t
+  for (int i = 0; i < nv; i++) {
+    std::vector<Fr> tab(1, Fr::one());
+    for (int j = i; j < nv; j++) {
+      const size_t m = tab.size();
+      tab.resize(2 * m);
+      for (size_t x = 0; x < m; x++) {
+        const Fr v = tab[x];
+        tab[x] = mul(v, sub(Fr::one(), t[j]));
+        tab[x + m] = mul(v, t[j]);
+      }
+    }
+    for (auto& v : tab) {
+      uint64_t c[4];
+      fr_out(v, c);
+      sc.insert(sc.end(), c, c + 4);
+    }
+  }
+  for (int i = 0; i < nv; i++) sc.insert(sc.end(), &vals[4 * (2 + i)], &vals[4 * (2 + i)] + 4);
+  const size_t ns = sc.size() / 4;
+  hipStream_t s = ctx->stream;
+  DevBuf d_sc, d_gh_sc, d_g, d_h, d_og, d_oh;
+  TPST_HIP(ctx, d_sc.alloc(ns * 32));
+  TPST_HIP(ctx, d_gh_sc.alloc(64));
+  TPST_HIP(ctx, d_g.alloc(96));
+  TPST_HIP(ctx, d_h.alloc(192));
+  TPST_HIP(ctx, d_og.alloc(ns * 96));
+  TPST_HIP(ctx, d_oh.alloc(ns * 192));
+  TPST_HIP(ctx, hipMemcpyAsync(d_sc.p, sc.data(), ns * 32, hipMemcpyHostToDevice, s));
+  TPST_HIP(ctx, hipMemcpyAsync(d_gh_sc.p, vals.data(), 64, hipMemcpyHostToDevice, s));
+  // g, h from the standard generators
+  {
+    const uint32_t* gs = params::G1_GEN_X;
+    std::vector<uint32_t> gen1(24), gen2(48);
+    memcpy(gen1.data(), params::G1_GEN_X, 48);
+    memcpy(gen1.data() + 12, params::G1_GEN_Y, 48);
+    memcpy(gen2.data(), params::G2_GEN_X, 96);
+    memcpy(gen2.data() + 24, params::G2_GEN_Y, 96);
+    (void)gs;
+    DevBuf dg1, dg2;
+    TPST_HIP(ctx, dg1.alloc(96));
+    TPST_HIP(ctx, dg2.alloc(192));
+    TPST_HIP(ctx, hipMemcpyAsync(dg1.p, gen1.data(), 96, hipMemcpyHostToDevice, s));
+    TPST_HIP(ctx, hipMemcpyAsync(dg2.p, gen2.data(), 192, hipMemcpyHostToDevice, s));
+    TPST_HIP(ctx, fixed_base_mul<Fq>(s, dg1.u(), d_gh_sc.u(), 1, d_g.u()));
+    TPST_HIP(ctx, fixed_base_mul<Fq2>(s, dg2.u(), d_gh_sc.u() + 8, 1, d_h.u()));
+    TPST_HIP(ctx, fixed_base_mul<Fq>(s, d_g.u(), d_sc.u(), ns, d_og.u()));
+    TPST_HIP(ctx, fixed_base_mul<Fq2>(s, d_h.u(), d_sc.u(), ns, d_oh.u()));
+    TPST_HIP(ctx, affine_from_mont<Fq>(s, d_g.u(), d_g.u(), 1));
+    TPST_HIP(ctx, affine_from_mont<Fq2>(s, d_h.u(), d_h.u(), 1));
+    TPST_HIP(ctx, affine_from_mont<Fq>(s, d_og.u(), d_og.u(), ns));
+    TPST_HIP(ctx, affine_from_mont<Fq2>(s, d_oh.u(), d_oh.u(), ns));
+    TPST_HIP(ctx, hipStreamSynchronize(s));
+  }
+  std::vector<uint64_t> og(ns * 12), oh(ns * 24), flat(tpst_srs_flat_len(nv));
+  TPST_HIP(ctx, hipMemcpy(og.data(), d_og.p, ns * 96, hipMemcpyDeviceToHost));
+  TPST_HIP(ctx, hipMemcpy(oh.data(), d_oh.p, ns * 192, hipMemcpyDeviceToHost));
+  TPST_HIP(ctx, hipMemcpy(flat.data(), d_g.p, 96, hipMemcpyDeviceToHost));
+  TPST_HIP(ctx, hipMemcpy(flat.data() + 12, d_h.p, 192, hipMemcpyDeviceToHost));
+  uint64_t* o = flat.data() + 36;
+  size_t off = 0;
+  for (int i = 0; i < nv; i++) {
+    const size_t m = (size_t)1 << (nv - i);
+    memcpy(o, &og[12 * off], m * 96);
+    o += 12 * m;
+    memcpy(o, &oh[24 * off], m * 192);
+    o += 24 * m;
+    off += m;
+  }
+  memcpy(o, &og[12 * off], nv * 96);
+  o += 12 * nv;
+  memcpy(o, &oh[24 * off], nv * 192);
+  return srs_install(ctx, nv, flat.data());
+}
+
+extern "C" int tpst_srs_load(tpst_ctx* ctx, int nv, const uint64_t* flat) {
+  if (!ctx || !flat || nv <= 0 || nv > 28) return fail(ctx, TPST_E_ARG, "bad argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  return srs_install(ctx, nv, flat);
+}
+
+extern "C" int tpst_srs_export(tpst_ctx* ctx, uint64_t* flat) {
+  if (!ctx || !flat) return fail(ctx, TPST_E_ARG, "null argument");
+  SrsState* st = srs_of(ctx);
+  if (!st) return fail(ctx, TPST_E_STATE, "no SRS loaded");
+  memcpy(flat, st->flat.data(), st->flat.size() * 8);
+  return TPST_OK;
+}
+
+// ============================================================ transcript ==
+extern "C" void tpst_transcript_init(tpst_transcript* t) {
+  if (!t) return;
+  memset(t, 0, sizeof *t);
+}
+
+extern "C" int tpst_transcript_append_g1(tpst_transcript* t, const uint64_t* p) {
+  if (!t || !p) return TPST_E_ARG;
+  Sponge sp;
+  sp.load(t);
+  uint8_t b[96];
+  g1_bytes(p, b);
+  sp.absorb_bytes(b, 96);
+  sp.store(t);
+  return TPST_OK;
+}
+
+extern "C" int tpst_transcript_append_gt(tpst_transcript* t, const uint64_t* gt) {
+  if (!t || !gt) return TPST_E_ARG;
+  Sponge sp;
+  sp.load(t);
+  sp.absorb_bytes((const uint8_t*)gt, 576);
+  sp.store(t);
+  return TPST_OK;
+}
+
+extern "C" int tpst_transcript_challenge(tpst_transcript* t, uint64_t* out) {
+  if (!t || !out) return TPST_E_ARG;
+  Sponge sp;
+  sp.load(t);
+  sp.challenge(out);
+  sp.store(t);
+  return TPST_OK;
+}
+
+// ================================================================ poly ===
+static int poly_dims(int n, int& m_col, int& m_row, int& odd) {
+  if (n < 2 || n > 40) return -1;
+  m_col = n / 2;
+  m_row = n - m_col;
+  odd = n % 2;
+  return 0;
+}
+
+extern "C" int tpst_poly_from_evaluations(tpst_ctx* ctx, const uint64_t* Z, int n, tpst_poly** out) {
+  if (!ctx || !Z || !out) return fail(ctx, TPST_E_ARG, "null argument");
+  auto p = std::make_unique<tpst_poly>();
+  if (poly_dims(n, p->m_col, p->m_row, p->odd)) return fail(ctx, TPST_E_ARG, "bad num_vars");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  p->ctx = ctx;
+  p->n = n;
+  TPST_HIP(ctx, p->Zown.alloc(((size_t)1 << n) * 32));
+  TPST_HIP(ctx, hipMemcpy(p->Zown.p, Z, ((size_t)1 << n) * 32, hipMemcpyHostToDevice));
+  p->d_Z = p->Zown.u();
+  *out = p.release();
+  return TPST_OK;
+}
+
+extern "C" int tpst_poly_from_evaluations_dev(tpst_ctx* ctx, const void* d_Z, int n, tpst_poly** out) {
+  if (!ctx || !d_Z || !out) return fail(ctx, TPST_E_ARG, "null argument");
+  auto p = std::make_unique<tpst_poly>();
+  if (poly_dims(n, p->m_col, p->m_row, p->odd)) return fail(ctx, TPST_E_ARG, "bad num_vars");
+  p->ctx = ctx;
+  p->n = n;
+  p->d_Z = (const uint32_t*)d_Z;
+  *out = p.release();
+  return TPST_OK;
+}
+
+extern "C" void tpst_poly_free(tpst_poly* p) { delete p; }
+
+// get_q (sqrt_pst.rs:81-101): chis over b = point[m_row..], q = Z^T chis
+static int poly_get_q(tpst_ctx* ctx, tpst_poly* p, const uint64_t* point) {
+  hipStream_t s = ctx->stream;
+  DevBuf b;
+  TPST_HIP(ctx, b.alloc((size_t)(p->m_col ? p->m_col : 1) * 32));
+  if (p->m_col) {
+    TPST_HIP(ctx, hipMemcpyAsync(b.p, point + 4 * p->m_row, p->m_col * 32, hipMemcpyHostToDevice, s));
+    TPST_HIP(ctx, fr_to_mont(s, b.u(), b.u(), p->m_col));
+  }
+  TPST_HIP(ctx, p->chis.alloc(((size_t)1 << p->m_col) * 32));
+  TPST_HIP(ctx, p->q.alloc(((size_t)1 << p->m_row) * 32));
+  TPST_HIP(ctx, chi_table(s, b.u(), p->m_col, p->chis.u()));
+  TPST_HIP(ctx, get_q(s, p->d_Z, p->m_col, p->m_row, p->chis.u(), p->q.u()));
+  TPST_HIP(ctx, hipStreamSynchronize(s));
+  p->has_q = true;
+  return TPST_OK;
+}
+
+extern "C" int tpst_poly_eval(tpst_ctx* ctx, tpst_poly* p, const uint64_t* point, uint64_t* out_v) {
+  if (!ctx || !p || !point || !out_v) return fail(ctx, TPST_E_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  if (!p->has_q) {
+    int rc = poly_get_q(ctx, p, point);
+    if (rc) return rc;
+  }
+  hipStream_t s = ctx->stream;
+  DevBuf a, ca, v;
+  TPST_HIP(ctx, a.alloc(p->m_row * 32));
+  TPST_HIP(ctx, ca.alloc(((size_t)1 << p->m_row) * 32));
+  TPST_HIP(ctx, v.alloc(32));
+  TPST_HIP(ctx, hipMemcpyAsync(a.p, point, p->m_row * 32, hipMemcpyHostToDevice, s));
+  TPST_HIP(ctx, fr_to_mont(s, a.u(), a.u(), p->m_row));
+  TPST_HIP(ctx, chi_table(s, a.u(), p->m_row, ca.u()));
+  TPST_HIP(ctx, fr_dot(s, p->q.u(), ca.u(), (size_t)1 << p->m_row, v.u()));
+  TPST_HIP(ctx, fr_from_mont(s, v.u(), v.u(), 1));
+  TPST_HIP(ctx, hipMemcpyAsync(out_v, v.p, 32, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipStreamSynchronize(s));
+  return TPST_OK;
+}
+
+// commit (sqrt_pst.rs:117-149): K1 row MSMs + IPP T = prod e(C_i, h_i)
+static int poly_commit_dev(tpst_ctx* ctx, tpst_poly* p, uint32_t* d_comms_mont, Fq12* d_T) {
+  SrsState* st = srs_of(ctx);
+  if (!st) return fail(ctx, TPST_E_STATE, "no SRS loaded");
+  if (st->nv != p->m_row) return fail(ctx, TPST_E_ARG, "SRS num_vars != ceil(n/2)");
+  hipStream_t s = ctx->stream;
+  const size_t C = (size_t)1 << p->m_col;
+  ctx->arena2.reset();
+  TPST_HIP(ctx, ctx->arena2.reserve(Arena::need(C, sizeof(Xyzz<Fq>)) + 256));
+  Xyzz<Fq>* rows = ctx->arena2.take<Xyzz<Fq>>(C);
+  TPST_HIP(ctx, msm_batch(ctx->arena, s, st->tables, p->d_Z, C, 1, C, rows));
+  TPST_HIP(ctx, xyzz_to_affine_mont<Fq>(s, rows, d_comms_mont, C));
+  const LineCoeff* hp = (const LineCoeff*)st->hprep[p->odd].p;
+  const size_t need = Arena::need(C, sizeof(Fq12)) + 4096;
+  ctx->arena.reset();
+  TPST_HIP(ctx, ctx->arena.reserve(need));
+  TPST_HIP(ctx, multi_pairing_prepared(ctx->arena, s, d_comms_mont, st->ph[p->odd]->u(), hp, 1, C, d_T));
+  return TPST_OK;
+}
+
+extern "C" int tpst_poly_commit(tpst_ctx* ctx, tpst_poly* p, uint64_t* comms, uint64_t* T) {
+  if (!ctx || !p || !comms || !T) return fail(ctx, TPST_E_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  const size_t C = (size_t)1 << p->m_col;
+  DevBuf cm, tt, out;
+  TPST_HIP(ctx, cm.alloc(C * 96));
+  TPST_HIP(ctx, tt.alloc(sizeof(Fq12)));
+  TPST_HIP(ctx, out.alloc(C * 96 + 576));
+  int rc = poly_commit_dev(ctx, p, cm.u(), (Fq12*)tt.p);
+  if (rc) return rc;
+  hipStream_t s = ctx->stream;
+  TPST_HIP(ctx, affine_from_mont<Fq>(s, cm.u(), out.u(), C));
+  TPST_HIP(ctx, fq12_from_mont(s, (Fq12*)tt.p, out.u() + 24 * C, 1));
+  TPST_HIP(ctx, hipMemcpyAsync(comms, out.p, C * 96, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipMemcpyAsync(T, out.u() + 24 * C, 576, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipStreamSynchronize(s));
+  return TPST_OK;
+}
+
+// device-resident commit: d_comms canonical affine (C*96 B), d_T canonical GT
+extern "C" int tpst_poly_commit_dev(tpst_ctx* ctx, tpst_poly* p, void* d_comms, void* d_T) {
+  if (!ctx || !p || !d_comms || !d_T) return fail(ctx, TPST_E_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  const size_t C = (size_t)1 << p->m_col;
+  ctx->io.reset();
+  TPST_HIP(ctx, ctx->io.reserve(Arena::need(C * 24, 4) + Arena::need(1, sizeof(Fq12)) + 512));
+  uint32_t* cm = ctx->io.take<uint32_t>(C * 24);
+  Fq12* tt = ctx->io.take<Fq12>(1);
+  int rc = poly_commit_dev(ctx, p, cm, tt);
+  if (rc) return rc;
+  TPST_HIP(ctx, affine_from_mont<Fq>(ctx->stream, cm, (uint32_t*)d_comms, C));
+  TPST_HIP(ctx, fq12_from_mont(ctx->stream, tt, (uint32_t*)d_T, 1));
+  return TPST_OK;
+}
+
+// --------------------------------------------------------------- open ----
+// MSM over device bases (Montgomery) with Montgomery Fr scalars (converted)
+template <class F>
+static hipError_t msm_mont_scalars(tpst_ctx* ctx, const uint32_t* bases, const uint32_t* scal_mont, size_t n,
+                                   uint32_t* tmp_canon, Xyzz<F>* out) {
+  hipError_t e = fr_from_mont(ctx->stream, scal_mont, tmp_canon, n);
+  if (e != hipSuccess) return e;
+  return msm_var<F>(ctx->arena, ctx->stream, bases, tmp_canon, n, out);
+}
+
+// PST open of evals (Montgomery, 2^k) at `pt` (k Montgomery Fr on device),
+// proofs over paired bases of level off+i; writes k XYZZ points
+template <class F>
+static int pst_open_dev(tpst_ctx* ctx, const std::vector<std::unique_ptr<DevBuf>>& pairs, int off,
+                        const uint32_t* d_evals, int k, const uint32_t* d_pt, Xyzz<F>* d_out) {
+  hipStream_t s = ctx->stream;
+  DevBuf r0, r1, qc;
+  const size_t full = (size_t)1 << k;
+  TPST_HIP(ctx, r0.alloc(full * 32));
+  TPST_HIP(ctx, r1.alloc(full * 32));
+  TPST_HIP(ctx, qc.alloc(full * 32));
+  TPST_HIP(ctx, hipMemcpyAsync(r0.p, d_evals, full * 32, hipMemcpyDeviceToDevice, s));
+  uint32_t* cur = r0.u();
+  uint32_t* nxt = r1.u();
+  for (int i = 0; i < k; i++) {
+    const size_t half = (size_t)1 << (k - i - 1);
+    TPST_HIP(ctx, pst_step(s, cur, half, d_pt + 8 * i, qc.u(), nxt));
+    TPST_HIP(ctx, msm_var<F>(ctx->arena, s, pairs[off + i]->u(), qc.u(), half, d_out + i));
+    std::swap(cur, nxt);
+  }
+  return TPST_OK;
+}
+
+extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, const uint64_t* comms,
+                              const uint64_t* point, const uint64_t* T, tpst_open_proof* proof) {
+  (void)T;  // the reference passes T but the prover does not use it (mipp.rs:38)
+  if (!ctx || !p || !tr || !comms || !point || !proof) return fail(ctx, TPST_E_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  SrsState* st = srs_of(ctx);
+  if (!st) return fail(ctx, TPST_E_STATE, "no SRS loaded");
+  if (st->nv != p->m_row) return fail(ctx, TPST_E_ARG, "SRS num_vars != ceil(n/2)");
+  if (!p->has_q) {
+    int rc = poly_get_q(ctx, p, point);
+    if (rc) return rc;
+  }
+  hipStream_t s = ctx->stream;
+  const int m = p->m_col;
+  const size_t C = (size_t)1 << m;
+  memset(proof, 0, sizeof *proof);
+  proof->m_col = m;
+  proof->m_row = p->m_row;
+  Sponge sp;
+  sp.load(tr);
+
+  DevBuf A, Y, H, tmp, xy, gts, small, canon;
+  TPST_HIP(ctx, A.alloc(C * 96));
+  TPST_HIP(ctx, Y.alloc(C * 32));
+  TPST_HIP(ctx, H.alloc(C * 192));
+  TPST_HIP(ctx, tmp.alloc(C * 32));
+  TPST_HIP(ctx, xy.alloc(4 * sizeof(Xyzz<Fq2>) + 64 * sizeof(Xyzz<Fq2>)));
+  TPST_HIP(ctx, gts.alloc(2 * sizeof(Fq12)));
+  TPST_HIP(ctx, small.alloc(256));
+  TPST_HIP(ctx, canon.alloc(4096));
+  // A = comms (Montgomery), Y = chis, H = powers_of_h[odd]
+  {
+    DevBuf up;
+    TPST_HIP(ctx, up.alloc(C * 96));
+    TPST_HIP(ctx, hipMemcpyAsync(up.p, comms, C * 96, hipMemcpyHostToDevice, s));
+    TPST_HIP(ctx, points_to_mont<Fq>(s, up.u(), A.u(), C));
+    TPST_HIP(ctx, hipStreamSynchronize(s));
+  }
+  TPST_HIP(ctx, hipMemcpyAsync(Y.p, p->chis.p, C * 32, hipMemcpyDeviceToDevice, s));
+  TPST_HIP(ctx, hipMemcpyAsync(H.p, st->ph[p->odd]->p, C * 192, hipMemcpyDeviceToDevice, s));
+  Xyzz<Fq>* x1 = (Xyzz<Fq>*)xy.p;
+
+  // U = c_u = MSM(comms, chis)          sqrt_pst.rs:198
+  TPST_HIP(ctx, msm_mont_scalars<Fq>(ctx, A.u(), Y.u(), C, tmp.u(), x1));
+  TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(s, x1, canon.u(), 1));
+  TPST_HIP(ctx, hipMemcpyAsync(proof->U, canon.p, 96, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipStreamSynchronize(s));
+  {
+    uint8_t b[96];
+    g1_bytes(proof->U, b);
+    sp.absorb_bytes(b, 96);  // mipp.rs:56
+  }
+  std::vector<Fr> xs_inv;
+  size_t len = C;
+  int round = 0;
+  while (len > 1) {  // mipp.rs:58-120
+    const size_t split = len / 2;
+    // u_l = a[:s] ^ y[s:], u_r = a[s:] ^ y[:s]
+    TPST_HIP(ctx, msm_mont_scalars<Fq>(ctx, A.u(), Y.u() + 8 * split, split, tmp.u(), x1));
+    TPST_HIP(ctx, msm_mont_scalars<Fq>(ctx, A.u() + 24 * split, Y.u(), split, tmp.u(), x1 + 1));
+    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(s, x1, canon.u(), 2));
+    // t_l = e(a[:s], h[s:]), t_r = e(a[s:], h[:s])
+    TPST_HIP(ctx, multi_pairing(ctx->arena, s, A.u(), H.u() + 48 * split, 1, split, (Fq12*)gts.p));
+    TPST_HIP(ctx, multi_pairing(ctx->arena, s, A.u() + 24 * split, H.u(), 1, split, (Fq12*)gts.p + 1));
+    TPST_HIP(ctx, fq12_from_mont(s, (Fq12*)gts.p, canon.u() + 48, 2));
+    uint64_t* ut = proof->comms_u[round][0];
+    TPST_HIP(ctx, hipMemcpyAsync(ut, canon.p, 96, hipMemcpyDeviceToHost, s));
+    TPST_HIP(ctx, hipMemcpyAsync(proof->comms_u[round][1], canon.u() + 24, 96, hipMemcpyDeviceToHost, s));
+    TPST_HIP(ctx, hipMemcpyAsync(proof->comms_t[round][0], canon.u() + 48, 576, hipMemcpyDeviceToHost, s));
+    TPST_HIP(ctx, hipMemcpyAsync(proof->comms_t[round][1], canon.u() + 48 + 144, 576, hipMemcpyDeviceToHost, s));
+    TPST_HIP(ctx, hipStreamSynchronize(s));
+    uint8_t b[96];
+    g1_bytes(proof->comms_u[round][0], b);
+    sp.absorb_bytes(b, 96);
+    g1_bytes(proof->comms_u[round][1], b);
+    sp.absorb_bytes(b, 96);
+    sp.absorb_bytes((const uint8_t*)proof->comms_t[round][0], 576);
+    sp.absorb_bytes((const uint8_t*)proof->comms_t[round][1], 576);
+    uint64_t ci_c[4], c_c[4];
+    sp.challenge(ci_c);  // mipp.rs:101
+    const Fr c_inv = fr_canon(ci_c);
+    const Fr c = fr_inv(c_inv);  // mipp.rs:106
+    fr_out(c, c_c);
+    uint32_t hbuf[24];
+    memcpy(hbuf, c_c, 32);           // c canonical
+    memcpy(hbuf + 8, ci_c, 32);      // c_inv canonical
+    memcpy(hbuf + 16, c_inv.v, 32);  // c_inv Montgomery
+    TPST_HIP(ctx, hipMemcpyAsync(small.p, hbuf, 96, hipMemcpyHostToDevice, s));
+    TPST_HIP(ctx, compress_points<Fq>(s, A.u(), split, small.u()));        // a_l + c a_r
+    TPST_HIP(ctx, compress_fr(s, Y.u(), split, small.u() + 16));           // y_l + c_inv y_r
+    TPST_HIP(ctx, compress_points<Fq2>(s, H.u(), split, small.u() + 8));   // h_l + c_inv h_r
+    TPST_HIP(ctx, hipStreamSynchronize(s));  // small.p is rewritten next round
+    xs_inv.push_back(c_inv);
+    len = split;
+    round++;
+  }
+  TPST_HIP(ctx, affine_from_mont<Fq>(s, A.u(), canon.u(), 1));
+  TPST_HIP(ctx, affine_from_mont<Fq2>(s, H.u(), canon.u() + 24, 1));
+  TPST_HIP(ctx, hipMemcpyAsync(proof->final_a, canon.p, 96, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipMemcpyAsync(proof->final_h, canon.u() + 24, 192, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipStreamSynchronize(s));
+  // p_h evaluations from the challenges (mipp.rs:159-180), then rs and open_g1
+  if (m > 0) {
+    std::vector<uint32_t> evals(C * 8);
+    for (size_t i = 0; i < C; i++) {
+      Fr v = Fr::one();
+      for (int j = 0; j < m; j++)
+        if ((i >> j) & 1) v = mul(v, xs_inv[m - j - 1]);
+      memcpy(&evals[8 * i], v.v, 32);
+    }
+    std::vector<uint32_t> rs(8 * m);
+    for (int i = 0; i < m; i++) {  // mipp.rs:138-141
+      uint64_t c[4];
+      sp.challenge(c);
+      const Fr r = fr_canon(c);
+      memcpy(&rs[8 * i], r.v, 32);
+    }
+    DevBuf de, dr;
+    TPST_HIP(ctx, de.alloc(C * 32));
+    TPST_HIP(ctx, dr.alloc(m * 32));
+    TPST_HIP(ctx, hipMemcpyAsync(de.p, evals.data(), C * 32, hipMemcpyHostToDevice, s));
+    TPST_HIP(ctx, hipMemcpyAsync(dr.p, rs.data(), m * 32, hipMemcpyHostToDevice, s));
+    int rc = pst_open_dev<Fq>(ctx, st->pg_pair, st->nv - m, de.u(), m, dr.u(), x1 + 4);
+    if (rc) return rc;
+    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(s, x1 + 4, canon.u(), m));
+    TPST_HIP(ctx, hipMemcpyAsync(proof->pst_proof_h, canon.p, (size_t)m * 96, hipMemcpyDeviceToHost, s));
+    TPST_HIP(ctx, hipStreamSynchronize(s));
+  }
+  // PST open of q at a_rev (sqrt_pst.rs:218-225)
+  {
+    const int k = p->m_row;
+    std::vector<uint64_t> arev(4 * k);
+    for (int i = 0; i < k; i++) memcpy(&arev[4 * i], point + 4 * (k - 1 - i), 32);
+    DevBuf da;
+    TPST_HIP(ctx, da.alloc(k * 32));
+    TPST_HIP(ctx, hipMemcpyAsync(da.p, arev.data(), k * 32, hipMemcpyHostToDevice, s));
+    TPST_HIP(ctx, fr_to_mont(s, da.u(), da.u(), k));
+    Xyzz<Fq2>* x2 = (Xyzz<Fq2>*)xy.p + 4;
+    int rc = pst_open_dev<Fq2>(ctx, st->ph_pair, st->nv - k, p->q.u(), k, da.u(), x2);
+    if (rc) return rc;
+    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq2>(s, x2, canon.u(), k));
+    TPST_HIP(ctx, hipMemcpyAsync(proof->pst_proof, canon.p, (size_t)k * 192, hipMemcpyDeviceToHost, s));
+    TPST_HIP(ctx, hipStreamSynchronize(s));
+  }
+  sp.store(tr);
+  return TPST_OK;
+}
+
+// -------------------------------------------------------------- verify ---
+// small helpers on host-side canonical points via device MSMs
+template <class F>
+static int small_msm(tpst_ctx* ctx, const std::vector<uint64_t>& pts_canon, const std::vector<uint64_t>& sc,
+                     uint64_t* out) {
+  constexpr size_t PW = 2 * Words<F>::n;
+  const size_t n = sc.size() / 4;
+  hipStream_t s = ctx->stream;
+  DevBuf b, bm, d_s, r, o;
+  TPST_HIP(ctx, b.alloc(n * PW * 4));
+  TPST_HIP(ctx, bm.alloc(n * PW * 4));
+  TPST_HIP(ctx, d_s.alloc(n * 32));
+  TPST_HIP(ctx, r.alloc(sizeof(Xyzz<F>)));
+  TPST_HIP(ctx, o.alloc(PW * 4));
+  TPST_HIP(ctx, hipMemcpyAsync(b.p, pts_canon.data(), n * PW * 4, hipMemcpyHostToDevice, s));
+  TPST_HIP(ctx, hipMemcpyAsync(d_s.p, sc.data(), n * 32, hipMemcpyHostToDevice, s));
+  TPST_HIP(ctx, points_to_mont<F>(s, b.u(), bm.u(), n));
+  TPST_HIP(ctx, msm_var<F>(ctx->arena, s, bm.u(), d_s.u(), n, (Xyzz<F>*)r.p));
+  TPST_HIP(ctx, xyzz_to_affine_canonical<F>(s, (Xyzz<F>*)r.p, o.u(), 1));
+  TPST_HIP(ctx, hipMemcpyAsync(out, o.p, PW * 4, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipStreamSynchronize(s));
+  return TPST_OK;
+}
+
+static int pairing_product(tpst_ctx* ctx, const std::vector<uint64_t>& g1, const std::vector<uint64_t>& g2,
+                           uint64_t* out_gt) {
+  const size_t n = g1.size() / 12;
+  hipStream_t s = ctx->stream;
+  DevBuf a, am, b, bm, f, o;
+  TPST_HIP(ctx, a.alloc(n * 96));
+  TPST_HIP(ctx, am.alloc(n * 96));
+  TPST_HIP(ctx, b.alloc(n * 192));
+  TPST_HIP(ctx, bm.alloc(n * 192));
+  TPST_HIP(ctx, f.alloc(sizeof(Fq12)));
+  TPST_HIP(ctx, o.alloc(576));
+  TPST_HIP(ctx, hipMemcpyAsync(a.p, g1.data(), n * 96, hipMemcpyHostToDevice, s));
+  TPST_HIP(ctx, hipMemcpyAsync(b.p, g2.data(), n * 192, hipMemcpyHostToDevice, s));
+  TPST_HIP(ctx, points_to_mont<Fq>(s, a.u(), am.u(), n));
+  TPST_HIP(ctx, points_to_mont<Fq2>(s, b.u(), bm.u(), n));
+  TPST_HIP(ctx, multi_pairing(ctx->arena, s, am.u(), bm.u(), 1, n, (Fq12*)f.p));
+  TPST_HIP(ctx, fq12_from_mont(s, (Fq12*)f.p, o.u(), 1));
+  TPST_HIP(ctx, hipMemcpyAsync(out_gt, o.p, 576, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipStreamSynchronize(s));
+  return TPST_OK;
+}
+
+static bool gt_is_one(const uint64_t* gt) {
+  if (gt[0] != 1) return false;
+  for (int i = 1; i < 72; i++)
+    if (gt[i]) return false;
+  return true;
+}
+
+static void push(std::vector<uint64_t>& v, const uint64_t* p, size_t n) { v.insert(v.end(), p, p + n); }
+
+extern "C" int tpst_pst_verify(tpst_ctx* ctx, tpst_transcript* tr, int n, const uint64_t* point, const uint64_t* v,
+                               const uint64_t* T, const tpst_open_proof* proof) {
+  if (!ctx || !tr || !point || !v || !T || !proof) return fail(ctx, TPST_E_ARG, "null argument");
+  int m_col, m_row, odd;
+  if (poly_dims(n, m_col, m_row, odd)) return fail(ctx, TPST_E_ARG, "bad num_vars");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  SrsState* st = srs_of(ctx);
+  if (!st) return fail(ctx, TPST_E_STATE, "no SRS loaded");
+  if (st->nv != m_row || proof->m_col != m_col || proof->m_row != m_row) return fail(ctx, TPST_E_ARG, "size mismatch");
+  const uint64_t* flat = st->flat.data();
+  const uint64_t* g = flat;
+  const uint64_t* h = flat + 12;
+  const uint64_t* gmask = flat + tpst_srs_flat_len(st->nv) - 36 * st->nv;
+  const uint64_t* hmask = gmask + 12 * st->nv;
+  const int m = m_col;
+  Sponge sp;
+  sp.load(tr);
+  uint8_t b[96];
+  g1_bytes(proof->U, b);
+  sp.absorb_bytes(b, 96);
+  std::vector<Fr> xs(m), xs_inv(m);
+  Fr final_y = Fr::one();
+  std::vector<uint64_t> exps;  // canonical exponents for the GT pows
+  for (int i = 0; i < m; i++) {  // mipp.rs:207-227
+    g1_bytes(proof->comms_u[i][0], b);
+    sp.absorb_bytes(b, 96);
+    g1_bytes(proof->comms_u[i][1], b);
+    sp.absorb_bytes(b, 96);
+    sp.absorb_bytes((const uint8_t*)proof->comms_t[i][0], 576);
+    sp.absorb_bytes((const uint8_t*)proof->comms_t[i][1], 576);
+    uint64_t cc[4];
+    sp.challenge(cc);
+    xs_inv[i] = fr_canon(cc);
+    xs[i] = fr_inv(xs_inv[i]);
+    const Fr bi = fr_canon(point + 4 * (m_row + i));
+    final_y = mul(final_y, sub(add(Fr::one(), mul(xs_inv[i], bi)), bi));
+  }
+  std::vector<Fr> rs(m);
+  for (int i = 0; i < m; i++) {
+    uint64_t cc[4];
+    sp.challenge(cc);
+    rs[i] = fr_canon(cc);
+  }
+  Fr vh = Fr::one();
+  for (int i = 0; i < m; i++) vh = mul(vh, sub(add(Fr::one(), mul(rs[i], xs_inv[m - i - 1])), rs[i]));
+  auto canon4 = [](const Fr& x) {
+    std::vector<uint64_t> c(4);
+    fr_out(x, c.data());
+    return c;
+  };
+  auto negc = [](const Fr& x) { return sub(Fr::zero(), x); };
+  int rc;
+  // U check: uc = U + sum(c_inv u_l + c u_r) == final_y * final_a
+  {
+    std::vector<uint64_t> pts, sc;
+    push(pts, proof->U, 12);
+    push(sc, canon4(Fr::one()).data(), 4);
+    for (int i = 0; i < m; i++) {
+      push(pts, proof->comms_u[i][0], 12);
+      push(sc, canon4(xs_inv[i]).data(), 4);
+      push(pts, proof->comms_u[i][1], 12);
+      push(sc, canon4(xs[i]).data(), 4);
+    }
+    push(pts, proof->final_a, 12);
+    push(sc, canon4(negc(final_y)).data(), 4);
+    uint64_t res[12];
+    if ((rc = small_msm<Fq>(ctx, pts, sc, res))) return rc;
+    for (int i = 0; i < 12; i++)
+      if (res[i]) return TPST_E_VERIFY;
+  }
+  // T check: T * prod t_l^{c_inv} t_r^{c} == e(final_a, final_h)
+  {
+    const size_t k = 2 * m;
+    std::vector<uint32_t> bases;
+    std::vector<uint64_t> ex;
+    for (int i = 0; i < m; i++) {
+      for (int j = 0; j < 2; j++) {
+        Fq12 f;
+        Fq* c = reinterpret_cast<Fq*>(&f);
+        for (int q = 0; q < 12; q++) c[q] = fq_canon(proof->comms_t[i][j] + 6 * q);
+        const uint32_t* fw = reinterpret_cast<const uint32_t*>(&f);
+        bases.insert(bases.end(), fw, fw + sizeof(Fq12) / 4);
+        push(ex, canon4(j == 0 ? xs_inv[i] : xs[i]).data(), 4);
+      }
+    }
+    Fq12 acc;
+    {
+      Fq* c = reinterpret_cast<Fq*>(&acc);
+      for (int q = 0; q < 12; q++) c[q] = fq_canon(T + 6 * q);
+    }
+    if (k) {
+      hipStream_t s = ctx->stream;
+      DevBuf db, de, dout;
+      TPST_HIP(ctx, db.alloc(k * sizeof(Fq12)));
+      TPST_HIP(ctx, de.alloc(k * 32));
+      TPST_HIP(ctx, dout.alloc(k * sizeof(Fq12)));
+      TPST_HIP(ctx, hipMemcpyAsync(db.p, bases.data(), k * sizeof(Fq12), hipMemcpyHostToDevice, s));
+      TPST_HIP(ctx, hipMemcpyAsync(de.p, ex.data(), k * 32, hipMemcpyHostToDevice, s));
+      TPST_HIP(ctx, gt_pow(s, (Fq12*)db.p, de.u(), k, (Fq12*)dout.p));
+      std::vector<Fq12> pw(k);
+      TPST_HIP(ctx, hipMemcpyAsync(pw.data(), dout.p, k * sizeof(Fq12), hipMemcpyDeviceToHost, s));
+      TPST_HIP(ctx, hipStreamSynchronize(s));
+      for (auto& x : pw) acc = mul(acc, x);
+    }
+    uint64_t ft[72];
+    std::vector<uint64_t> a1(proof->final_a, proof->final_a + 12), a2(proof->final_h, proof->final_h + 24);
+    if ((rc = pairing_product(ctx, a1, a2, ft))) return rc;
+    const Fq* c = reinterpret_cast<const Fq*>(&acc);
+    for (int q = 0; q < 12; q++) {
+      uint64_t lim[6];
+      fq_out(c[q], lim);
+      if (memcmp(lim, ft + 6 * q, 48) != 0) return TPST_E_VERIFY;
+    }
+  }
+  // check_2 (mipp.rs:307): e(g, C_h - h^v) * prod e(pi_i, h^{rs_i} - h_mask[nv-m+i]) == 1
+  {
+    std::vector<uint64_t> g1s, g2s;
+    uint64_t q[24];
+    std::vector<uint64_t> pts, sc;
+    push(pts, proof->final_h, 24);
+    push(sc, canon4(Fr::one()).data(), 4);
+    push(pts, h, 24);
+    push(sc, canon4(negc(vh)).data(), 4);
+    if ((rc = small_msm<Fq2>(ctx, pts, sc, q))) return rc;
+    push(g1s, g, 12);
+    push(g2s, q, 24);
+    for (int i = 0; i < m; i++) {
+      pts.clear();
+      sc.clear();
+      push(pts, h, 24);
+      push(sc, canon4(rs[i]).data(), 4);
+      push(pts, hmask + 24 * (st->nv - m + i), 24);
+      push(sc, canon4(negc(Fr::one())).data(), 4);
+      if ((rc = small_msm<Fq2>(ctx, pts, sc, q))) return rc;
+      push(g1s, proof->pst_proof_h[i], 12);
+      push(g2s, q, 24);
+    }
+    uint64_t gt[72];
+    if ((rc = pairing_product(ctx, g1s, g2s, gt))) return rc;
+    if (!gt_is_one(gt)) return TPST_E_VERIFY;
+  }
+  // MultilinearPC::check (sqrt_pst.rs:261): e(U - g^v, h) * prod e(g^{a_i} - g_mask_i, pi_i) == 1
+  {
+    std::vector<uint64_t> g1s, g2s, pts, sc;
+    uint64_t q[12];
+    push(pts, proof->U, 12);
+    push(sc, canon4(Fr::one()).data(), 4);
+    push(pts, g, 12);
+    push(sc, canon4(negc(fr_canon(v))).data(), 4);
+    if ((rc = small_msm<Fq>(ctx, pts, sc, q))) return rc;
+    push(g1s, q, 12);
+    push(g2s, h, 24);
+    for (int i = 0; i < m_row; i++) {
+      pts.clear();
+      sc.clear();
+      push(pts, g, 12);
+      push(sc, point + 4 * (m_row - 1 - i), 4);  // a_rev[i]
+      push(pts, gmask + 12 * i, 12);
+      push(sc, canon4(negc(Fr::one())).data(), 4);
+      if ((rc = small_msm<Fq>(ctx, pts, sc, q))) return rc;
+      push(g1s, q, 12);
+      push(g2s, proof->pst_proof[i], 24);
+    }
+    uint64_t gt[72];
+    if ((rc = pairing_product(ctx, g1s, g2s, gt))) return rc;
+    if (!gt_is_one(gt)) return TPST_E_VERIFY;
+  }
+  sp.store(tr);
+  return TPST_OK;
+}

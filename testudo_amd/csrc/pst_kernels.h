@@ -1,0 +1,50 @@
+// Device kernels for the sqrt-PST protocol layer (pst.hip): Fr vector
+// kernels (chi tables, get_q mat-vec, PST quotient recurrence, MIPP y fold),
+// MIPP compress (fixed-scalar point folds) and SRS generation.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "msm.h"
+#include "pairing_kernels.h"
+
+namespace tpst {
+
+// canonical <-> Montgomery Fr vectors (8 u32 each)
+hipError_t fr_to_mont(hipStream_t s, const uint32_t* in, uint32_t* out, size_t n);
+hipError_t fr_from_mont(hipStream_t s, const uint32_t* in, uint32_t* out, size_t n);
+
+// out[i] = chi_i(b) = prod_j (bit (m-1-j) of i ? b_j : 1-b_j), b Montgomery (sqrt_pst.rs:152-166)
+hipError_t chi_table(hipStream_t s, const uint32_t* d_b, int m, uint32_t* d_out);
+
+// q[j] = sum_i Z[(j << m_col) | i] * chis[i]  (sqrt_pst.rs:93-96); Z canonical, chis/q Montgomery
+hipError_t get_q(hipStream_t s, const uint32_t* d_Z, int m_col, int m_row, const uint32_t* d_chis, uint32_t* d_q);
+
+// v = sum_j x[j] * y[j] (Montgomery), one value
+hipError_t fr_dot(hipStream_t s, const uint32_t* d_x, const uint32_t* d_y, size_t n, uint32_t* d_v);
+
+// PST open step: from r (2h, Montgomery) and pt (Montgomery
+// scalar at d_pt): q_can[b] = canonical(r[2b+1]-r[2b]), r_next[b] = r[2b](1-pt)+r[2b+1]pt
+hipError_t pst_step(hipStream_t s, const uint32_t* d_r, size_t half, const uint32_t* d_pt, uint32_t* d_qcan,
+                    uint32_t* d_rnext);
+
+// MIPP compress (mipp.rs:354-383): v[i] = v[i] + k * v[i+split] for i < split;
+// k is a canonical Fr at d_k.  In place; points stay affine Montgomery.
+template <class F>
+hipError_t compress_points(hipStream_t s, uint32_t* d_v, size_t split, const uint32_t* d_k);
+hipError_t compress_fr(hipStream_t s, uint32_t* d_y, size_t split, const uint32_t* d_kmont);
+
+// out[i] = k_i * P for a fixed affine (Montgomery) point P at d_p; scalars canonical
+template <class F>
+hipError_t fixed_base_mul(hipStream_t s, const uint32_t* d_p, const uint32_t* d_scalars, size_t n, uint32_t* d_out);
+
+// pair sums for the halved PST-open MSM: out[b] = in[2b] + in[2b+1] (affine)
+template <class F>
+hipError_t pair_sum(hipStream_t s, const uint32_t* d_in, size_t half, uint32_t* d_out);
+
+// batch XYZZ -> affine (Montgomery)
+template <class F>
+hipError_t xyzz_to_affine_mont(hipStream_t s, const Xyzz<F>* d_in, uint32_t* d_out, size_t n);
+
+// GT: out[i] = base[i]^(canonical exps[i]) , n independent
+hipError_t gt_pow(hipStream_t s, const Fq12* d_base, const uint32_t* d_exps, size_t n, Fq12* d_out);
+
+}  // namespace tpst

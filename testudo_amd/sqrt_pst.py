@@ -1,0 +1,188 @@
+"""Host-side mirror of Testudo's sqrt-PST surface over libtpst.
+
+Reference: ``src/sqrt_pst.rs:14-265`` (``Polynomial``), ``src/mipp.rs``
+(``MippProof``) and ``src/poseidon_transcript.rs`` (``PoseidonTranscript``).
+Names and argument meaning follow the reference; every computation runs in
+libtpst (HIP on gfx950) -- this module only marshals arrays:
+
+* field elements are numpy ``uint64`` arrays of canonical little-endian limbs
+  (Fr: 4, Fq: 6), G1 affine 12 limbs, G2 affine 24, GT 72 (include/tpst.h);
+* errors raise ``TpstError``; ``verify`` returns ``False`` on an invalid proof
+  where the reference would ``assert!`` (sqrt_pst.rs:250, mipp.rs:308-317).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from .encoding import ptr
+from .engine import Context, TpstError
+
+
+def _u64(a, shape=None):
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    return a if shape is None else a.reshape(shape)
+
+
+class PoseidonTranscript:
+    """PoseidonTranscript<Fq> with get_bls12377_fq_params (parameters.rs:309-338)."""
+
+    def __init__(self):
+        self.lib = _lib.load()
+        self.t = _lib.Transcript()
+        self.lib.tpst_transcript_init(C.byref(self.t))
+
+    def append_g1(self, p):
+        self.lib.tpst_transcript_append_g1(C.byref(self.t), ptr(_u64(p, (12,))))
+
+    def append_gt(self, f):
+        self.lib.tpst_transcript_append_gt(C.byref(self.t), ptr(_u64(f, (72,))))
+
+    def challenge_scalar(self) -> np.ndarray:
+        out = np.zeros(4, dtype=np.uint64)
+        self.lib.tpst_transcript_challenge(C.byref(self.t), ptr(out))
+        return out
+
+    def state(self) -> np.ndarray:
+        return np.ctypeslib.as_array(self.t.state).reshape(18).copy()
+
+
+@dataclass
+class MippProof:
+    """mipp.rs:21-28."""
+    comms_t: np.ndarray      # (m_col, 2, 72) GT
+    comms_u: np.ndarray      # (m_col, 2, 12) G1
+    final_a: np.ndarray      # (12,)
+    final_h: np.ndarray      # (24,)
+    pst_proof_h: np.ndarray  # (m_col, 12) ProofG1
+
+
+def srs_setup(ctx: Context, nv: int, seed: int):
+    """MultilinearPC::setup + trim to nv variables, trapdoor from ``seed``."""
+    ctx.check(ctx.lib.tpst_srs_setup(ctx.h, nv, seed), "tpst_srs_setup")
+
+
+def srs_load(ctx: Context, nv: int, flat: np.ndarray):
+    flat = _u64(flat)
+    if len(flat) != ctx.lib.tpst_srs_flat_len(nv):
+        raise TpstError("SRS flat length mismatch")
+    ctx.check(ctx.lib.tpst_srs_load(ctx.h, nv, ptr(flat)), "tpst_srs_load")
+
+
+def srs_export(ctx: Context, nv: int) -> np.ndarray:
+    out = np.zeros(ctx.lib.tpst_srs_flat_len(nv), dtype=np.uint64)
+    ctx.check(ctx.lib.tpst_srs_export(ctx.h, ptr(out)), "tpst_srs_export")
+    return out
+
+
+def fr_stream(seed: int, n: int, start: int = 0):
+    lib = _lib.load()
+    out = np.zeros((n, 4), dtype=np.uint64)
+    nxt = lib.tpst_fr_stream(seed, n, start, ptr(out))
+    return out, nxt
+
+
+class Polynomial:
+    """sqrt_pst.rs:14-20 -- 2^n evaluations viewed as 2^m_col rows of 2^m_row."""
+
+    def __init__(self, ctx: Context, handle, n: int, keep=None):
+        self.ctx = ctx
+        self.h = handle
+        self.n = n
+        self.m_col = n // 2
+        self.m_row = n - self.m_col
+        self.odd = n % 2
+        self._keep = keep
+
+    @classmethod
+    def from_evaluations(cls, ctx: Context, Z: np.ndarray) -> "Polynomial":
+        """sqrt_pst.rs:32-75."""
+        Z = _u64(Z).reshape(-1, 4)
+        n = int(len(Z)).bit_length() - 1
+        if 1 << n != len(Z):
+            raise TpstError("evaluation count must be a power of two")
+        h = C.c_void_p()
+        ctx.check(ctx.lib.tpst_poly_from_evaluations(ctx.h, ptr(Z), n, C.byref(h)), "from_evaluations")
+        return cls(ctx, h, n)
+
+    @classmethod
+    def from_device(cls, ctx: Context, d_ptr: int, n: int, keep=None) -> "Polynomial":
+        h = C.c_void_p()
+        ctx.check(ctx.lib.tpst_poly_from_evaluations_dev(ctx.h, C.c_void_p(d_ptr), n, C.byref(h)),
+                  "from_evaluations_dev")
+        return cls(ctx, h, n, keep)
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.ctx.lib.tpst_poly_free(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def eval(self, point) -> np.ndarray:
+        """sqrt_pst.rs:105-115 (computes and caches q on first use)."""
+        point = _u64(point, (self.n, 4))
+        out = np.zeros(4, dtype=np.uint64)
+        self.ctx.check(self.ctx.lib.tpst_poly_eval(self.ctx.h, self.h, ptr(point), ptr(out)), "eval")
+        return out
+
+    def commit(self):
+        """sqrt_pst.rs:117-149 -> (comm_list (2^m_col, 12), T (72,))."""
+        comms = np.zeros((1 << self.m_col, 12), dtype=np.uint64)
+        T = np.zeros(72, dtype=np.uint64)
+        self.ctx.check(self.ctx.lib.tpst_poly_commit(self.ctx.h, self.h, ptr(comms), ptr(T)), "commit")
+        return comms, T
+
+    def commit_dev(self, d_comms: int, d_T: int):
+        self.ctx.check(self.ctx.lib.tpst_poly_commit_dev(self.ctx.h, self.h, C.c_void_p(d_comms),
+                                                         C.c_void_p(d_T)), "commit_dev")
+
+    def open(self, transcript: PoseidonTranscript, comm_list, point, T):
+        """sqrt_pst.rs:168-230 -> (U, pst_proof (m_row, 24), MippProof)."""
+        comm_list = _u64(comm_list, (1 << self.m_col, 12))
+        point = _u64(point, (self.n, 4))
+        T = _u64(T, (72,))
+        pr = _lib.OpenProof()
+        self.ctx.check(self.ctx.lib.tpst_poly_open(self.ctx.h, self.h, C.byref(transcript.t), ptr(comm_list),
+                                                   ptr(point), ptr(T), C.byref(pr)), "open")
+        return _unpack(pr)
+
+
+def _unpack(pr):
+    mc, mr = pr.m_col, pr.m_row
+    arr = lambda x: np.ctypeslib.as_array(x).copy()  # noqa: E731
+    U = arr(pr.U)
+    pst = arr(pr.pst_proof)[:mr]
+    mipp = MippProof(comms_t=arr(pr.comms_t)[:mc], comms_u=arr(pr.comms_u)[:mc], final_a=arr(pr.final_a),
+                     final_h=arr(pr.final_h), pst_proof_h=arr(pr.pst_proof_h)[:mc])
+    return U, pst, mipp
+
+
+def pack_proof(n, U, pst_proof, mipp: MippProof):
+    pr = _lib.OpenProof()
+    pr.m_col, pr.m_row = n // 2, n - n // 2
+    np.ctypeslib.as_array(pr.U)[:] = _u64(U, (12,))
+    np.ctypeslib.as_array(pr.pst_proof)[:pr.m_row] = _u64(pst_proof, (pr.m_row, 24))
+    np.ctypeslib.as_array(pr.comms_t)[:pr.m_col] = _u64(mipp.comms_t, (pr.m_col, 2, 72))
+    np.ctypeslib.as_array(pr.comms_u)[:pr.m_col] = _u64(mipp.comms_u, (pr.m_col, 2, 12))
+    np.ctypeslib.as_array(pr.final_a)[:] = _u64(mipp.final_a, (12,))
+    np.ctypeslib.as_array(pr.final_h)[:] = _u64(mipp.final_h, (24,))
+    np.ctypeslib.as_array(pr.pst_proof_h)[:pr.m_col] = _u64(mipp.pst_proof_h, (pr.m_col, 12))
+    return pr
+
+
+def verify(ctx: Context, transcript: PoseidonTranscript, U, point, v, pst_proof, mipp: MippProof, T) -> bool:
+    """Polynomial::verify (sqrt_pst.rs:232-264)."""
+    point = _u64(point).reshape(-1, 4)
+    n = len(point)
+    pr = pack_proof(n, U, pst_proof, mipp)
+    rc = ctx.lib.tpst_pst_verify(ctx.h, C.byref(transcript.t), n, ptr(point), ptr(_u64(v, (4,))),
+                                 ptr(_u64(T, (72,))), C.byref(pr))
+    if rc == -5:
+        return False
+    ctx.check(rc, "verify")
+    return True
