@@ -10,6 +10,7 @@ from __future__ import annotations
 import concurrent.futures as cf
 import glob
 import os
+import re
 import subprocess
 import sys
 
@@ -30,9 +31,17 @@ def _deps_mtime() -> float:
     return max(os.path.getmtime(f) for f in files)
 
 
+def _src_mtime(src: str) -> float:
+    """mtime of a .hip file and of any .hip it #includes (msm_g2.hip)."""
+    t = os.path.getmtime(src)
+    for inc in re.findall(r'#include "([^"]+\.hip)"', open(src).read()):
+        t = max(t, os.path.getmtime(os.path.join(os.path.dirname(src), inc)))
+    return t
+
+
 def _compile(src: str, hdr_mtime: float) -> str:
     obj = os.path.join(BUILD, os.path.basename(src) + ".o")
-    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_mtime):
+    if os.path.exists(obj) and os.path.getmtime(obj) >= max(_src_mtime(src), hdr_mtime):
         return obj
     cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj + ".tmp"]
     r = subprocess.run(cmd, capture_output=True, text=True)

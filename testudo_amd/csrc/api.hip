@@ -151,7 +151,7 @@ extern "C" int tpst_multi_pairing(tpst_ctx* ctx, const uint64_t* g1, const uint6
 
 // ------------------------------------------------- generator multiples ----
 template <class F>
-__global__ void k_mul_gen(const uint32_t* __restrict__ scalars, size_t n, uint32_t* __restrict__ out, int canonical) {
+__global__ void __launch_bounds__(64, 1) k_mul_gen(const uint32_t* __restrict__ scalars, size_t n, uint32_t* __restrict__ out, int canonical) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   Affine<F> g;

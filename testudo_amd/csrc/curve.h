@@ -157,7 +157,7 @@ template <class F>
 TPST_HD Xyzz<F> neg(const Xyzz<F>& p) { return {p.X, neg(p.Y), p.ZZ, p.ZZZ}; }
 
 template <class F>
-TPST_NI Affine<F> to_affine(const Xyzz<F>& p) {
+TPST_HD Affine<F> to_affine(const Xyzz<F>& p) {
   if (is_zero(p.ZZ)) return Affine<F>::inf();
   const F t = inv(mul(p.ZZ, p.ZZZ));
   const F izz = mul(t, p.ZZZ);   // 1/ZZ
@@ -181,7 +181,7 @@ TPST_NI bool eq(const Xyzz<F>& a, const Xyzz<F>& b) {
 // `nbits` bits held in 32-bit words.  Used for the small per-element products
 // (MIPP compress, SRS setup, verifier), not for MSMs.
 template <class F>
-TPST_NI Xyzz<F> scalar_mul(const Affine<F>& a, const uint32_t* k, int nbits) {
+TPST_HD Xyzz<F> scalar_mul(const Affine<F>& a, const uint32_t* k, int nbits) {
   Xyzz<F> acc = Xyzz<F>::inf();
   for (int i = nbits - 1; i >= 0; i--) {
     acc = dbl(acc);
@@ -191,7 +191,7 @@ TPST_NI Xyzz<F> scalar_mul(const Affine<F>& a, const uint32_t* k, int nbits) {
 }
 
 template <class F>
-TPST_NI Xyzz<F> scalar_mul_xyzz(const Xyzz<F>& a, const uint32_t* k, int nbits) {
+TPST_HD Xyzz<F> scalar_mul_xyzz(const Xyzz<F>& a, const uint32_t* k, int nbits) {
   Xyzz<F> acc = Xyzz<F>::inf();
   for (int i = nbits - 1; i >= 0; i--) {
     acc = dbl(acc);

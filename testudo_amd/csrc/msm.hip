@@ -11,27 +11,6 @@ namespace tpst {
     if (_e != hipSuccess) return _e;         \
   } while (0)
 
-hipError_t Arena::reserve(size_t bytes) {
-  if (bytes <= cap) return hipSuccess;
-  if (base) {
-    hipError_t e = hipFree(base);
-    if (e != hipSuccess) return e;
-    base = nullptr;
-    cap = 0;
-  }
-  size_t want = bytes + (bytes >> 3);
-  hipError_t e = hipMalloc(&base, want);
-  if (e != hipSuccess) return e;
-  cap = want;
-  return hipSuccess;
-}
-
-void Arena::release() {
-  if (base) (void)hipFree(base);
-  base = nullptr;
-  cap = off = 0;
-}
-
 static inline unsigned grid_for(size_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
 
 static inline int bit_length(uint64_t v) {
@@ -41,25 +20,6 @@ static inline int bit_length(uint64_t v) {
     v >>= 1;
   }
   return b;
-}
-
-int msm_window_bits(size_t n) {
-  // 16-bit signed windows are the sweet spot for ~2^18..2^22 points; smaller
-  // inputs use smaller windows so buckets stay populated.
-  int lg = bit_length(n ? n - 1 : 0);
-  if (lg >= 20) return 16;
-  if (lg >= 16) return 13;
-  if (lg >= 12) return 10;
-  if (lg >= 8) return 7;
-  return 4;
-}
-
-int batch_window_bits(size_t N) {
-  int lg = bit_length(N ? N - 1 : 0);
-  if (lg >= 12) return 12;
-  if (lg >= 10) return 10;
-  if (lg >= 6) return 7;
-  return 4;
 }
 
 // number of signed-digit windows: ceil(254 / c) keeps the top digit < 2^(c-1)
@@ -93,7 +53,7 @@ __device__ __forceinline__ void load_scalar(const uint32_t* p, uint32_t* s) {
 }
 
 // ------------------------------------------------------ K2 decomposition --
-__global__ void k_decompose_var(const uint32_t* __restrict__ scalars, size_t n, int c, int W,
+static __global__ void k_decompose_var(const uint32_t* __restrict__ scalars, size_t n, int c, int W,
                                 uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -114,7 +74,7 @@ __global__ void k_decompose_var(const uint32_t* __restrict__ scalars, size_t n, 
   }
 }
 
-__global__ void k_bucket_bounds(const uint32_t* __restrict__ keys, size_t m, uint32_t sent,
+static __global__ void k_bucket_bounds(const uint32_t* __restrict__ keys, size_t m, uint32_t sent,
                                 uint32_t* __restrict__ bstart, uint32_t* __restrict__ bend) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
@@ -126,7 +86,7 @@ __global__ void k_bucket_bounds(const uint32_t* __restrict__ keys, size_t m, uin
 
 // one thread per bucket: sum its (signed) points with XYZZ mixed additions
 template <class F>
-__global__ void k_bucket_acc(const uint32_t* __restrict__ vals, const uint32_t* __restrict__ bstart,
+__global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2)) k_bucket_acc(const uint32_t* __restrict__ vals, const uint32_t* __restrict__ bstart,
                              const uint32_t* __restrict__ bend, const uint32_t* __restrict__ bases,
                              size_t nbk, Xyzz<F>* __restrict__ out) {
   const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -145,7 +105,7 @@ __global__ void k_bucket_acc(const uint32_t* __restrict__ vals, const uint32_t* 
 // segment t of group g: sum_{b in seg} (b+1) * S_b with b the bucket index
 // inside the group (bucket b holds digit value b+1)
 template <class F>
-__global__ void k_seg_reduce(const Xyzz<F>* __restrict__ buckets, uint32_t nb, uint32_t L, size_t nseg,
+__global__ void __launch_bounds__(64, 1) k_seg_reduce(const Xyzz<F>* __restrict__ buckets, uint32_t nb, uint32_t L, size_t nseg,
                              Xyzz<F>* __restrict__ seg_out) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nseg) return;
@@ -186,7 +146,7 @@ __global__ void __launch_bounds__(BS) k_group_reduce(const Xyzz<F>* __restrict__
 
 // Horner over windows: sum_w 2^(c w) G_w
 template <class F>
-__global__ void k_window_combine(const Xyzz<F>* __restrict__ win, int W, int c, Xyzz<F>* __restrict__ out) {
+__global__ void __launch_bounds__(64, 1) k_window_combine(const Xyzz<F>* __restrict__ win, int W, int c, Xyzz<F>* __restrict__ out) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   Xyzz<F> acc = load_xyzz(win, W - 1);
   for (int w = W - 2; w >= 0; w--) {
@@ -219,7 +179,7 @@ __global__ void k_affine_from_mont(const uint32_t* __restrict__ in, uint32_t* __
 }
 
 template <class F>
-__global__ void k_xyzz_to_affine_canonical(const Xyzz<F>* __restrict__ in, uint32_t* __restrict__ out, size_t n) {
+__global__ void __launch_bounds__(64, 1) k_xyzz_to_affine_canonical(const Xyzz<F>* __restrict__ in, uint32_t* __restrict__ out, size_t n) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   Affine<F> a = to_affine(load_xyzz(in, i));
@@ -312,9 +272,50 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   return hipGetLastError();
 }
 
+#ifndef TPST_MSM_G2_ONLY
+hipError_t Arena::reserve(size_t bytes) {
+  if (bytes <= cap) return hipSuccess;
+  if (base) {
+    hipError_t e = hipFree(base);
+    if (e != hipSuccess) return e;
+    base = nullptr;
+    cap = 0;
+  }
+  size_t want = bytes + (bytes >> 3);
+  hipError_t e = hipMalloc(&base, want);
+  if (e != hipSuccess) return e;
+  cap = want;
+  return hipSuccess;
+}
+
+void Arena::release() {
+  if (base) (void)hipFree(base);
+  base = nullptr;
+  cap = off = 0;
+}
+
+int msm_window_bits(size_t n) {
+  // 16-bit signed windows are the sweet spot for ~2^18..2^22 points; smaller
+  // inputs use smaller windows so buckets stay populated.
+  int lg = bit_length(n ? n - 1 : 0);
+  if (lg >= 20) return 16;
+  if (lg >= 16) return 13;
+  if (lg >= 12) return 10;
+  if (lg >= 8) return 7;
+  return 4;
+}
+
+int batch_window_bits(size_t N) {
+  int lg = bit_length(N ? N - 1 : 0);
+  if (lg >= 12) return 12;
+  if (lg >= 10) return 10;
+  if (lg >= 6) return 7;
+  return 4;
+}
+
 // ------------------------------------------------------------------ K1 ---
 // T[w][j] = 2^(c w) B_j, one thread per base
-__global__ void k_build_tables(const uint32_t* __restrict__ bases, size_t N, int c, int W, uint32_t* __restrict__ table) {
+__global__ void __launch_bounds__(64, 1) k_build_tables(const uint32_t* __restrict__ bases, size_t N, int c, int W, uint32_t* __restrict__ table) {
   const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= N) return;
   G1A p = load_affine<Fq>(bases, j);
@@ -437,14 +438,17 @@ hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint3
   return reduce_buckets<Fq>(ar, s, buckets, rows, nb, d_out);
 }
 
-// explicit instantiations
+// explicit instantiations (G1)
 template hipError_t msm_var<Fq>(Arena&, hipStream_t, const uint32_t*, const uint32_t*, size_t, Xyzz<Fq>*);
-template hipError_t msm_var<Fq2>(Arena&, hipStream_t, const uint32_t*, const uint32_t*, size_t, Xyzz<Fq2>*);
 template hipError_t points_to_mont<Fq>(hipStream_t, const uint32_t*, uint32_t*, size_t);
-template hipError_t points_to_mont<Fq2>(hipStream_t, const uint32_t*, uint32_t*, size_t);
 template hipError_t affine_from_mont<Fq>(hipStream_t, const uint32_t*, uint32_t*, size_t);
-template hipError_t affine_from_mont<Fq2>(hipStream_t, const uint32_t*, uint32_t*, size_t);
 template hipError_t xyzz_to_affine_canonical<Fq>(hipStream_t, const Xyzz<Fq>*, uint32_t*, size_t);
+#else
+// explicit instantiations (G2)
+template hipError_t msm_var<Fq2>(Arena&, hipStream_t, const uint32_t*, const uint32_t*, size_t, Xyzz<Fq2>*);
+template hipError_t points_to_mont<Fq2>(hipStream_t, const uint32_t*, uint32_t*, size_t);
+template hipError_t affine_from_mont<Fq2>(hipStream_t, const uint32_t*, uint32_t*, size_t);
 template hipError_t xyzz_to_affine_canonical<Fq2>(hipStream_t, const Xyzz<Fq2>*, uint32_t*, size_t);
+#endif
 
 }  // namespace tpst

@@ -107,7 +107,7 @@ hipError_t pst_step(hipStream_t s, const uint32_t* d_r, size_t half, const uint3
 }
 
 template <class F>
-__global__ void k_compress(uint32_t* __restrict__ v, size_t split, const uint32_t* __restrict__ k) {
+__global__ void __launch_bounds__(64, 1) k_compress(uint32_t* __restrict__ v, size_t split, const uint32_t* __restrict__ k) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= split) return;
   uint32_t sc[8];
@@ -140,7 +140,7 @@ hipError_t compress_fr(hipStream_t s, uint32_t* d_y, size_t split, const uint32_
 }
 
 template <class F>
-__global__ void k_fixed_base(const uint32_t* __restrict__ p, const uint32_t* __restrict__ scalars, size_t n,
+__global__ void __launch_bounds__(64, 1) k_fixed_base(const uint32_t* __restrict__ p, const uint32_t* __restrict__ scalars, size_t n,
                              uint32_t* __restrict__ out) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -159,7 +159,7 @@ hipError_t fixed_base_mul(hipStream_t s, const uint32_t* d_p, const uint32_t* d_
 }
 
 template <class F>
-__global__ void k_pair_sum(const uint32_t* __restrict__ in, size_t half, uint32_t* __restrict__ out) {
+__global__ void __launch_bounds__(64, 1) k_pair_sum(const uint32_t* __restrict__ in, size_t half, uint32_t* __restrict__ out) {
   const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= half) return;
   Xyzz<F> a = to_xyzz(load_affine<F>(in, 2 * b));
@@ -175,7 +175,7 @@ hipError_t pair_sum(hipStream_t s, const uint32_t* d_in, size_t half, uint32_t* 
 }
 
 template <class F>
-__global__ void k_xyzz_to_affine_mont(const Xyzz<F>* __restrict__ in, uint32_t* __restrict__ out, size_t n) {
+__global__ void __launch_bounds__(64, 1) k_xyzz_to_affine_mont(const Xyzz<F>* __restrict__ in, uint32_t* __restrict__ out, size_t n) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   store_affine(out, i, to_affine(load_xyzz(in, i)));
