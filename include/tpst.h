@@ -145,6 +145,13 @@ int tpst_g1_mul_generator_dev(tpst_ctx* ctx, const void* d_scalars, size_t n, vo
  * threads x `iters` dependent ops each; returns kernel milliseconds. */
 int tpst_microbench(tpst_ctx* ctx, int kind, size_t threads, int iters, double* ms);
 
+/* Per-stage HIP-event timing of the MSM pipeline on the context's stream.
+ * stage: 0 decompose, 1 sort, 2 bucket bounds, 3 bucket accumulation (the
+ * dominant kernel), 4 bucket reduction, 5 window combine, 6 K1 row sort. */
+int tpst_profile_enable(tpst_ctx* ctx, int on);
+int tpst_profile_reset(tpst_ctx* ctx);
+int tpst_profile_read(tpst_ctx* ctx, int stage, double* total_ms, uint64_t* launches);
+
 #ifdef __cplusplus
 }
 #endif

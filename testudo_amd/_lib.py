@@ -49,6 +49,9 @@ PROTOTYPES = [
     ("tpst_poly_commit_dev", C.c_int, [_vp, _vp, _vp, _vp]),
     ("tpst_poly_open", C.c_int, [_vp, _vp, _vp, _u64p, _u64p, _u64p, _vp]),
     ("tpst_pst_verify", C.c_int, [_vp, _vp, C.c_int, _u64p, _u64p, _u64p, _vp]),
+    ("tpst_profile_enable", C.c_int, [_vp, C.c_int]),
+    ("tpst_profile_reset", C.c_int, [_vp]),
+    ("tpst_profile_read", C.c_int, [_vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
 ]
 
 MAX_VARS = 20

@@ -38,6 +38,7 @@ extern "C" int tpst_create(int device, tpst_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return TPST_E_HIP;
   tpst_ctx* c = new tpst_ctx();
   c->device = device;
+  c->arena.prof = &c->prof;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return TPST_E_HIP;
@@ -254,5 +255,32 @@ extern "C" int tpst_microbench(tpst_ctx* ctx, int kind, size_t threads, int iter
   *ms = f;
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
+  return TPST_OK;
+}
+
+// ------------------------------------------------------ stage profiling ----
+extern "C" int tpst_profile_enable(tpst_ctx* ctx, int on) {
+  if (!ctx) return TPST_E_ARG;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->prof.on = on != 0;
+  return TPST_OK;
+}
+
+extern "C" int tpst_profile_reset(tpst_ctx* ctx) {
+  if (!ctx) return TPST_E_ARG;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->prof.collect();
+  ctx->prof.reset();
+  return TPST_OK;
+}
+
+extern "C" int tpst_profile_read(tpst_ctx* ctx, int stage, double* total_ms, uint64_t* launches) {
+  if (!ctx || !total_ms || !launches || stage < 0 || stage >= N_STAGES) return fail(ctx, TPST_E_ARG, "bad stage");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->prof.collect();
+  *total_ms = ctx->prof.total_ms[stage];
+  *launches = ctx->prof.count[stage];
   return TPST_OK;
 }

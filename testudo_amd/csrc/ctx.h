@@ -14,6 +14,7 @@ struct tpst_ctx {
   tpst::Arena arena;   // kernel scratch (reset per primitive)
   tpst::Arena io;      // staging for host-pointer entry points
   tpst::Arena arena2;  // scratch for nested primitives (open / MIPP)
+  tpst::Profiler prof; // stage timing (tpst_profile_*)
 };
 
 void tpst_release_pst_state(tpst_ctx* ctx);

@@ -17,12 +17,31 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <vector>
 #include "curve.h"
 
 namespace tpst {
 
+// Optional per-stage HIP-event timing of the MSM pipeline (the bench's
+// roofline needs the dominant kernel's own duration on the stream it runs on).
+enum MsmStage { ST_DECOMPOSE = 0, ST_SORT, ST_BOUNDS, ST_BUCKET_ACC, ST_REDUCE, ST_COMBINE, ST_BATCH_SORT, N_STAGES };
+
+struct Profiler {
+  bool on = false;
+  std::vector<hipEvent_t> ev[N_STAGES];  // begin/end pairs
+  size_t used[N_STAGES] = {};
+  double total_ms[N_STAGES] = {};
+  uint64_t count[N_STAGES] = {};
+  void begin(int st, hipStream_t s);
+  void end(int st, hipStream_t s);
+  void collect();  // caller synchronised the stream
+  void reset();
+  ~Profiler();
+};
+
 // grow-only device scratch arena; reset() per call, never freed mid-call
 struct Arena {
+  Profiler* prof = nullptr;
   char* base = nullptr;
   size_t cap = 0;
   size_t off = 0;

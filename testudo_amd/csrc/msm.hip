@@ -258,18 +258,34 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   Xyzz<F>* win = ar.take<Xyzz<F>>(W);
   void* tmp = ar.take<char>(sort_bytes);
 
+  Profiler* pf = ar.prof;
+  Profiler dummy;
+  if (!pf) pf = &dummy;
+  pf->begin(ST_DECOMPOSE, s);
   k_decompose_var<<<grid_for(n, 256), 256, 0, s>>>(d_scalars, n, c, W, keys, vals);
   TPST_TRY(hipGetLastError());
+  pf->end(ST_DECOMPOSE, s);
+  pf->begin(ST_SORT, s);
   TPST_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, sort_bytes, keys, keys2, vals, vals2, (int)m, 0, end_bit, s));
+  pf->end(ST_SORT, s);
+  pf->begin(ST_BOUNDS, s);
   TPST_TRY(hipMemsetAsync(bstart, 0, nbk * 4, s));
   TPST_TRY(hipMemsetAsync(bend, 0, nbk * 4, s));
   k_bucket_bounds<<<grid_for(m, 256), 256, 0, s>>>(keys2, m, sent, bstart, bend);
   TPST_TRY(hipGetLastError());
+  pf->end(ST_BOUNDS, s);
+  pf->begin(ST_BUCKET_ACC, s);
   k_bucket_acc<F><<<grid_for(nbk, 64), 64, 0, s>>>(vals2, bstart, bend, d_bases, nbk, buckets);
   TPST_TRY(hipGetLastError());
+  pf->end(ST_BUCKET_ACC, s);
+  pf->begin(ST_REDUCE, s);
   TPST_TRY(reduce_buckets<F>(ar, s, buckets, W, nb, win));
+  pf->end(ST_REDUCE, s);
+  pf->begin(ST_COMBINE, s);
   k_window_combine<F><<<1, 64, 0, s>>>(win, W, c, d_out);
-  return hipGetLastError();
+  TPST_TRY(hipGetLastError());
+  pf->end(ST_COMBINE, s);
+  return hipSuccess;
 }
 
 #ifndef TPST_MSM_G2_ONLY
@@ -286,6 +302,49 @@ hipError_t Arena::reserve(size_t bytes) {
   if (e != hipSuccess) return e;
   cap = want;
   return hipSuccess;
+}
+
+void Profiler::begin(int st, hipStream_t s) {
+  if (!on) return;
+  if (used[st] + 2 > ev[st].size()) {
+    hipEvent_t a, b;
+    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
+    ev[st].push_back(a);
+    ev[st].push_back(b);
+  }
+  (void)hipEventRecord(ev[st][used[st]], s);
+}
+
+void Profiler::end(int st, hipStream_t s) {
+  if (!on || used[st] + 2 > ev[st].size()) return;
+  (void)hipEventRecord(ev[st][used[st] + 1], s);
+  used[st] += 2;
+}
+
+void Profiler::collect() {
+  for (int st = 0; st < N_STAGES; st++) {
+    for (size_t i = 0; i + 1 < used[st]; i += 2) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, ev[st][i], ev[st][i + 1]) == hipSuccess) {
+        total_ms[st] += ms;
+        count[st] += 1;
+      }
+    }
+    used[st] = 0;
+  }
+}
+
+void Profiler::reset() {
+  for (int st = 0; st < N_STAGES; st++) {
+    used[st] = 0;
+    total_ms[st] = 0;
+    count[st] = 0;
+  }
+}
+
+Profiler::~Profiler() {
+  for (auto& v : ev)
+    for (auto e : v) (void)hipEventDestroy(e);
 }
 
 void Arena::release() {
@@ -430,12 +489,22 @@ hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint3
   uint32_t* bend = ar.take<uint32_t>(nbk);
   Xyzz<Fq>* buckets = ar.take<Xyzz<Fq>>(nbk);
   unsigned nblk = (unsigned)rows;
+  Profiler* pf = ar.prof;
+  Profiler dummy;
+  if (!pf) pf = &dummy;
+  pf->begin(ST_BATCH_SORT, s);
   k_batch_sort<<<nblk, 256, nb * sizeof(uint32_t), s>>>(d_scalars, rows, N, row_stride, col_stride, c, W, entries,
                                                         bstart, bend);
   TPST_TRY(hipGetLastError());
+  pf->end(ST_BATCH_SORT, s);
+  pf->begin(ST_BUCKET_ACC, s);
   k_bucket_acc<Fq><<<grid_for(nbk, 64), 64, 0, s>>>(entries, bstart, bend, t.d_table, nbk, buckets);
   TPST_TRY(hipGetLastError());
-  return reduce_buckets<Fq>(ar, s, buckets, rows, nb, d_out);
+  pf->end(ST_BUCKET_ACC, s);
+  pf->begin(ST_REDUCE, s);
+  TPST_TRY(reduce_buckets<Fq>(ar, s, buckets, rows, nb, d_out));
+  pf->end(ST_REDUCE, s);
+  return hipSuccess;
 }
 
 // explicit instantiations (G1)

@@ -82,6 +82,34 @@ class Context:
                    "tpst_g2_mul_generator")
         return out
 
+    # ------------------------------------------------------- profiling ---
+    STAGES = ("decompose", "sort", "bounds", "bucket_acc", "reduce", "combine", "batch_sort")
+
+    def profile(self, on: bool):
+        self.check(self.lib.tpst_profile_enable(self.h, 1 if on else 0), "tpst_profile_enable")
+
+    def profile_reset(self):
+        self.check(self.lib.tpst_profile_reset(self.h), "tpst_profile_reset")
+
+    def profile_read(self) -> dict:
+        out = {}
+        for i, name in enumerate(self.STAGES):
+            ms, cnt = C.c_double(), C.c_uint64()
+            self.check(self.lib.tpst_profile_read(self.h, i, C.byref(ms), C.byref(cnt)), "tpst_profile_read")
+            out[name] = (ms.value, cnt.value)
+        return out
+
+    def synchronize(self):
+        self.check(self.lib.tpst_synchronize(self.h), "tpst_synchronize")
+
+    def g1_msm_dev(self, d_bases: int, d_scalars: int, n: int, d_out: int):
+        self.check(self.lib.tpst_g1_msm_dev(self.h, C.c_void_p(d_bases), C.c_void_p(d_scalars), n,
+                                            C.c_void_p(d_out)), "tpst_g1_msm_dev")
+
+    def g1_mul_generator_dev(self, d_scalars: int, n: int, d_out: int):
+        self.check(self.lib.tpst_g1_mul_generator_dev(self.h, C.c_void_p(d_scalars), n, C.c_void_p(d_out)),
+                   "tpst_g1_mul_generator_dev")
+
     def microbench(self, kind: int, threads: int, iters: int) -> float:
         ms = C.c_double()
         self.check(self.lib.tpst_microbench(self.h, kind, threads, iters, C.byref(ms)), "tpst_microbench")
