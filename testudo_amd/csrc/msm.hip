@@ -22,21 +22,26 @@ static inline int bit_length(uint64_t v) {
   return b;
 }
 
-// number of signed-digit windows: ceil(254 / c) keeps the top digit < 2^(c-1)
-static inline int num_windows(int c) { return (254 + c - 1) / c; }
+// signed-digit windows covering `bits` bits: ceil(bits / c) keeps the top
+// digit <= 2^(c-1) (bits = 254 for full scalars, 128 for GLV halves)
+static inline int num_windows_bits(int c, int bits) { return (bits + c - 1) / c; }
+static inline int num_windows(int c) { return num_windows_bits(c, 254); }
 
-// c-bit window of an 8-word canonical scalar starting at bit `off`
-__device__ __forceinline__ uint32_t window_bits(const uint32_t* s, int off, int c) {
+// entries per thread in the balanced bucket accumulation
+constexpr uint32_t ACC_CHUNK = 32;
+
+// c-bit window of an nw-word canonical scalar starting at bit `off`
+__device__ __forceinline__ uint32_t window_bits(const uint32_t* s, int nw, int off, int c) {
   const int w = off >> 5, b = off & 31;
-  const uint64_t lo = (w < 8) ? s[w] : 0u;
-  const uint64_t hi = (w + 1 < 8) ? s[w + 1] : 0u;
+  const uint64_t lo = (w < nw) ? s[w] : 0u;
+  const uint64_t hi = (w + 1 < nw) ? s[w + 1] : 0u;
   return (uint32_t)(((lo | (hi << 32)) >> b) & ((1ull << c) - 1));
 }
 
 // signed digit of window w given the running carry (arkworks make_digits,
 // except the top window keeps its carry instead of recentering)
-__device__ __forceinline__ int signed_digit(const uint32_t* s, int w, int c, int W, uint32_t& carry) {
-  const uint32_t coef = window_bits(s, w * c, c) + carry;
+__device__ __forceinline__ int signed_digit(const uint32_t* s, int nw, int w, int c, int W, uint32_t& carry) {
+  const uint32_t coef = window_bits(s, nw, w * c, c) + carry;
   if (w == W - 1) {
     carry = 0;
     return (int)coef;
@@ -52,30 +57,100 @@ __device__ __forceinline__ void load_scalar(const uint32_t* p, uint32_t* s) {
   s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
 }
 
+// GLV split k = k1 + k2 * lambda (lambda = x^2 - 1, 127 bits), both halves
+// < 2^127: k2 = floor(k * mu / 2^256) (+1 correction), k1 = k - k2 * lambda
+__device__ __forceinline__ void glv_split(const uint32_t* k, uint32_t* k1, uint32_t* k2) {
+  uint32_t prod[13];
+#pragma unroll
+  for (int i = 0; i < 13; i++) prod[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+      const uint64_t t = (uint64_t)k[i] * params::GLV_MU[j] + prod[i + j] + carry;
+      prod[i + j] = (uint32_t)t;
+      carry = t >> 32;
+    }
+    prod[i + 5] = (uint32_t)carry;
+  }
+  uint32_t q[4] = {prod[8], prod[9], prod[10], prod[11]};
+  uint32_t ql[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) ql[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    uint64_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint64_t t = (uint64_t)q[i] * params::GLV_LAMBDA[j] + ql[i + j] + carry;
+      ql[i + j] = (uint32_t)t;
+      carry = t >> 32;
+    }
+    ql[i + 4] = (uint32_t)carry;
+  }
+  uint32_t r[4];
+  int64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {  // k - q*lambda < 2*lambda < 2^128
+    const int64_t d = (int64_t)k[i] - ql[i] + br;
+    r[i] = (uint32_t)d;
+    br = d >> 32;
+  }
+  // r >= lambda ?  -> subtract once more
+  uint32_t s[4];
+  br = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int64_t d = (int64_t)r[i] - params::GLV_LAMBDA[i] + br;
+    s[i] = (uint32_t)d;
+    br = d >> 32;
+  }
+  const bool ge = (br == 0);
+  uint64_t c = ge ? 1 : 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    k1[i] = ge ? s[i] : r[i];
+    c += q[i];
+    k2[i] = (uint32_t)c;
+    c >>= 32;
+  }
+}
+
 // ------------------------------------------------------ K2 decomposition --
-static __global__ void k_decompose_var(const uint32_t* __restrict__ scalars, size_t n, int c, int W,
-                                uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+// entries (key = window*nb + |digit|-1, val = point index | sign<<31); with
+// GLV, point index i < n is P_i and n + i is phi(P_i)
+static __global__ void k_decompose_var(const uint32_t* __restrict__ scalars, size_t n, int c, int W, int glv,
+                                       uint32_t sent, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t s[8];
   load_scalar(scalars + 8 * i, s);
   const uint32_t nb = 1u << (c - 1);
-  const uint32_t sent = (uint32_t)W * nb;
-  uint32_t carry = 0;
-  for (int w = 0; w < W; w++) {
-    const int d = signed_digit(s, w, c, W, carry);
-    uint32_t key = sent, val = 0;
-    if (d != 0) {
-      key = (uint32_t)w * nb + (uint32_t)(abs(d) - 1);
-      val = (uint32_t)i | (d < 0 ? 0x80000000u : 0u);
+  const int halves = glv ? 2 : 1;
+  uint32_t parts[2][4];
+  if (glv) glv_split(s, parts[0], parts[1]);
+  for (int h = 0; h < halves; h++) {
+    const uint32_t* sc = glv ? parts[h] : s;
+    const int nw = glv ? 4 : 8;
+    const uint32_t idx = (uint32_t)(h * n + i);
+    uint32_t carry = 0;
+    for (int w = 0; w < W; w++) {
+      const int d = signed_digit(sc, nw, w, c, W, carry);
+      uint32_t key = sent, val = 0;
+      if (d != 0) {
+        key = (uint32_t)w * nb + (uint32_t)(abs(d) - 1);
+        val = idx | (d < 0 ? 0x80000000u : 0u);
+      }
+      const size_t slot = ((size_t)h * W + w) * n + i;
+      keys[slot] = key;
+      vals[slot] = val;
     }
-    keys[(size_t)w * n + i] = key;
-    vals[(size_t)w * n + i] = val;
   }
 }
 
 static __global__ void k_bucket_bounds(const uint32_t* __restrict__ keys, size_t m, uint32_t sent,
-                                uint32_t* __restrict__ bstart, uint32_t* __restrict__ bend) {
+                                       uint32_t* __restrict__ bstart, uint32_t* __restrict__ bend) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
   const uint32_t k = keys[i];
@@ -84,22 +159,82 @@ static __global__ void k_bucket_bounds(const uint32_t* __restrict__ keys, size_t
   if (i == m - 1 || keys[i + 1] != k) bend[k] = (uint32_t)i + 1;
 }
 
-// one thread per bucket: sum its (signed) points with XYZZ mixed additions
+// phi(P) = (beta x, y), the GLV endomorphism (phi(P) = [x^2 - 1] P)
+static __global__ void k_glv_phi(const uint32_t* __restrict__ bases, size_t n, uint32_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  G1A p = load_affine<Fq>(bases, i);
+  if (!is_inf(p)) p.x = mul(p.x, Fq::from_limbs(params::G1_BETA));
+  store_affine(out, i, p);
+}
+
 template <class F>
-__global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2)) k_bucket_acc(const uint32_t* __restrict__ vals, const uint32_t* __restrict__ bstart,
-                             const uint32_t* __restrict__ bend, const uint32_t* __restrict__ bases,
-                             size_t nbk, Xyzz<F>* __restrict__ out) {
+__device__ __forceinline__ Affine<F> fetch_point(const uint32_t* bases, const uint32_t* phib, uint32_t nbase,
+                                                uint32_t v) {
+  const uint32_t idx = v & 0x7fffffffu;
+  Affine<F> p = (idx < nbase) ? load_affine<F>(bases, idx) : load_affine<F>(phib, idx - nbase);
+  if (v >> 31) p.y = neg(p.y);
+  return p;
+}
+
+// Balanced bucket accumulation over the key-sorted entries: thread t owns
+// entries [t*CH, (t+1)*CH).  A bucket lying wholly inside the chunk is
+// written directly; the chunk's first / last segment of a bucket that crosses
+// the chunk boundary goes to part[2t] (bucket began earlier) / part[2t+1]
+// (bucket continues), summed by k_bucket_fixup.  The next point is loaded
+// before the current mixed add runs (software prefetch).
+template <class F>
+__global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
+    k_bucket_acc_chunk(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals, size_t m,
+                       uint32_t sent, const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend,
+                       const uint32_t* __restrict__ bases, const uint32_t* __restrict__ phib, uint32_t nbase,
+                       Xyzz<F>* __restrict__ buckets, Xyzz<F>* __restrict__ part) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t c0 = t * ACC_CHUNK;
+  if (c0 >= m) return;
+  const size_t c1 = (c0 + ACC_CHUNK < m) ? c0 + ACC_CHUNK : m;
+  uint32_t key = keys[c0];
+  Affine<F> pt;
+  if (key < sent) pt = fetch_point<F>(bases, phib, nbase, vals[c0]);
+  Xyzz<F> acc = Xyzz<F>::inf();
+  for (size_t e = c0; e < c1; e++) {
+    uint32_t key_n = sent;
+    Affine<F> pt_n;
+    if (e + 1 < c1) {
+      key_n = keys[e + 1];
+      if (key_n < sent) pt_n = fetch_point<F>(bases, phib, nbase, vals[e + 1]);
+    }
+    if (key < sent) {
+      acc = add_affine(acc, pt);
+      if (key_n != key) {
+        const bool starts = bstart[key] >= c0;
+        const bool ends = bend[key] <= c1;
+        if (starts && ends)
+          store_xyzz(buckets, key, acc);
+        else
+          store_xyzz(part, 2 * t + (starts ? 1 : 0), acc);
+        acc = Xyzz<F>::inf();
+      }
+    }
+    key = key_n;
+    pt = pt_n;
+  }
+}
+
+// buckets that cross chunk boundaries: tail of the first chunk + heads of the rest
+template <class F>
+__global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
+    k_bucket_fixup(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend, size_t nbk,
+                   const Xyzz<F>* __restrict__ part, Xyzz<F>* __restrict__ buckets) {
   const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= nbk) return;
-  const uint32_t e0 = bstart[b], e1 = bend[b];
-  Xyzz<F> acc = Xyzz<F>::inf();
-  for (uint32_t e = e0; e < e1; e++) {
-    const uint32_t v = vals[e];
-    Affine<F> p = load_affine<F>(bases, v & 0x7fffffffu);
-    if (v >> 31) p.y = neg(p.y);
-    acc = add_affine(acc, p);
-  }
-  store_xyzz(out, b, acc);
+  const uint32_t s = bstart[b], e = bend[b];
+  if (e <= s) return;
+  const size_t t0 = s / ACC_CHUNK, t1 = (e - 1) / ACC_CHUNK;
+  if (t0 == t1) return;
+  Xyzz<F> acc = load_xyzz(part, 2 * t0 + 1);
+  for (size_t t = t0 + 1; t <= t1; t++) acc = add(acc, load_xyzz(part, 2 * t));
+  store_xyzz(buckets, b, acc);
 }
 
 // segment t of group g: sum_{b in seg} (b+1) * S_b with b the bucket index
@@ -127,7 +262,7 @@ __global__ void __launch_bounds__(64, 1) k_seg_reduce(const Xyzz<F>* __restrict_
   store_xyzz(seg_out, t, sum);
 }
 
-// one workgroup per group: sum its S segment results
+// one workgroup per group: sum its S partial points
 template <class F, int BS>
 __global__ void __launch_bounds__(BS) k_group_reduce(const Xyzz<F>* __restrict__ seg, uint32_t S,
                                                      Xyzz<F>* __restrict__ out) {
@@ -210,17 +345,32 @@ hipError_t xyzz_to_affine_canonical(hipStream_t s, const Xyzz<F>* d_in, uint32_t
   return hipGetLastError();
 }
 
-// reduce `groups` bucket sets of nb buckets each into one point per group
+// reduce `groups` bucket sets of nb buckets each into one point per group:
+// short weighted segments (L = 4) then two tree passes
+template <class F>
+static size_t reduce_scratch(size_t groups, uint32_t nb) {
+  const uint32_t L = nb >= 4 ? 4 : nb;
+  const size_t nseg = groups * (nb / L);
+  return Arena::need(nseg, sizeof(Xyzz<F>)) + Arena::need(nseg / 64 + groups + 1, sizeof(Xyzz<F>));
+}
+
 template <class F>
 static hipError_t reduce_buckets(Arena& ar, hipStream_t s, const Xyzz<F>* d_buckets, size_t groups, uint32_t nb,
                                  Xyzz<F>* d_group_out) {
-  uint32_t L = nb >= 32 ? 32 : nb;
+  const uint32_t L = nb >= 4 ? 4 : nb;
   const uint32_t S = nb / L;
   const size_t nseg = groups * S;
   Xyzz<F>* seg = ar.take<Xyzz<F>>(nseg);
   k_seg_reduce<F><<<grid_for(nseg, 64), 64, 0, s>>>(d_buckets, nb, L, nseg, seg);
   TPST_TRY(hipGetLastError());
-  k_group_reduce<F, 64><<<(unsigned)groups, 64, 0, s>>>(seg, S, d_group_out);
+  if (S >= 256 && S % 64 == 0) {  // two-pass tree: 64 -> 1, then per group
+    Xyzz<F>* mid = ar.take<Xyzz<F>>(nseg / 64);
+    k_group_reduce<F, 64><<<(unsigned)(nseg / 64), 64, 0, s>>>(seg, 64, mid);
+    TPST_TRY(hipGetLastError());
+    k_group_reduce<F, 64><<<(unsigned)groups, 64, 0, s>>>(mid, S / 64, d_group_out);
+  } else {
+    k_group_reduce<F, 64><<<(unsigned)groups, 64, 0, s>>>(seg, S, d_group_out);
+  }
   return hipGetLastError();
 }
 
@@ -231,21 +381,23 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
     Xyzz<F> inf = Xyzz<F>::inf();
     return hipMemcpyAsync(d_out, &inf, sizeof(inf), hipMemcpyHostToDevice, s);
   }
-  const int c = msm_window_bits(n);
-  const int W = num_windows(c);
+  constexpr bool kGlv = sizeof(F) == sizeof(Fq);  // G1: phi(x, y) = (beta x, y)
+  const bool glv = kGlv && n >= 64;
+  const int c = msm_window_bits(glv ? 2 * n : n);
+  const int W = glv ? num_windows_bits(c, 128) : num_windows(c);
   const uint32_t nb = 1u << (c - 1);
-  const size_t m = (size_t)W * n;
+  const size_t m = (size_t)(glv ? 2 : 1) * W * n;
   const size_t nbk = (size_t)W * nb;
-  const uint32_t sent = (uint32_t)nbk;
+  const uint32_t sent = (uint32_t)nbk;  // zero digits; sorts after every bucket key
   const int end_bit = bit_length(sent);
-
   size_t sort_bytes = 0;
   TPST_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                               (uint32_t*)nullptr, (uint32_t*)nullptr, (int)m, 0, end_bit, s));
-  const uint32_t L = nb >= 32 ? 32 : nb;
+  const size_t nchunk = (m + ACC_CHUNK - 1) / ACC_CHUNK;
   size_t need = Arena::need(m, 4) * 4 + Arena::need(nbk, 4) * 2 + Arena::need(nbk, sizeof(Xyzz<F>)) +
-                Arena::need((size_t)W * (nb / L), sizeof(Xyzz<F>)) + Arena::need(W, sizeof(Xyzz<F>)) +
-                Arena::need(sort_bytes, 1) + 4096;
+                Arena::need(2 * nchunk, sizeof(Xyzz<F>)) + reduce_scratch<F>(W, nb) +
+                Arena::need(W, sizeof(Xyzz<F>)) + Arena::need(glv ? n * 24 : 1, 4) + Arena::need(sort_bytes, 1) +
+                8192;
   ar.reset();
   TPST_TRY(ar.reserve(need));
   uint32_t* keys = ar.take<uint32_t>(m);
@@ -255,15 +407,21 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   uint32_t* bstart = ar.take<uint32_t>(nbk);
   uint32_t* bend = ar.take<uint32_t>(nbk);
   Xyzz<F>* buckets = ar.take<Xyzz<F>>(nbk);
+  Xyzz<F>* part = ar.take<Xyzz<F>>(2 * nchunk);
   Xyzz<F>* win = ar.take<Xyzz<F>>(W);
+  uint32_t* phib = ar.take<uint32_t>(glv ? n * 24 : 1);
   void* tmp = ar.take<char>(sort_bytes);
 
   Profiler* pf = ar.prof;
   Profiler dummy;
   if (!pf) pf = &dummy;
   pf->begin(ST_DECOMPOSE, s);
-  k_decompose_var<<<grid_for(n, 256), 256, 0, s>>>(d_scalars, n, c, W, keys, vals);
+  k_decompose_var<<<grid_for(n, 256), 256, 0, s>>>(d_scalars, n, c, W, glv ? 1 : 0, sent, keys, vals);
   TPST_TRY(hipGetLastError());
+  if (glv) {
+    k_glv_phi<<<grid_for(n, 256), 256, 0, s>>>(d_bases, n, phib);
+    TPST_TRY(hipGetLastError());
+  }
   pf->end(ST_DECOMPOSE, s);
   pf->begin(ST_SORT, s);
   TPST_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, sort_bytes, keys, keys2, vals, vals2, (int)m, 0, end_bit, s));
@@ -271,11 +429,15 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   pf->begin(ST_BOUNDS, s);
   TPST_TRY(hipMemsetAsync(bstart, 0, nbk * 4, s));
   TPST_TRY(hipMemsetAsync(bend, 0, nbk * 4, s));
+  TPST_TRY(hipMemsetAsync(buckets, 0, nbk * sizeof(Xyzz<F>), s));  // ZZ = 0 == infinity
   k_bucket_bounds<<<grid_for(m, 256), 256, 0, s>>>(keys2, m, sent, bstart, bend);
   TPST_TRY(hipGetLastError());
   pf->end(ST_BOUNDS, s);
   pf->begin(ST_BUCKET_ACC, s);
-  k_bucket_acc<F><<<grid_for(nbk, 64), 64, 0, s>>>(vals2, bstart, bend, d_bases, nbk, buckets);
+  k_bucket_acc_chunk<F><<<grid_for(nchunk, 64), 64, 0, s>>>(keys2, vals2, m, sent, bstart, bend, d_bases, phib,
+                                                            (uint32_t)n, buckets, part);
+  TPST_TRY(hipGetLastError());
+  k_bucket_fixup<F><<<grid_for(nbk, 64), 64, 0, s>>>(bstart, bend, nbk, part, buckets);
   TPST_TRY(hipGetLastError());
   pf->end(ST_BUCKET_ACC, s);
   pf->begin(ST_REDUCE, s);
@@ -408,8 +570,8 @@ void batch_tables_free(BatchTables& t) {
 // by bucket; writes the row's entries and bucket bounds.
 __global__ void __launch_bounds__(256) k_batch_sort(const uint32_t* __restrict__ scalars, size_t rows, size_t N,
                                                     size_t row_stride, size_t col_stride, int c, int W,
-                                                    uint32_t* __restrict__ entries, uint32_t* __restrict__ bstart,
-                                                    uint32_t* __restrict__ bend) {
+                                                    uint32_t* __restrict__ keys, uint32_t* __restrict__ entries,
+                                                    uint32_t* __restrict__ bstart, uint32_t* __restrict__ bend) {
   extern __shared__ uint32_t cnt[];  // nb counters
   // XCD-aware: consecutive rows on the same XCD (blocks b, b+8, ... share one)
   const size_t nblk = gridDim.x;
@@ -424,13 +586,14 @@ __global__ void __launch_bounds__(256) k_batch_sort(const uint32_t* __restrict__
     load_scalar(scalars + 8 * (r * row_stride + j * col_stride), s);
     uint32_t carry = 0;
     for (int w = 0; w < W; w++) {
-      const int d = signed_digit(s, w, c, W, carry);
+      const int d = signed_digit(s, 8, w, c, W, carry);
       if (d) atomicAdd(&cnt[abs(d) - 1], 1u);
     }
   }
   __syncthreads();
   // exclusive scan of nb counters: thread t owns a contiguous slice
   __shared__ uint32_t part[256];
+  __shared__ uint32_t total_sh;
   const uint32_t per = (nb + blockDim.x - 1) / blockDim.x;
   const uint32_t b0 = threadIdx.x * per;
   uint32_t local = 0;
@@ -444,6 +607,7 @@ __global__ void __launch_bounds__(256) k_batch_sort(const uint32_t* __restrict__
       part[t] = run;
       run += v;
     }
+    total_sh = run;
   }
   __syncthreads();
   const size_t rowbase = r * N * (size_t)W;
@@ -461,13 +625,19 @@ __global__ void __launch_bounds__(256) k_batch_sort(const uint32_t* __restrict__
     load_scalar(scalars + 8 * (r * row_stride + j * col_stride), s);
     uint32_t carry = 0;
     for (int w = 0; w < W; w++) {
-      const int d = signed_digit(s, w, c, W, carry);
+      const int d = signed_digit(s, 8, w, c, W, carry);
       if (d) {
-        const uint32_t pos = atomicAdd(&cnt[abs(d) - 1], 1u);
+        const uint32_t b = (uint32_t)abs(d) - 1;
+        const uint32_t pos = atomicAdd(&cnt[b], 1u);
+        keys[rowbase + pos] = (uint32_t)(r * nb + b);
         entries[rowbase + pos] = (uint32_t)(w * N + j) | (d < 0 ? 0x80000000u : 0u);
       }
     }
   }
+  // zero digits leave the row's region short: pad it with the sentinel
+  const uint32_t total = total_sh;
+  const uint32_t sent = (uint32_t)(rows * nb);
+  for (size_t e = total + threadIdx.x; e < N * (size_t)W; e += blockDim.x) keys[rowbase + e] = sent;
 }
 
 hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint32_t* d_scalars, size_t rows,
@@ -479,12 +649,14 @@ hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint3
   const size_t m = rows * N * (size_t)W;
   if (m >= (1ull << 32)) return hipErrorInvalidValue;  // entry offsets are u32
   const size_t nbk = rows * nb;
-  const uint32_t L = nb >= 32 ? 32 : nb;
-  size_t need = Arena::need(m, 4) + 2 * Arena::need(nbk, 4) + Arena::need(nbk, sizeof(Xyzz<Fq>)) +
-                Arena::need(rows * (nb / L), sizeof(Xyzz<Fq>)) + 4096;
+  const size_t nchunk = (m + ACC_CHUNK - 1) / ACC_CHUNK;
+  size_t need = 2 * Arena::need(m, 4) + 2 * Arena::need(nbk, 4) + Arena::need(nbk, sizeof(Xyzz<Fq>)) +
+                Arena::need(2 * nchunk, sizeof(Xyzz<Fq>)) + reduce_scratch<Fq>(rows, nb) + 4096;
   ar.reset();
   TPST_TRY(ar.reserve(need));
+  uint32_t* keys = ar.take<uint32_t>(m);
   uint32_t* entries = ar.take<uint32_t>(m);
+  Xyzz<Fq>* part = ar.take<Xyzz<Fq>>(2 * nchunk);
   uint32_t* bstart = ar.take<uint32_t>(nbk);
   uint32_t* bend = ar.take<uint32_t>(nbk);
   Xyzz<Fq>* buckets = ar.take<Xyzz<Fq>>(nbk);
@@ -493,12 +665,16 @@ hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint3
   Profiler dummy;
   if (!pf) pf = &dummy;
   pf->begin(ST_BATCH_SORT, s);
-  k_batch_sort<<<nblk, 256, nb * sizeof(uint32_t), s>>>(d_scalars, rows, N, row_stride, col_stride, c, W, entries,
-                                                        bstart, bend);
+  TPST_TRY(hipMemsetAsync(buckets, 0, nbk * sizeof(Xyzz<Fq>), s));  // ZZ = 0 == infinity
+  k_batch_sort<<<nblk, 256, nb * sizeof(uint32_t), s>>>(d_scalars, rows, N, row_stride, col_stride, c, W, keys,
+                                                        entries, bstart, bend);
   TPST_TRY(hipGetLastError());
   pf->end(ST_BATCH_SORT, s);
   pf->begin(ST_BUCKET_ACC, s);
-  k_bucket_acc<Fq><<<grid_for(nbk, 64), 64, 0, s>>>(entries, bstart, bend, t.d_table, nbk, buckets);
+  k_bucket_acc_chunk<Fq><<<grid_for(nchunk, 64), 64, 0, s>>>(keys, entries, m, (uint32_t)nbk, bstart, bend,
+                                                             t.d_table, nullptr, 0x7fffffffu, buckets, part);
+  TPST_TRY(hipGetLastError());
+  k_bucket_fixup<Fq><<<grid_for(nbk, 64), 64, 0, s>>>(bstart, bend, nbk, part, buckets);
   TPST_TRY(hipGetLastError());
   pf->end(ST_BUCKET_ACC, s);
   pf->begin(ST_REDUCE, s);
