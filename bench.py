@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--no-pst", action="store_true", help="skip the sqrt-PST commit+open leg")
     ap.add_argument("--pst-log-n", type=int, default=20)
+    ap.add_argument("--no-sharded", action="store_true", help="skip the row-sharded 2^24 commit leg")
+    ap.add_argument("--sharded-log-n", type=int, default=24)
     return ap.parse_args()
 
 
@@ -127,6 +129,12 @@ def main():
     parity_ok = bool(np.array_equal(out, expect))
     del limbs_to_int
 
+    sharded = None
+    if dist is not None and not args.no_sharded:
+        try:
+            sharded = sharded_leg(ctx, args.sharded_log_n, dist, dev)
+        except Exception as e:
+            sharded = {"error": repr(e)}
     if rank != 0:
         if dist:
             dist.barrier()
@@ -180,6 +188,7 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                      "kernel": "k_bucket_acc<Fq>", "alg_bytes_per_launch": alg_bytes,
                      "kernel_avg_ms": round(acc_avg_ms, 4)},
+        **({"pst_sharded_commit": sharded} if sharded is not None else {}),
         "compute": {"bound": "valu-int32", "kernel": "k_bucket_acc<Fq>",
                     "achieved_fq_mul_per_s": achieved_fqmul, "peak_fq_mul_per_s_measured": peak_fqmul,
                     "frac": round(achieved_fqmul / peak_fqmul, 4)},
@@ -187,6 +196,11 @@ def main():
 
     if not args.no_pst and world == 1:
         result["pst"] = pst_leg(ctx, args.pst_log_n)
+    if dist is None and not args.no_sharded:
+        try:
+            result["pst_sharded_commit"] = sharded_leg(ctx, args.sharded_log_n, None, dev)
+        except Exception as e:  # never lose the bench line to the secondary leg
+            result["pst_sharded_commit"] = {"error": repr(e)}
     if not args.no_cpu and world == 1:
         result["cpu_baseline"] = cpu_leg(ctx, bk, sc, out)
     print(json.dumps(result), flush=True)
@@ -222,6 +236,43 @@ def pst_leg(ctx, log_n):
             "commit_plus_open_s": round(commit_s + open_s, 4), "verify_s": round(verify_s, 4),
             "srs_setup_s": round(setup_s, 3), "verified": ok,
             "note": "host-pointer API: commit time includes H2D of nothing (Z resident after from_evaluations)"}
+
+
+def sharded_leg(ctx, log_n, dist, dev):
+    """sqrt-PST commit at 2^log_n variables (BASELINE configs[3]) with the row
+    MSMs sharded over the ranks (RCCL all-gather of row commitments, IPP on
+    rank 0); on one process it is the plain single-GPU commit."""
+    import torch
+    from testudo_amd import sqrt_pst as S
+    from testudo_amd.distributed import sharded_commit
+    nv = (log_n + 1) // 2
+    S.srs_setup(ctx, nv, SEED + 1)
+    Z, _ = S.fr_stream(SEED, 1 << log_n)
+    pl = S.Polynomial.from_evaluations(ctx, Z)
+    reps = 2
+    times = []
+    for _ in range(reps + 1):
+        if dist:
+            dist.barrier()
+        ctx.synchronize()
+        t = time.perf_counter()
+        if dist:
+            comms, T = sharded_commit(log_n, pl.commit_rows, lambda c: S.ipp(ctx, log_n, c), dist, dev)
+        else:
+            comms, T = pl.commit()
+        ctx.synchronize()
+        if dist:
+            dist.barrier()
+        el = time.perf_counter() - t
+        if dist:
+            tt = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        times.append(el)
+    world = dist.get_world_size() if dist else 1
+    return {"log_n": log_n, "commit_s": round(min(times[1:]), 4), "ranks": world,
+            "rows_per_rank": (1 << (log_n // 2)) // world,
+            "exchange": "all_gather of 96-B row commitments (RCCL) + IPP on rank 0" if dist else "none"}
 
 
 def cpu_leg(ctx, bk, sc, gpu_out):

@@ -126,6 +126,11 @@ int tpst_poly_eval(tpst_ctx* ctx, tpst_poly* p, const uint64_t* point, uint64_t*
 /* Polynomial::commit (sqrt_pst.rs:117-149): comms = 2^m_col G1, T = GT */
 int tpst_poly_commit(tpst_ctx* ctx, tpst_poly* p, uint64_t* comms, uint64_t* T);
 int tpst_poly_commit_dev(tpst_ctx* ctx, tpst_poly* p, void* d_comms, void* d_T);
+/* Row-sharded commit (multi-GPU): the MSMs of rows [r0, r1)
+ * of the sqrt_pst.rs:121-125 loop -> (r1-r0) canonical G1; and the IPP of a
+ * gathered commitment list (sqrt_pst.rs:128-143) -> T. */
+int tpst_poly_commit_rows(tpst_ctx* ctx, tpst_poly* p, size_t r0, size_t r1, uint64_t* comms);
+int tpst_poly_ipp(tpst_ctx* ctx, int n, const uint64_t* comms, uint64_t* T);
 /* Polynomial::open (sqrt_pst.rs:168-230); the transcript is updated in place */
 int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, const uint64_t* comms,
                    const uint64_t* point, const uint64_t* T, tpst_open_proof* proof);

@@ -1,0 +1,115 @@
+"""world_size-2 gloo tests on CPU of the multi-rank paths:
+
+* the row-sharded commit orchestration (testudo_amd/distributed.py) with the
+  C++ oracle standing in for the per-rank GPU compute -- the gathered
+  commitment list and T must equal the single-process commit bit for bit;
+* bench.py's timing aggregation (barrier + max over ranks).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle", "cpu"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import orc
+        from testudo_amd.distributed import sharded_commit
+        nv = (n + 1) // 2
+        srs = orc.SRS(nv, 0x7E57D1)
+        flat = srs.export()
+        C, Rn = 1 << (n // 2), 1 << nv
+        pg0 = flat[36:36 + Rn * 12].reshape(Rn, 12)
+        # powers_of_h[odd]: skip g, h, level 0 (G1 + G2) when odd
+        off = 36
+        levels = []
+        for i in range(nv):
+            m = 1 << (nv - i)
+            levels.append((off, off + m * 12))
+            off += m * 12 + m * 24
+        odd = n % 2
+        hstart = levels[odd][1]
+        hvec = flat[hstart:hstart + C * 24].reshape(C, 24)
+        Z, _ = orc.fr_stream(0x7E57D0, 1 << n)
+
+        def commit_rows(r0, r1):
+            return orc.g1_msm_batch(pg0, Z[r0:].reshape(-1), r1 - r0, 1, C)
+
+        def ipp(comms):
+            return orc.multi_pairing(comms, hvec)
+
+        comms, T = sharded_commit(n, commit_rows, ipp, dist, torch.device("cpu"))
+        if rank == 0:
+            c2, T2 = orc.pst_commit(srs, Z, n)
+            q.put((bool(np.array_equal(comms, c2)), bool(np.array_equal(T, T2))))
+        else:
+            q.put(None)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [6, 7])
+def test_sharded_commit_gloo_world2(n):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res = [r for r in res if r is not None]
+    assert res == [(True, True)]
+
+
+def _timing_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import time
+        dist.barrier()
+        t0 = time.perf_counter()
+        time.sleep(0.05 * (rank + 1))  # rank 1 is the slow one
+        dist.barrier()
+        el = time.perf_counter() - t0
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        q.put((rank, float(t.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_max_over_ranks_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_timing_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0] == res[1] and res[0] >= 0.1

@@ -210,3 +210,19 @@ def test_commit_homomorphism_n20(ctx):
     for i in (0, 1, 517, 1023):
         row = Z[i::1024]
         assert np.array_equal(comms[i], ctx.g1_msm(pg0, row))
+
+
+def test_commit_rows_and_ipp_match_full_commit(ctx):
+    """The per-rank pieces of the sharded commit:
+    row blocks concatenate to the full comm_list and ipp(comm_list) == T."""
+    from testudo_amd import sqrt_pst as S
+    for n in (9, 12):
+        nv = (n + 1) // 2
+        S.srs_setup(ctx, nv, 0x7E57D1)
+        Z, _ = S.fr_stream(0x7E57D0 + n, 1 << n)
+        pl = S.Polynomial.from_evaluations(ctx, Z)
+        comms, T = pl.commit()
+        C = 1 << (n // 2)
+        parts = [pl.commit_rows(r, r + C // 4) for r in range(0, C, C // 4)]
+        assert np.array_equal(np.concatenate(parts), comms)
+        assert np.array_equal(S.ipp(ctx, n, comms), T)

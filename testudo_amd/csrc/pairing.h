@@ -76,10 +76,36 @@ TPST_NI Fq12 ell(const Fq12& f, const LineCoeff& c, const G1A& p) {
   return mul_by_034(f, mul_fq(c.c0, p.y), mul_fq(c.c1, p.x), c.c2);
 }
 
+// Granger-Scott squaring in the cyclotomic subgroup (valid after the easy
+// part of the final exponentiation), as ark-ff Fp12::cyclotomic_square:
+// 6 Fq2 products instead of the 12 of a generic Fq12 squaring.
+TPST_NI Fq12 cyclotomic_sqr(const Fq12& f) {
+  const Fq2 &r0 = f.c0.c0, &r4 = f.c0.c1, &r3 = f.c0.c2, &r2 = f.c1.c0, &r1 = f.c1.c1, &r5 = f.c1.c2;
+  Fq2 tmp = mul(r0, r1);
+  const Fq2 t0 = sub(sub(mul(add(r0, r1), add(mul_by_u(r1), r0)), tmp), mul_by_u(tmp));
+  const Fq2 t1 = dbl(tmp);
+  tmp = mul(r2, r3);
+  const Fq2 t2 = sub(sub(mul(add(r2, r3), add(mul_by_u(r3), r2)), tmp), mul_by_u(tmp));
+  const Fq2 t3 = dbl(tmp);
+  tmp = mul(r4, r5);
+  const Fq2 t4 = sub(sub(mul(add(r4, r5), add(mul_by_u(r5), r4)), tmp), mul_by_u(tmp));
+  const Fq2 t5 = dbl(tmp);
+  Fq12 z;
+  z.c0.c0 = add(dbl(sub(t0, r0)), t0);  // 3 t0 - 2 r0
+  z.c1.c1 = add(dbl(add(t1, r1)), t1);  // 3 t1 + 2 r1
+  tmp = mul_by_u(t5);
+  z.c1.c0 = add(dbl(add(r2, tmp)), tmp);  // 3 nr(t5) + 2 r2
+  z.c0.c2 = add(dbl(sub(t4, r3)), t4);  // 3 t4 - 2 r3
+  z.c0.c1 = add(dbl(sub(t2, r4)), t2);  // 3 t2 - 2 r4
+  z.c1.c2 = add(dbl(add(t3, r5)), t3);  // 3 t3 + 2 r5
+  return z;
+}
+
+// f^x for f in the cyclotomic subgroup (x = BLS parameter, positive)
 TPST_NI Fq12 exp_by_x(const Fq12& f) {
   Fq12 res = f;
   for (int b = X_BITS - 2; b >= 0; b--) {
-    res = sqr(res);
+    res = cyclotomic_sqr(res);
     if ((params::BLS_X >> b) & 1) res = mul(res, f);
   }
   return res;
@@ -90,7 +116,7 @@ TPST_NI Fq12 final_exponentiation(const Fq12& f) {
   Fq12 r = mul(conj(f), inv(f));
   r = mul(frobenius(r, 2), r);
   // hard part, eprint 2020/875 (ark-ec Bls12::final_exponentiation)
-  Fq12 y0 = sqr(r);
+  Fq12 y0 = cyclotomic_sqr(r);
   Fq12 y1 = exp_by_x(r);
   Fq12 y2 = conj(r);
   y1 = mul(y1, y2);

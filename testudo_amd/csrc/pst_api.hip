@@ -598,6 +598,60 @@ extern "C" int tpst_poly_commit_dev(tpst_ctx* ctx, tpst_poly* p, void* d_comms, 
   return TPST_OK;
 }
 
+// row-sharded commit: rows [r0, r1) of the strided view,
+// i.e. this rank's block of columns of Z.  comms: (r1-r0) canonical affine G1.
+extern "C" int tpst_poly_commit_rows(tpst_ctx* ctx, tpst_poly* p, size_t r0, size_t r1, uint64_t* comms) {
+  if (!ctx || !p || !comms || r1 < r0) return fail(ctx, TPST_E_ARG, "bad argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  SrsState* st = srs_of(ctx);
+  if (!st) return fail(ctx, TPST_E_STATE, "no SRS loaded");
+  if (st->nv != p->m_row) return fail(ctx, TPST_E_ARG, "SRS num_vars != ceil(n/2)");
+  const size_t C = (size_t)1 << p->m_col;
+  if (r1 > C) return fail(ctx, TPST_E_ARG, "row range out of bounds");
+  const size_t R = r1 - r0;
+  if (R == 0) return TPST_OK;
+  hipStream_t s = ctx->stream;
+  DevBuf rows, out;
+  TPST_HIP(ctx, rows.alloc(R * sizeof(Xyzz<Fq>)));
+  TPST_HIP(ctx, out.alloc(R * 96));
+  TPST_HIP(ctx, msm_batch(ctx->arena, s, st->tables, p->d_Z + 8 * r0, R, 1, C, (Xyzz<Fq>*)rows.p));
+  TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(s, (Xyzz<Fq>*)rows.p, out.u(), R));
+  TPST_HIP(ctx, hipMemcpyAsync(comms, out.p, R * 96, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipStreamSynchronize(s));
+  return TPST_OK;
+}
+
+// IPP of a full commitment list: T = prod_i e(comms[i], powers_of_h[odd][i])
+// (sqrt_pst.rs:128-143), for a list gathered from the ranks
+extern "C" int tpst_poly_ipp(tpst_ctx* ctx, int n, const uint64_t* comms, uint64_t* T) {
+  if (!ctx || !comms || !T) return fail(ctx, TPST_E_ARG, "null argument");
+  int m_col, m_row, odd;
+  if (poly_dims(n, m_col, m_row, odd)) return fail(ctx, TPST_E_ARG, "bad num_vars");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  SrsState* st = srs_of(ctx);
+  if (!st) return fail(ctx, TPST_E_STATE, "no SRS loaded");
+  if (st->nv != m_row) return fail(ctx, TPST_E_ARG, "SRS num_vars != ceil(n/2)");
+  const size_t C = (size_t)1 << m_col;
+  hipStream_t s = ctx->stream;
+  DevBuf up, cm, tt, out;
+  TPST_HIP(ctx, up.alloc(C * 96));
+  TPST_HIP(ctx, cm.alloc(C * 96));
+  TPST_HIP(ctx, tt.alloc(sizeof(Fq12)));
+  TPST_HIP(ctx, out.alloc(576));
+  TPST_HIP(ctx, hipMemcpyAsync(up.p, comms, C * 96, hipMemcpyHostToDevice, s));
+  TPST_HIP(ctx, points_to_mont<Fq>(s, up.u(), cm.u(), C));
+  ctx->arena.reset();
+  TPST_HIP(ctx, ctx->arena.reserve(Arena::need(C, sizeof(Fq12)) + 4096));
+  TPST_HIP(ctx, multi_pairing_prepared(ctx->arena, s, cm.u(), st->ph[odd]->u(), (const LineCoeff*)st->hprep[odd].p, 1,
+                                       C, (Fq12*)tt.p));
+  TPST_HIP(ctx, fq12_from_mont(s, (Fq12*)tt.p, out.u(), 1));
+  TPST_HIP(ctx, hipMemcpyAsync(T, out.p, 576, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipStreamSynchronize(s));
+  return TPST_OK;
+}
+
 // --------------------------------------------------------------- open ----
 // MSM over device bases (Montgomery) with Montgomery Fr scalars (converted)
 template <class F>
@@ -653,8 +707,9 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   Sponge sp;
   sp.load(tr);
 
-  DevBuf A, Y, H, tmp, xy, gts, small, canon;
+  DevBuf A, Y, H, H2, tmp, xy, gts, small, canon;
   TPST_HIP(ctx, A.alloc(C * 96));
+  TPST_HIP(ctx, H2.alloc(C * 192));
   TPST_HIP(ctx, Y.alloc(C * 32));
   TPST_HIP(ctx, H.alloc(C * 192));
   TPST_HIP(ctx, tmp.alloc(C * 32));
@@ -693,9 +748,12 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     TPST_HIP(ctx, msm_mont_scalars<Fq>(ctx, A.u(), Y.u() + 8 * split, split, tmp.u(), x1));
     TPST_HIP(ctx, msm_mont_scalars<Fq>(ctx, A.u() + 24 * split, Y.u(), split, tmp.u(), x1 + 1));
     TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(s, x1, canon.u(), 2));
-    // t_l = e(a[:s], h[s:]), t_r = e(a[s:], h[:s])
-    TPST_HIP(ctx, multi_pairing(ctx->arena, s, A.u(), H.u() + 48 * split, 1, split, (Fq12*)gts.p));
-    TPST_HIP(ctx, multi_pairing(ctx->arena, s, A.u() + 24 * split, H.u(), 1, split, (Fq12*)gts.p + 1));
+    // t_l = e(a[:s], h[s:]), t_r = e(a[s:], h[:s]) as one batched launch of
+    // two groups (their final exponentiations run side by side): G2 side is
+    // H with its halves swapped, G1 side is A as is
+    TPST_HIP(ctx, hipMemcpyAsync(H2.p, H.u() + 48 * split, split * 192, hipMemcpyDeviceToDevice, s));
+    TPST_HIP(ctx, hipMemcpyAsync(H2.u() + 48 * split, H.p, split * 192, hipMemcpyDeviceToDevice, s));
+    TPST_HIP(ctx, multi_pairing(ctx->arena, s, A.u(), H2.u(), 2, split, (Fq12*)gts.p));
     TPST_HIP(ctx, fq12_from_mont(s, (Fq12*)gts.p, canon.u() + 48, 2));
     uint64_t* ut = proof->comms_u[round][0];
     TPST_HIP(ctx, hipMemcpyAsync(ut, canon.p, 96, hipMemcpyDeviceToHost, s));

@@ -137,6 +137,12 @@ class Polynomial:
         self.ctx.check(self.ctx.lib.tpst_poly_commit(self.ctx.h, self.h, ptr(comms), ptr(T)), "commit")
         return comms, T
 
+    def commit_rows(self, r0: int, r1: int) -> np.ndarray:
+        """Row MSMs of rows [r0, r1) only (one rank's shard of sqrt_pst.rs:121-125)."""
+        out = np.zeros((r1 - r0, 12), dtype=np.uint64)
+        self.ctx.check(self.ctx.lib.tpst_poly_commit_rows(self.ctx.h, self.h, r0, r1, ptr(out)), "commit_rows")
+        return out
+
     def commit_dev(self, d_comms: int, d_T: int):
         self.ctx.check(self.ctx.lib.tpst_poly_commit_dev(self.ctx.h, self.h, C.c_void_p(d_comms),
                                                          C.c_void_p(d_T)), "commit_dev")
@@ -173,6 +179,13 @@ def pack_proof(n, U, pst_proof, mipp: MippProof):
     np.ctypeslib.as_array(pr.final_h)[:] = _u64(mipp.final_h, (24,))
     np.ctypeslib.as_array(pr.pst_proof_h)[:pr.m_col] = _u64(mipp.pst_proof_h, (pr.m_col, 12))
     return pr
+
+
+def ipp(ctx: Context, n: int, comms) -> np.ndarray:
+    """T = prod e(C_i, h_i) for a full (gathered) commitment list."""
+    T = np.zeros(72, dtype=np.uint64)
+    ctx.check(ctx.lib.tpst_poly_ipp(ctx.h, n, ptr(_u64(comms, (-1, 12))), ptr(T)), "ipp")
+    return T
 
 
 def verify(ctx: Context, transcript: PoseidonTranscript, U, point, v, pst_proof, mipp: MippProof, T) -> bool:
