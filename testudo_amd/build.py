@@ -25,23 +25,29 @@ FLAGS = ["-std=c++17", "-O3", "--offload-arch=" + ARCH, "-fPIC", "-Wno-unused-re
          "-I" + CSRC, "-I" + os.path.join(ROOT, "include")]
 
 
-def _deps_mtime() -> float:
-    files = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.inc"))
-    files.append(os.path.join(ROOT, "include", "tpst.h"))
-    return max(os.path.getmtime(f) for f in files)
+def _includes(path: str, seen: set) -> None:
+    """Transitive local #includes of a source or header (csrc/ and include/)."""
+    for inc in re.findall(r'#include "([^"]+)"', open(path).read()):
+        for d in (os.path.dirname(path), CSRC, os.path.join(ROOT, "include")):
+            f = os.path.join(d, inc)
+            if os.path.exists(f):
+                f = os.path.abspath(f)
+                if f not in seen:
+                    seen.add(f)
+                    _includes(f, seen)
+                break
 
 
 def _src_mtime(src: str) -> float:
-    """mtime of a .hip file and of any .hip it #includes (msm_g2.hip)."""
-    t = os.path.getmtime(src)
-    for inc in re.findall(r'#include "([^"]+\.hip)"', open(src).read()):
-        t = max(t, os.path.getmtime(os.path.join(os.path.dirname(src), inc)))
-    return t
+    """newest mtime over a .hip file and everything it includes."""
+    seen = {os.path.abspath(src)}
+    _includes(src, seen)
+    return max(os.path.getmtime(f) for f in seen)
 
 
-def _compile(src: str, hdr_mtime: float) -> str:
+def _compile(src: str) -> str:
     obj = os.path.join(BUILD, os.path.basename(src) + ".o")
-    if os.path.exists(obj) and os.path.getmtime(obj) >= max(_src_mtime(src), hdr_mtime):
+    if os.path.exists(obj) and os.path.getmtime(obj) >= _src_mtime(src):
         return obj
     cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj + ".tmp"]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -54,10 +60,9 @@ def _compile(src: str, hdr_mtime: float) -> str:
 def build(verbose: bool = True) -> str:
     os.makedirs(BUILD, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
-    hdr = _deps_mtime()
     jobs = min(len(srcs), int(os.environ.get("MAX_JOBS", "8")))
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, hdr), srcs))
+        objs = list(ex.map(_compile, srcs))
     newest = max(os.path.getmtime(o) for o in objs)
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < newest:
         cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", LIB + ".tmp"] + objs

@@ -7,6 +7,7 @@
 // (arkworks does the same with chunks of 4, bls12/mod.rs multi_miller_loop).
 #include "device_util.h"
 #include "pairing_kernels.h"
+#include "wave_tower.h"
 
 namespace tpst {
 
@@ -32,58 +33,203 @@ hipError_t g2_prepare_batch(hipStream_t s, const uint32_t* d_g2, size_t n, LineC
   return hipGetLastError();
 }
 
-// thread (g, t) handles pairs t, t+T, ... of group g; writes its partial f
-__global__ void k_miller(const uint32_t* __restrict__ g1, const uint32_t* __restrict__ g2,
-                         const LineCoeff* __restrict__ coeffs, size_t groups, size_t n, size_t T,
-                         Fq12* __restrict__ partial) {
-  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid >= groups * T) return;
-  const size_t g = tid / T, t = tid % T;
-  const size_t stride = groups * n;
-  Fq12 f = Fq12::one();
-  int idx = 0;
-  for (int b = X_BITS - 2; b >= 0; b--) {
-    f = sqr(f);
-    const bool add_step = (params::BLS_X >> b) & 1;
-    for (size_t i = t; i < n; i += T) {
-      const size_t pi = g * n + i;
-      const G1A p = load_affine<Fq>(g1, pi);
-      const G2A q = load_affine<Fq2>(g2, pi);
-      if (is_inf(p) || is_inf(q)) continue;
-      f = ell(f, coeffs[(size_t)idx * stride + pi], p);
-      if (add_step) f = ell(f, coeffs[(size_t)(idx + 1) * stride + pi], p);
-    }
-    idx += add_step ? 2 : 1;
+// ---- wave-cooperative Miller loop (wave_tower.h) -------------------------
+// One wave per pair: per bit one SQR_LP stage (f^2 and the line products
+// c0*py, c1*px of this bit's 1-2 lines, 58-62 lanes) and one MUL034 stage
+// per line (39 lanes).  The line coefficients of bit k+1 are fetched while
+// bit k's stages run.
+constexpr int MW = 4;                          // waves per workgroup
+constexpr int MW_SLOTS = 64 + 12 + 12 + 14 + 12;  // PROD, F, F2, B (lines + P), D (prepared lines)
+constexpr int MW_PROG = ((int)(wave::OP_LEN[wave::OP_SQR_LP1] + wave::OP_LEN[wave::OP_SQR_LP2] +
+                               wave::OP_LEN[wave::OP_MUL034]) + 3) & ~3;
+constexpr size_t MW_LDS = (size_t)(MW_PROG + MW * MW_SLOTS * wave::SLOT) * 4;
+static_assert(MW_LDS <= 65536, "Miller kernel LDS");
+
+__global__ void __launch_bounds__(64 * MW) k_miller_wave(const uint32_t* __restrict__ g1,
+                                                         const uint32_t* __restrict__ g2,
+                                                         const LineCoeff* __restrict__ coeffs, size_t np,
+                                                         Fq12* __restrict__ partial) {
+  extern __shared__ uint4 smem4[];
+  uint32_t* prog = reinterpret_cast<uint32_t*>(smem4);
+  uint32_t* vals = prog + MW_PROG;
+  const int ops[3] = {wave::OP_SQR_LP1, wave::OP_SQR_LP2, wave::OP_MUL034};
+  uint32_t off[3];
+  wave::load_ops(prog, ops, 3, off);
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t pi = (size_t)blockIdx.x * MW + w;
+  if (pi >= np) return;
+  const G1A p = load_affine<Fq>(g1, pi);
+  const G2A q = load_affine<Fq2>(g2, pi);
+  if (is_inf(p) || is_inf(q)) {
+    if (lane < 12) reinterpret_cast<Fq*>(partial + pi)[lane] = lane == 0 ? Fq::one() : Fq::zero();
+    return;
   }
-  partial[tid] = f;
+  const int base = w * MW_SLOTS;
+  const wave::Eng e{vals, base, 0};
+  int F = base + 64, F2 = base + 76;
+  const int B = base + 88, D = base + 102;
+  if (lane == 0) wave::put_slot(vals, B + 6, p.x);
+  if (lane == 1) wave::put_slot(vals, B + 7, p.y);
+  wave::set_one(vals, F);
+  const Fq* cf = reinterpret_cast<const Fq*>(coeffs);  // LineCoeff = 6 Fq
+  // lanes 0..5: line idx, lanes 6..11: line idx + 1 (addition step)
+  int idx = 0;
+  Fq pre = Fq::zero();
+  if (lane < 12) pre = cf[((size_t)(idx + (lane >= 6)) * np + pi) * 6 + lane % 6];
+  for (int b = X_BITS - 2; b >= 0; b--) {
+    const bool add = (params::BLS_X >> b) & 1;
+    if (lane < 6 || (add && lane < 12)) wave::put_slot(vals, B + (lane < 6 ? lane : lane + 2), pre);
+    const int nidx = idx + (add ? 2 : 1);
+    if (b > 0 && lane < 12) {
+      const bool nadd = (params::BLS_X >> (b - 1)) & 1;
+      if (lane < 6 || nadd) pre = cf[((size_t)(nidx + (lane >= 6)) * np + pi) * 6 + lane % 6];
+    }
+    wave::wave_sync();
+    wave::run(e, prog + off[add ? 1 : 0], F, B, F2, D);
+    wave::run(e, prog + off[2], F2, D, F);
+    if (add) {
+      wave::run(e, prog + off[2], F, D + 6, F2);
+      const int t = F;
+      F = F2;
+      F2 = t;
+    }
+    idx = nidx;
+  }
+  wave::store_f12(vals, F, partial + pi);
 }
 
-// one workgroup per group: product of T partials, then final exponentiation
-template <int BS>
-__global__ void __launch_bounds__(BS) k_gt_reduce_final(const Fq12* __restrict__ partial, size_t T,
-                                                       Fq12* __restrict__ out) {
-  __shared__ Fq12 sh[BS];
-  const size_t g = blockIdx.x;
-  Fq12 acc = Fq12::one();
-  for (size_t k = threadIdx.x; k < T; k += BS) acc = mul(acc, partial[g * T + k]);
-  sh[threadIdx.x] = acc;
-  __syncthreads();
-  for (int h = BS / 2; h > 0; h >>= 1) {
-    if ((int)threadIdx.x < h) sh[threadIdx.x] = mul(sh[threadIdx.x], sh[threadIdx.x + h]);
-    __syncthreads();
+// ---- product of a group's partials + final exponentiation ----------------
+constexpr int FW = 4;  // waves per workgroup
+constexpr int FW_SLOTS = 64 + 36;          // PROD, ACC, IN, TMP per wave
+constexpr int FE_SLOTS = 10 * 12 + 24;     // wave 0: 10 registers + inversion temporaries
+constexpr int FE_OPS[] = {wave::OP_F12_MUL, wave::OP_CYC_SQR, wave::OP_FROB1, wave::OP_FROB2, wave::OP_CONJ,
+                          wave::OP_INV1,    wave::OP_INV2,    wave::OP_INV3,  wave::OP_INV4,  wave::OP_INV5,
+                          wave::OP_INV6,    wave::OP_INV7};
+constexpr int N_FE_OPS = sizeof(FE_OPS) / sizeof(FE_OPS[0]);
+constexpr int fe_prog_words() {
+  int s = 0;
+  for (int i = 0; i < N_FE_OPS; i++) s += (int)wave::OP_LEN[FE_OPS[i]];
+  return (s + 3) & ~3;
+}
+constexpr int FW_PROG = fe_prog_words();
+constexpr size_t FW_LDS = (size_t)(FW_PROG + (wave::N_CONSTS + FW * FW_SLOTS + FE_SLOTS) * wave::SLOT) * 4;
+static_assert(FW_LDS <= 65536, "final-exponentiation kernel LDS");
+
+enum { FE_MUL, FE_CYC, FE_FROB1, FE_FROB2, FE_CONJ, FE_INV1 };
+
+__device__ int fe_exp_by_x(const wave::Eng& e, const uint32_t* const* op, int src, int r1, int r2) {
+  int cur = src;
+  for (int b = X_BITS - 2; b >= 0; b--) {
+    int nxt = cur == r1 ? r2 : r1;
+    wave::run(e, op[FE_CYC], cur, 0, nxt);
+    cur = nxt;
+    if ((params::BLS_X >> b) & 1) {
+      nxt = cur == r1 ? r2 : r1;
+      wave::run(e, op[FE_MUL], cur, src, nxt);
+      cur = nxt;
+    }
   }
-  if (threadIdx.x == 0) out[g] = final_exponentiation(sh[0]);
+  return cur;
+}
+
+// f (register F) -> f^(3(p^12-1)/r); returns the result register.  Same chain
+// as final_exponentiation() in pairing.h (eprint 2020/875).
+__device__ int fe_final_exp(const wave::Eng& e, const uint32_t* const* op, int F, int regs, int I) {
+  const int lane = threadIdx.x & 63;
+  int R[10];
+  for (int i = 0; i < 10; i++) R[i] = regs + 12 * i;
+  // f^-1 through the tower norms, one Fq inversion on lane 0
+  wave::run(e, op[FE_INV1 + 0], F, 0, I + 0);        // t = c0^2 - v c1^2
+  wave::run(e, op[FE_INV1 + 1], I + 0, 0, I + 6);    // Fq6 adjugate c'
+  wave::run(e, op[FE_INV1 + 2], I + 6, I + 0, I + 12);  // Fq6 norm t'
+  wave::run(e, op[FE_INV1 + 3], I + 12, 0, I + 14);  // Fq2 norm n
+  if (lane == 0) wave::put_slot(e.lds, I + 15, inv(wave::get_slot(e.lds, I + 14)));
+  wave::wave_sync();
+  wave::run(e, op[FE_INV1 + 4], I + 12, I + 15, I + 16);  // t'^-1
+  wave::run(e, op[FE_INV1 + 5], I + 6, I + 16, I + 18);   // t^-1
+  wave::run(e, op[FE_INV1 + 6], F, I + 18, R[0]);         // f^-1
+  // easy part
+  wave::run(e, op[FE_CONJ], F, 0, R[1]);
+  wave::run(e, op[FE_MUL], R[1], R[0], R[2]);  // r = conj(f) f^-1
+  wave::run(e, op[FE_FROB2], R[2], 0, R[1]);
+  wave::run(e, op[FE_MUL], R[1], R[2], R[3]);  // r = r^(p^2) r
+  // hard part
+  wave::run(e, op[FE_CYC], R[3], 0, R[4]);  // y0
+  int t = fe_exp_by_x(e, op, R[3], R[5], R[6]);
+  wave::run(e, op[FE_CONJ], R[3], 0, R[7]);  // y2 = conj(r)
+  wave::run(e, op[FE_MUL], t, R[7], R[8]);   // y1 = y1 y2
+  t = fe_exp_by_x(e, op, R[8], R[5], R[6]);  // y2
+  wave::run(e, op[FE_CONJ], R[8], 0, R[7]);
+  wave::run(e, op[FE_MUL], R[7], t, R[9]);   // y1 = conj(y1) y2
+  t = fe_exp_by_x(e, op, R[9], R[5], R[6]);  // y2
+  wave::run(e, op[FE_FROB1], R[9], 0, R[7]);
+  wave::run(e, op[FE_MUL], R[7], t, R[8]);   // y1 = frob(y1) y2
+  wave::run(e, op[FE_MUL], R[3], R[4], R[0]);  // r = r y0
+  const int y0 = fe_exp_by_x(e, op, R[8], R[5], R[6]);
+  const int y2 = fe_exp_by_x(e, op, y0, y0 == R[5] ? R[6] : R[5], R[1]);
+  wave::run(e, op[FE_FROB2], R[8], 0, R[2]);  // y0 = frob2(y1)
+  wave::run(e, op[FE_CONJ], R[8], 0, R[3]);
+  wave::run(e, op[FE_MUL], R[3], y2, R[4]);   // y1 = conj(y1) y2
+  wave::run(e, op[FE_MUL], R[4], R[2], R[7]);  // y1 = y1 y0
+  wave::run(e, op[FE_MUL], R[0], R[7], R[9]);  // r = r y1
+  return R[9];
+}
+
+__global__ void __launch_bounds__(64 * FW) k_final_wave(const Fq12* __restrict__ partial, size_t T,
+                                                        Fq12* __restrict__ out) {
+  extern __shared__ uint4 smem4[];
+  __shared__ int acc_slot[FW];
+  uint32_t* prog = reinterpret_cast<uint32_t*>(smem4);
+  uint32_t* vals = prog + FW_PROG;
+  uint32_t off[N_FE_OPS];
+  wave::load_ops(prog, FE_OPS, N_FE_OPS, off);
+  wave::load_consts(vals, 0);
+  __syncthreads();
+  const uint32_t* op[N_FE_OPS];
+  for (int i = 0; i < N_FE_OPS; i++) op[i] = prog + off[i];
+  const int w = threadIdx.x >> 6;
+  const size_t g = blockIdx.x;
+  const int base = wave::N_CONSTS + w * FW_SLOTS;
+  const wave::Eng e{vals, base, 0};
+  int acc = base + 64, in = base + 76, tmp = base + 88;
+  size_t cnt = 0;
+  for (size_t k = w; k < T; k += FW, cnt++) {
+    if (cnt == 0) {
+      wave::load_f12(vals, acc, partial + g * T + k);
+    } else {
+      wave::load_f12(vals, in, partial + g * T + k);
+      wave::run(e, op[FE_MUL], acc, in, tmp);
+      const int t = acc;
+      acc = tmp;
+      tmp = t;
+    }
+  }
+  if (cnt == 0) wave::set_one(vals, acc);
+  if ((threadIdx.x & 63) == 0) acc_slot[w] = acc;
+  __syncthreads();
+  if (w != 0) return;
+  for (int v = 1; v < FW; v++) {
+    wave::run(e, op[FE_MUL], acc, acc_slot[v], tmp);
+    const int t = acc;
+    acc = tmp;
+    tmp = t;
+  }
+  const int fe = wave::N_CONSTS + FW * FW_SLOTS;
+  const int r = fe_final_exp(e, op, acc, fe, fe + 120);
+  wave::store_f12(vals, r, out + g);
 }
 
 hipError_t multi_pairing_prepared(Arena& ar, hipStream_t s, const uint32_t* d_g1, const uint32_t* d_g2,
                                   const LineCoeff* d_coeffs, size_t groups, size_t n, Fq12* d_out) {
   if (!groups) return hipSuccess;
-  // one pair per thread: latency-bound chains favour width
-  size_t T = n ? n : 1;
-  Fq12* partial = ar.take<Fq12>(groups * T);
-  k_miller<<<grid_for(groups * T, 64), 64, 0, s>>>(d_g1, d_g2, d_coeffs, groups, n, T, partial);
-  TPST_TRY(hipGetLastError());
-  k_gt_reduce_final<32><<<(unsigned)groups, 32, 0, s>>>(partial, T, d_out);
+  const size_t np = groups * n;
+  Fq12* partial = ar.take<Fq12>(np ? np : 1);
+  if (np) {
+    k_miller_wave<<<grid_for(np, MW), 64 * MW, MW_LDS, s>>>(d_g1, d_g2, d_coeffs, np, partial);
+    TPST_TRY(hipGetLastError());
+  }
+  k_final_wave<<<(unsigned)groups, 64 * FW, FW_LDS, s>>>(partial, n, d_out);
   return hipGetLastError();
 }
 
