@@ -66,6 +66,17 @@ int tpst_g2_msm(tpst_ctx* ctx, const uint64_t* bases, size_t n_bases, const uint
  * canonical Fr (8 u32 each), d_out one canonical affine G1 */
 int tpst_g1_msm_dev(tpst_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, void* d_out);
 
+/* ---- fixed-base grouped MSM (csrc/fbt.h) --------------------------------
+ * Builds the 64-window x 8-multiple lookup table of the n bases, then
+ * out[g] = sum over k in group g of scalars[k] * bases[k] for L/D groups,
+ * k(g, m) = (m / D) * L + g * D + m % D  (n % L == 0, L % D == 0).
+ * L = D = n is a plain MSM; D = 1 is the MIPP fold a_i + sum_t w_t a_{i+tL}
+ * (mipp.rs:124-136 applied over all rounds at once). */
+int tpst_g1_msm_fixed(tpst_ctx* ctx, const uint64_t* bases, size_t n, const uint64_t* scalars, size_t L, size_t D,
+                      uint64_t* out);
+int tpst_g2_msm_fixed(tpst_ctx* ctx, const uint64_t* bases, size_t n, const uint64_t* scalars, size_t L, size_t D,
+                      uint64_t* out);
+
 /* ---- K4: multi-pairing ---------------------------------------------------
  * prod_i e(g1[i], g2[i]) after final exponentiation (ark-ec
  * Pairing::multi_pairing(...).0; sqrt_pst.rs:143, mipp.rs:397). */

@@ -226,3 +226,24 @@ def test_commit_rows_and_ipp_match_full_commit(ctx):
         parts = [pl.commit_rows(r, r + C // 4) for r in range(0, C, C // 4)]
         assert np.array_equal(np.concatenate(parts), comms)
         assert np.array_equal(S.ipp(ctx, n, comms), T)
+
+
+@pytest.mark.parametrize("g2", [False, True])
+def test_fixed_base_grouped_msm_vs_oracle(ctx, g2):
+    """csrc/fbt.h lookup-table MSM: plain (one group), MIPP-fold groups
+    (D = 1) and cross-product groups (D = L/2), against the oracle MSM of
+    each group's members; includes an infinity base and edge scalars."""
+    n = 64
+    k, _ = orc.fr_stream(81, n)
+    s, _ = orc.fr_stream(82, n)
+    bases = orc.g2_mul_gen(k) if g2 else orc.g1_mul_gen(k)
+    bases[5] = 0
+    s[0] = fr_array([O.R - 1])[0]
+    s[1] = 0
+    s[2] = fr_array([1])[0]
+    ref_msm = orc.g2_msm if g2 else orc.g1_msm
+    for L, D in ((n, n), (16, 1), (16, 8), (8, 2)):
+        got = ctx.msm_fixed(bases, s, L, D, g2=g2)
+        for g in range(L // D):
+            idx = [(m // D) * L + g * D + m % D for m in range(n // L * D)]
+            assert np.array_equal(got[g], ref_msm(bases[idx], s[idx])), (L, D, g)

@@ -5,6 +5,7 @@
 #include "../../include/tpst.h"
 #include "ctx.h"
 #include "device_util.h"
+#include "fbt.h"
 
 using namespace tpst;
 
@@ -107,6 +108,53 @@ extern "C" int tpst_g1_msm(tpst_ctx* ctx, const uint64_t* bases, size_t n_bases,
 extern "C" int tpst_g2_msm(tpst_ctx* ctx, const uint64_t* bases, size_t n_bases, const uint64_t* scalars,
                            size_t n_scalars, uint64_t* out) {
   return msm_host<Fq2>(ctx, bases, n_bases, scalars, n_scalars, out);
+}
+
+// fixed-base table path (fbt.h): builds the table of the n bases, then the
+// grouped MSM out[g] = sum_{k in g} s_k B_k with strided groups (L, D)
+template <class F>
+static int msm_fixed_host(tpst_ctx* ctx, const uint64_t* bases, size_t n, const uint64_t* scalars, size_t L,
+                          size_t D, uint64_t* out) {
+  if (!ctx || !out || (n && (!bases || !scalars))) return fail(ctx, TPST_E_ARG, "null argument");
+  if (!n || !L || !D || n % L || L % D) return fail(ctx, TPST_E_ARG, "bad group shape");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  constexpr size_t PW = 2 * Words<F>::n;
+  const size_t G = L / D;
+  ctx->io.reset();
+  TPST_HIP(ctx, ctx->io.reserve(Arena::need(n * PW, 4) * 2 + Arena::need(n * 8, 4) + Arena::need(G, sizeof(Xyzz<F>)) +
+                                Arena::need(G * PW, 4) + Arena::need(fbt_words<F>(n), 4) + 4096));
+  uint32_t* d_b = ctx->io.take<uint32_t>(n * PW);
+  uint32_t* d_bm = ctx->io.take<uint32_t>(n * PW);
+  uint32_t* d_s = ctx->io.take<uint32_t>(n * 8);
+  Xyzz<F>* d_r = ctx->io.take<Xyzz<F>>(G);
+  uint32_t* d_o = ctx->io.take<uint32_t>(G * PW);
+  uint32_t* d_t = ctx->io.take<uint32_t>(fbt_words<F>(n));
+  hipStream_t s = ctx->stream;
+  TPST_HIP(ctx, hipMemcpyAsync(d_b, bases, n * PW * 4, hipMemcpyHostToDevice, s));
+  TPST_HIP(ctx, hipMemcpyAsync(d_s, scalars, n * 32, hipMemcpyHostToDevice, s));
+  TPST_HIP(ctx, points_to_mont<F>(s, d_b, d_bm, n));
+  TPST_HIP(ctx, fbt_build<F>(ctx->arena, s, d_bm, n, d_t));
+  FbGroups g;
+  g.groups = G;
+  g.members = (n / L) * D;
+  g.L = L;
+  g.D = D;
+  TPST_HIP(ctx, fbt_msm<F>(ctx->arena, s, d_t, d_s, g, d_r));
+  TPST_HIP(ctx, xyzz_to_affine_canonical<F>(s, d_r, d_o, G));
+  TPST_HIP(ctx, hipMemcpyAsync(out, d_o, G * PW * 4, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipStreamSynchronize(s));
+  return TPST_OK;
+}
+
+extern "C" int tpst_g1_msm_fixed(tpst_ctx* ctx, const uint64_t* bases, size_t n, const uint64_t* scalars, size_t L,
+                                 size_t D, uint64_t* out) {
+  return msm_fixed_host<Fq>(ctx, bases, n, scalars, L, D, out);
+}
+
+extern "C" int tpst_g2_msm_fixed(tpst_ctx* ctx, const uint64_t* bases, size_t n, const uint64_t* scalars, size_t L,
+                                 size_t D, uint64_t* out) {
+  return msm_fixed_host<Fq2>(ctx, bases, n, scalars, L, D, out);
 }
 
 extern "C" int tpst_g1_msm_dev(tpst_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, void* d_out) {

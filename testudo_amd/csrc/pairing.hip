@@ -19,17 +19,66 @@ namespace tpst {
 
 static inline unsigned grid_for(size_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
 
-__global__ void k_g2_prepare(const uint32_t* __restrict__ g2, size_t n, LineCoeff* __restrict__ coeffs) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const G2A q = load_affine<Fq2>(g2, i);
+// ---- G2Prepared on the wave engine ----------------------------------------
+// One wave per G2 point; each doubling / addition step of pairing.h is four
+// stages (tools/gen_wave_ops.py G2_DBL1-4 / G2_ADD1-4) over a 44-slot region.
+constexpr int PW = 4;
+constexpr int PW_SLOTS = 64 + 44;
+constexpr int PW_OPS[] = {wave::OP_G2_DBL1, wave::OP_G2_DBL2, wave::OP_G2_DBL3, wave::OP_G2_DBL4,
+                          wave::OP_G2_ADD1, wave::OP_G2_ADD2, wave::OP_G2_ADD3, wave::OP_G2_ADD4};
+constexpr int pw_prog_words() {
+  int s = 0;
+  for (int i = 0; i < 8; i++) s += (int)wave::OP_LEN[PW_OPS[i]];
+  return (s + 3) & ~3;
+}
+constexpr int PW_PROG = pw_prog_words();
+constexpr size_t PW_LDS = (size_t)(PW_PROG + (wave::N_CONSTS + PW * PW_SLOTS) * wave::SLOT) * 4;
+static_assert(PW_LDS <= 65536, "prepare kernel LDS");
+
+__global__ void __launch_bounds__(64 * PW) k_g2_prepare_wave(const uint32_t* __restrict__ g2, size_t n,
+                                                             LineCoeff* __restrict__ coeffs) {
+  extern __shared__ uint4 smem4[];
+  uint32_t* prog = reinterpret_cast<uint32_t*>(smem4);
+  uint32_t* vals = prog + PW_PROG;
+  uint32_t off[8];
+  wave::load_ops(prog, PW_OPS, 8, off);
+  wave::load_consts(vals, 0);
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t pi = (size_t)blockIdx.x * PW + w;
+  if (pi >= n) return;
+  const G2A q = load_affine<Fq2>(g2, pi);
   if (is_inf(q)) return;
-  g2_prepare(q, coeffs + i, (long)n);
+  const int base = wave::N_CONSTS + w * PW_SLOTS;
+  const wave::Eng e{vals, base, 0};
+  const int R = base + 64;
+  if (lane < 4) {
+    const Fq v = lane == 0 ? q.x.c0 : lane == 1 ? q.x.c1 : lane == 2 ? q.y.c0 : q.y.c1;
+    wave::put_slot(vals, R + lane, v);
+    wave::put_slot(vals, R + 26 + lane, v);
+  } else if (lane < 6) {
+    wave::put_slot(vals, R + lane, lane == 4 ? Fq::one() : Fq::zero());
+  }
+  wave::wave_sync();
+  Fq* cf = reinterpret_cast<Fq*>(coeffs);
+  int idx = 0;
+  for (int b = X_BITS - 2; b >= 0; b--) {
+    for (int k = 0; k < 4; k++) wave::run(e, prog + off[k], R, R, R);
+    if (lane < 6) cf[((size_t)idx * n + pi) * 6 + lane] = wave::get_slot(vals, R + 6 + lane);
+    idx++;
+    if ((params::BLS_X >> b) & 1) {
+      wave::wave_sync();
+      for (int k = 4; k < 8; k++) wave::run(e, prog + off[k], R, R, R);
+      if (lane < 6) cf[((size_t)idx * n + pi) * 6 + lane] = wave::get_slot(vals, R + 6 + lane);
+      idx++;
+    }
+    wave::wave_sync();
+  }
 }
 
 hipError_t g2_prepare_batch(hipStream_t s, const uint32_t* d_g2, size_t n, LineCoeff* d_coeffs) {
   if (!n) return hipSuccess;
-  k_g2_prepare<<<grid_for(n, 64), 64, 0, s>>>(d_g2, n, d_coeffs);
+  k_g2_prepare_wave<<<grid_for(n, PW), 64 * PW, PW_LDS, s>>>(d_g2, n, d_coeffs);
   return hipGetLastError();
 }
 

@@ -60,6 +60,19 @@ class Context:
                    "tpst_g2_msm")
         return out
 
+    def msm_fixed(self, bases: np.ndarray, scalars: np.ndarray, L: int = 0, D: int = 0, g2: bool = False):
+        """Grouped fixed-base MSM (include/tpst.h tpst_g*_msm_fixed): (L/D, 12|24)."""
+        w = 24 if g2 else 12
+        bases = np.ascontiguousarray(bases, dtype=np.uint64).reshape(-1, w)
+        scalars = np.ascontiguousarray(scalars, dtype=np.uint64).reshape(-1, 4)
+        n = len(bases)
+        L = L or n
+        D = D or L
+        out = np.zeros((L // D, w), dtype=np.uint64)
+        fn = self.lib.tpst_g2_msm_fixed if g2 else self.lib.tpst_g1_msm_fixed
+        self.check(fn(self.h, ptr(bases), n, ptr(scalars), L, D, ptr(out)), "tpst_msm_fixed")
+        return out
+
     def multi_pairing(self, g1: np.ndarray, g2: np.ndarray) -> np.ndarray:
         g1 = np.ascontiguousarray(g1, dtype=np.uint64).reshape(-1, 12)
         g2 = np.ascontiguousarray(g2, dtype=np.uint64).reshape(-1, 24)

@@ -346,6 +346,108 @@ def op_inv7(pg):
     return {"C": flat12((f6_mul(pg, f[0], ti), f6_neg(f6_mul(pg, f[1], ti))))}
 
 
+# ---- G2 line preparation (pairing.h g2_double_step / g2_add_step) ---------
+# Region ops: every operand is a slot of one per-wave region (atoms ("A", s)),
+# outputs {slot: form}.  Layout: R = x 0-1, y 2-3, z 4-5; line c0 6-7, c1 8-9,
+# c2 10-11; scratch 12-25; Q = x 26-27, y 28-29; addition scratch 30-43.
+def rf2(s):
+    return (atom("A", s), atom("A", s + 1))
+
+
+def put2(d, s, v):
+    d[s], d[s + 1] = v[0], v[1]
+
+
+B1 = (-pow(5, -1, P)) % P  # G2_B = (0, b1) = 1/u
+TWO_INV = pow(2, -1, P)
+
+
+def op_dbl1(pg):
+    x, y, z = rf2(0), rf2(2), rf2(4)
+    o = {}
+    xy = f2_mul(pg, x, y)
+    b = f2_mul(pg, y, y)
+    c = f2_mul(pg, z, z)
+    hh = f2_mul(pg, f2_add(y, z), f2_add(y, z))
+    j = f2_mul(pg, x, x)
+    put2(o, 12, xy)
+    put2(o, 14, b)
+    put2(o, 16, c)
+    put2(o, 6, f2_sub(f2_add(b, c), hh))  # c0 = -h
+    put2(o, 8, f2_sc(j, 3))               # c1 = 3 j
+    return {"C": o}
+
+
+def op_dbl2(pg):
+    xy, c = rf2(12), rf2(16)
+    ti = pg.const(TWO_INV)
+    o = {}
+    put2(o, 18, f2_mul_fq(pg, xy, ti))                      # a = xy / 2
+    put2(o, 20, (pg.mul(c[1], pg.const(-15 * B1)), pg.mul(c[0], pg.const(3 * B1))))  # e = b' 3c
+    return {"C": o}
+
+
+def op_dbl3(pg):
+    nh, b, a, e = rf2(6), rf2(14), rf2(18), rf2(20)
+    ti = pg.const(TWO_INV)
+    o = {}
+    put2(o, 22, f2_mul_fq(pg, f2_add(b, f2_sc(e, 3)), ti))  # g = (b + 3e) / 2
+    put2(o, 24, f2_mul(pg, e, e))                           # e^2
+    put2(o, 0, f2_mul(pg, a, f2_sub(b, f2_sc(e, 3))))       # x' = a (b - f)
+    put2(o, 4, f2_neg(f2_mul(pg, b, nh)))                   # z' = b h
+    put2(o, 10, f2_sub(e, b))                               # c2 = i = e - b
+    return {"C": o}
+
+
+def op_dbl4(pg):
+    g, e2 = rf2(22), rf2(24)
+    o = {}
+    put2(o, 2, f2_sub(f2_mul(pg, g, g), f2_sc(e2, 3)))     # y' = g^2 - 3 e^2
+    return {"C": o}
+
+
+def op_add1(pg):
+    x, y, z, qx, qy = rf2(0), rf2(2), rf2(4), rf2(26), rf2(28)
+    o = {}
+    theta = f2_sub(y, f2_mul(pg, qy, z))
+    lam = f2_sub(x, f2_mul(pg, qx, z))
+    put2(o, 30, theta)
+    put2(o, 32, lam)
+    put2(o, 6, lam)               # c0 = lambda
+    put2(o, 8, f2_neg(theta))     # c1 = -theta
+    return {"C": o}
+
+
+def op_add2(pg):
+    theta, lam, qx, qy = rf2(30), rf2(32), rf2(26), rf2(28)
+    o = {}
+    put2(o, 34, f2_mul(pg, theta, theta))  # c
+    put2(o, 36, f2_mul(pg, lam, lam))      # d
+    put2(o, 10, f2_sub(f2_mul(pg, theta, qx), f2_mul(pg, lam, qy)))  # c2 = j
+    return {"C": o}
+
+
+def op_add3(pg):
+    x, z, lam, c, d = rf2(0), rf2(4), rf2(32), rf2(34), rf2(36)
+    o = {}
+    e = f2_mul(pg, lam, d)
+    f = f2_mul(pg, z, c)
+    g = f2_mul(pg, x, d)
+    put2(o, 38, e)
+    put2(o, 40, g)
+    put2(o, 42, f2_sub(f2_add(e, f), f2_sc(g, 2)))  # h
+    return {"C": o}
+
+
+def op_add4(pg):
+    y, z, theta, lam, e, g, h = rf2(2), rf2(4), rf2(30), rf2(32), rf2(38), rf2(40), rf2(42)
+    o = {}
+    put2(o, 0, f2_mul(pg, lam, h))
+    put2(o, 2, f2_sub(f2_mul(pg, theta, f2_sub(g, h)), f2_mul(pg, e, y)))
+    put2(o, 4, f2_mul(pg, z, e))
+    return {"C": o}
+
+
 OP_LIST = [
     ("F12_MUL", op_f12_mul),
     ("F12_SQR", op_f12_sqr),
@@ -366,6 +468,14 @@ OP_LIST = [
     ("INV5", op_inv5),
     ("INV6", op_inv6),
     ("INV7", op_inv7),
+    ("G2_DBL1", op_dbl1),
+    ("G2_DBL2", op_dbl2),
+    ("G2_DBL3", op_dbl3),
+    ("G2_DBL4", op_dbl4),
+    ("G2_ADD1", op_add1),
+    ("G2_ADD2", op_add2),
+    ("G2_ADD3", op_add3),
+    ("G2_ADD4", op_add4),
 ]
 
 
@@ -382,7 +492,8 @@ def evaluate(pg, outs, env):
                 s += c * env[kind][i]
         return s % P
     prods = [ev(x, None) * ev(y, None) % P for x, y in pg.products]
-    return {d: [ev(l, prods) for l in lst] for d, lst in outs.items()}
+    return {d: ({k: ev(l, prods) for k, l in lst.items()} if isinstance(lst, dict) else [ev(l, prods) for l in lst])
+            for d, lst in outs.items()}
 
 
 def t2p(t):
@@ -434,6 +545,30 @@ def check(name, pg, outs):
     return True
 
 
+def check_prepare_chain(pgs):
+    q = O.g2_mul(O.G2_GEN, 0x1234567)
+    ref = O.g2_prepare(q)
+    reg = {i: 0 for i in range(44)}
+    reg[0], reg[1] = q[0]
+    reg[2], reg[3] = q[1]
+    reg[4], reg[5] = 1, 0
+    reg[26], reg[27] = q[0]
+    reg[28], reg[29] = q[1]
+    idx = 0
+    for bit in bin(O.X)[3:]:
+        steps = ["G2_DBL1", "G2_DBL2", "G2_DBL3", "G2_DBL4"]
+        if bit == "1":
+            steps += ["G2_ADD1", "G2_ADD2", "G2_ADD3", "G2_ADD4"]
+        for st in steps:
+            pg, outs = pgs[st]
+            reg.update(evaluate(pg, outs, {"A": reg, "B": reg})["C"])
+            if st in ("G2_DBL4", "G2_ADD4"):
+                c0, c1, c2 = ref[idx]
+                assert (reg[6], reg[7], reg[8], reg[9], reg[10], reg[11]) == (*c0, *c1, *c2), (st, idx)
+                idx += 1
+    assert idx == len(ref)
+
+
 def check_inverse_chain(pgs):
     f = rnd(12)
     env = lambda a, b=None: {"A": a, "B": b or [0] * 16}  # noqa: E731
@@ -471,9 +606,10 @@ def main():
         outs = fn(pg)
         built[name] = (pg, outs)
     for name, (pg, outs) in built.items():
-        if not name.startswith("INV"):
+        if not name.startswith(("INV", "G2_")):
             check(name, pg, outs)
     check_inverse_chain(built)
+    check_prepare_chain(built)
     blob, offs, lens, stats = [], [], [], []
     lines = ["// Generated by tools/gen_wave_ops.py -- do not edit.", "#pragma once", "#include <stdint.h>",
              "namespace tpst { namespace wave {"]
@@ -489,7 +625,8 @@ def main():
         need_red = int(any(x.weight() * y.weight() > 64 for x, y in pg.products))
         if need_red:
             assert all(x.weight() < 1024 and y.weight() < 1024 for x, y in pg.products)
-        olist = [(DSTCODE[d] << 8 | k, lin) for d, lst in outs.items() for k, lin in enumerate(lst)]
+        olist = [(DSTCODE[d] << 8 | k, lin) for d, lst in outs.items()
+                 for k, lin in (sorted(lst.items()) if isinstance(lst, dict) else enumerate(lst))]
         no = len(olist)
         assert no <= 64
         terms, info_x, info_y, info_o = [], [], [], []
