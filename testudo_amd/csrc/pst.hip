@@ -207,6 +207,25 @@ hipError_t gt_pow(hipStream_t s, const Fq12* d_base, const uint32_t* d_exps, siz
   return hipGetLastError();
 }
 
+// MIPP fold scalars over the original bases (fbt.h strided groups):
+// fold:  out[k] = W[k / len]                      (a^(r)_i = sum_t W_t a_{i + t len})
+// cross: out[k] = W[k / len] * y[(k % len + s) % len]   (u_l / u_r, mipp.rs:66-75)
+__global__ void k_mipp_scalars(const uint32_t* __restrict__ W, const uint32_t* __restrict__ y, size_t len, size_t s,
+                               size_t n, uint32_t* __restrict__ out) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  Fr v = load_f<Fr>(W + 8 * (k / len));
+  if (y) v = mul(v, load_f<Fr>(y + 8 * ((k % len + s) % len)));
+  store_f<Fr>(out + 8 * k, from_mont(v));
+}
+
+hipError_t mipp_scalars(hipStream_t s, const uint32_t* d_W, const uint32_t* d_y, size_t len, size_t split, size_t n,
+                        uint32_t* d_out) {
+  if (!n) return hipSuccess;
+  k_mipp_scalars<<<grid_for(n, 256), 256, 0, s>>>(d_W, d_y, len, split, n, d_out);
+  return hipGetLastError();
+}
+
 template hipError_t compress_points<Fq>(hipStream_t, uint32_t*, size_t, const uint32_t*);
 template hipError_t compress_points<Fq2>(hipStream_t, uint32_t*, size_t, const uint32_t*);
 template hipError_t fixed_base_mul<Fq>(hipStream_t, const uint32_t*, const uint32_t*, size_t, uint32_t*);

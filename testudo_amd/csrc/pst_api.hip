@@ -12,6 +12,7 @@
 
 #include "../../include/tpst.h"
 #include "ctx.h"
+#include "fbt.h"
 #include "device_util.h"
 #include "pst_kernels.h"
 
@@ -215,6 +216,15 @@ struct SrsState {
   DevBuf gmask, hmask;
   BatchTables tables;             // K1 tables over powers_of_g[0]
   DevBuf hprep[2];                // G2Prepared of powers_of_h[odd], odd = 0/1
+  // fixed-base tables (fbt.h), built on first open
+  DevBuf t_pg0;                   // powers_of_g[0]            (U = commit(q))
+  DevBuf t_h[2];                  // powers_of_h[odd]           (MIPP h folds)
+  DevBuf t_pgp, t_php;            // concatenated pg_pair / ph_pair levels (PST level proofs)
+  DevBuf seg;                     // u32 level offsets into the concatenation
+  std::vector<size_t> lvl_off;
+  bool fbt_ready = false, t_h_ready[2] = {false, false};
+  DevBuf t_A;                     // per-opening table over the row commitments
+  size_t t_A_n = 0;
   std::vector<uint64_t> flat;     // canonical export
   ~SrsState() { batch_tables_free(tables); }
 };
@@ -653,35 +663,73 @@ extern "C" int tpst_poly_ipp(tpst_ctx* ctx, int n, const uint64_t* comms, uint64
 }
 
 // --------------------------------------------------------------- open ----
-// MSM over device bases (Montgomery) with Montgomery Fr scalars (converted)
-template <class F>
-static hipError_t msm_mont_scalars(tpst_ctx* ctx, const uint32_t* bases, const uint32_t* scal_mont, size_t n,
-                                   uint32_t* tmp_canon, Xyzz<F>* out) {
-  hipError_t e = fr_from_mont(ctx->stream, scal_mont, tmp_canon, n);
-  if (e != hipSuccess) return e;
-  return msm_var<F>(ctx->arena, ctx->stream, bases, tmp_canon, n, out);
+// The opening is latency-bound (transcript rounds of small MSMs and pairings),
+// so every MSM of it runs on fixed-base lookup tables (fbt.h): the SRS sides
+// are tabulated once per SRS, the row commitments once per opening, and each
+// MIPP round's folds / cross terms are grouped MSMs over the ORIGINAL bases
+// with scalars that are products of the challenges so far.
+
+// lazily tabulate the SRS (fbt.h) for opening polynomials of parity `odd`
+static int srs_fbt(tpst_ctx* ctx, SrsState* st, int odd) {
+  hipStream_t s = ctx->stream;
+  const int nv = st->nv;
+  if (!st->fbt_ready) {
+    const size_t N = (size_t)1 << nv;
+    TPST_HIP(ctx, st->t_pg0.alloc(fbt_words<Fq>(N) * 4));
+    TPST_HIP(ctx, fbt_build<Fq>(ctx->arena, s, st->pg[0]->u(), N, st->t_pg0.u()));
+    st->lvl_off.assign(nv + 1, 0);
+    for (int i = 0; i < nv; i++) st->lvl_off[i + 1] = st->lvl_off[i] + ((size_t)1 << (nv - i - 1));
+    const size_t tot = st->lvl_off[nv];
+    TPST_HIP(ctx, st->t_pgp.alloc(fbt_words<Fq>(tot) * 4));
+    TPST_HIP(ctx, st->t_php.alloc(fbt_words<Fq2>(tot) * 4));
+    for (int i = 0; i < nv; i++) {
+      const size_t m = (size_t)1 << (nv - i - 1);
+      TPST_HIP(ctx, fbt_build<Fq>(ctx->arena, s, st->pg_pair[i]->u(), m, st->t_pgp.u() + fbt_words<Fq>(st->lvl_off[i])));
+      TPST_HIP(ctx,
+               fbt_build<Fq2>(ctx->arena, s, st->ph_pair[i]->u(), m, st->t_php.u() + fbt_words<Fq2>(st->lvl_off[i])));
+    }
+    std::vector<uint32_t> off32(st->lvl_off.begin(), st->lvl_off.end());
+    TPST_HIP(ctx, st->seg.alloc(off32.size() * 4));
+    TPST_HIP(ctx, hipMemcpyAsync(st->seg.p, off32.data(), off32.size() * 4, hipMemcpyHostToDevice, s));
+    TPST_HIP(ctx, hipStreamSynchronize(s));
+    st->fbt_ready = true;
+  }
+  if (!st->t_h_ready[odd]) {
+    const size_t C = (size_t)1 << (nv - odd);
+    TPST_HIP(ctx, st->t_h[odd].alloc(fbt_words<Fq2>(C) * 4));
+    TPST_HIP(ctx, fbt_build<Fq2>(ctx->arena, s, st->ph[odd]->u(), C, st->t_h[odd].u()));
+    TPST_HIP(ctx, hipStreamSynchronize(s));
+    st->t_h_ready[odd] = true;
+  }
+  return TPST_OK;
 }
 
-// PST open of evals (Montgomery, 2^k) at `pt` (k Montgomery Fr on device),
-// proofs over paired bases of level off+i; writes k XYZZ points
+// PST open of 2^k evals (Montgomery) at k Montgomery
+// scalars d_pt over the pair levels off..off+k-1: the k quotient scalar
+// vectors first (cheap Fr recurrence), then ONE grouped table MSM with a
+// group per level.  Writes k XYZZ points.
 template <class F>
-static int pst_open_dev(tpst_ctx* ctx, const std::vector<std::unique_ptr<DevBuf>>& pairs, int off,
-                        const uint32_t* d_evals, int k, const uint32_t* d_pt, Xyzz<F>* d_out) {
+static int pst_open_fbt(tpst_ctx* ctx, SrsState* st, const uint32_t* table, int off, const uint32_t* d_evals, int k,
+                        const uint32_t* d_pt, Xyzz<F>* d_out) {
   hipStream_t s = ctx->stream;
-  DevBuf r0, r1, qc;
+  DevBuf r0, r1, sc;
   const size_t full = (size_t)1 << k;
   TPST_HIP(ctx, r0.alloc(full * 32));
   TPST_HIP(ctx, r1.alloc(full * 32));
-  TPST_HIP(ctx, qc.alloc(full * 32));
+  TPST_HIP(ctx, sc.alloc(st->lvl_off[st->nv] * 32));
   TPST_HIP(ctx, hipMemcpyAsync(r0.p, d_evals, full * 32, hipMemcpyDeviceToDevice, s));
   uint32_t* cur = r0.u();
   uint32_t* nxt = r1.u();
   for (int i = 0; i < k; i++) {
     const size_t half = (size_t)1 << (k - i - 1);
-    TPST_HIP(ctx, pst_step(s, cur, half, d_pt + 8 * i, qc.u(), nxt));
-    TPST_HIP(ctx, msm_var<F>(ctx->arena, s, pairs[off + i]->u(), qc.u(), half, d_out + i));
+    TPST_HIP(ctx, pst_step(s, cur, half, d_pt + 8 * i, sc.u() + 8 * st->lvl_off[off + i], nxt));
     std::swap(cur, nxt);
   }
+  FbGroups g;
+  g.groups = k;
+  g.members = (size_t)1 << (k - 1);
+  g.d_seg = st->seg.u() + off;
+  TPST_HIP(ctx, fbt_msm<F>(ctx->arena, s, table, sc.u(), g, d_out));
   return TPST_OK;
 }
 
@@ -698,39 +746,62 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     int rc = poly_get_q(ctx, p, point);
     if (rc) return rc;
   }
+  {
+    int rc = srs_fbt(ctx, st, p->odd);
+    if (rc) return rc;
+  }
   hipStream_t s = ctx->stream;
   const int m = p->m_col;
   const size_t C = (size_t)1 << m;
+  const size_t N = (size_t)1 << p->m_row;
   memset(proof, 0, sizeof *proof);
   proof->m_col = m;
   proof->m_row = p->m_row;
   Sponge sp;
   sp.load(tr);
 
-  DevBuf A, Y, H, H2, tmp, xy, gts, small, canon;
+  DevBuf A, Ar, Hr, H2, Y, Sc, qc, dW, xa, xh, xy, gts, small, canon;
   TPST_HIP(ctx, A.alloc(C * 96));
+  TPST_HIP(ctx, Ar.alloc(C * 96));
+  TPST_HIP(ctx, Hr.alloc(C * 192));
   TPST_HIP(ctx, H2.alloc(C * 192));
   TPST_HIP(ctx, Y.alloc(C * 32));
-  TPST_HIP(ctx, H.alloc(C * 192));
-  TPST_HIP(ctx, tmp.alloc(C * 32));
+  TPST_HIP(ctx, Sc.alloc(C * 32));
+  TPST_HIP(ctx, qc.alloc(N * 32));
+  TPST_HIP(ctx, dW.alloc(C * 32));
+  TPST_HIP(ctx, xa.alloc(C * sizeof(Xyzz<Fq>)));
+  TPST_HIP(ctx, xh.alloc(C * sizeof(Xyzz<Fq2>)));
   TPST_HIP(ctx, xy.alloc(4 * sizeof(Xyzz<Fq2>) + 64 * sizeof(Xyzz<Fq2>)));
   TPST_HIP(ctx, gts.alloc(2 * sizeof(Fq12)));
   TPST_HIP(ctx, small.alloc(256));
   TPST_HIP(ctx, canon.alloc(4096));
-  // A = comms (Montgomery), Y = chis, H = powers_of_h[odd]
+  // A = comms (Montgomery), tabulated for the folds; Y = chis
   {
     DevBuf up;
     TPST_HIP(ctx, up.alloc(C * 96));
     TPST_HIP(ctx, hipMemcpyAsync(up.p, comms, C * 96, hipMemcpyHostToDevice, s));
     TPST_HIP(ctx, points_to_mont<Fq>(s, up.u(), A.u(), C));
+    if (st->t_A_n < C) {
+      TPST_HIP(ctx, st->t_A.alloc(fbt_words<Fq>(C) * 4));
+      st->t_A_n = C;
+    }
+    TPST_HIP(ctx, fbt_build<Fq>(ctx->arena, s, A.u(), C, st->t_A.u()));
     TPST_HIP(ctx, hipStreamSynchronize(s));
   }
   TPST_HIP(ctx, hipMemcpyAsync(Y.p, p->chis.p, C * 32, hipMemcpyDeviceToDevice, s));
-  TPST_HIP(ctx, hipMemcpyAsync(H.p, st->ph[p->odd]->p, C * 192, hipMemcpyDeviceToDevice, s));
   Xyzz<Fq>* x1 = (Xyzz<Fq>*)xy.p;
+  const uint32_t* H0 = st->ph[p->odd]->u();
+  const uint32_t* tA = st->t_A.u();
+  const uint32_t* tH = st->t_h[p->odd].u();
 
-  // U = c_u = MSM(comms, chis)          sqrt_pst.rs:198
-  TPST_HIP(ctx, msm_mont_scalars<Fq>(ctx, A.u(), Y.u(), C, tmp.u(), x1));
+  // U = c_u = MSM(comms, chis) = commit(q) = MSM(powers_of_g[0], q)   sqrt_pst.rs:198, 206
+  {
+    TPST_HIP(ctx, fr_from_mont(s, p->q.u(), qc.u(), N));
+    FbGroups g;
+    g.members = N;
+    g.L = g.D = N;
+    TPST_HIP(ctx, fbt_msm<Fq>(ctx->arena, s, st->t_pg0.u(), qc.u(), g, x1));
+  }
   TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(s, x1, canon.u(), 1));
   TPST_HIP(ctx, hipMemcpyAsync(proof->U, canon.p, 96, hipMemcpyDeviceToHost, s));
   TPST_HIP(ctx, hipStreamSynchronize(s));
@@ -739,24 +810,55 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     g1_bytes(proof->U, b);
     sp.absorb_bytes(b, 96);  // mipp.rs:56
   }
-  std::vector<Fr> xs_inv;
+  // W[t] / Wi[t]: products of the challenges (inverses) folded so far, so that
+  // a^(r)_i = sum_t W[t] a_{i + t len}, h^(r)_i = sum_t Wi[t] h_{i + t len}
+  std::vector<Fr> W(1, Fr::one()), Wi(1, Fr::one()), xs_inv;
+  auto upload = [&](const std::vector<Fr>& v) -> hipError_t {
+    return hipMemcpyAsync(dW.p, v.data(), v.size() * 32, hipMemcpyHostToDevice, s);
+  };
   size_t len = C;
   int round = 0;
   while (len > 1) {  // mipp.rs:58-120
     const size_t split = len / 2;
-    // u_l = a[:s] ^ y[s:], u_r = a[s:] ^ y[:s]
-    TPST_HIP(ctx, msm_mont_scalars<Fq>(ctx, A.u(), Y.u() + 8 * split, split, tmp.u(), x1));
-    TPST_HIP(ctx, msm_mont_scalars<Fq>(ctx, A.u() + 24 * split, Y.u(), split, tmp.u(), x1 + 1));
+    const uint32_t* Acur = A.u();
+    const uint32_t* Hcur = H0;
+    if (round > 0) {  // a^(r), h^(r) as table folds of the original vectors
+      FbGroups g;
+      g.groups = len;
+      g.members = C / len;
+      g.L = len;
+      g.D = 1;
+      TPST_HIP(ctx, upload(Wi));
+      TPST_HIP(ctx, mipp_scalars(s, dW.u(), nullptr, len, 0, C, Sc.u()));
+      TPST_HIP(ctx, fbt_msm<Fq2>(ctx->arena, s, tH, Sc.u(), g, (Xyzz<Fq2>*)xh.p));
+      TPST_HIP(ctx, xyzz_to_affine_mont<Fq2>(s, (Xyzz<Fq2>*)xh.p, Hr.u(), len));
+      TPST_HIP(ctx, upload(W));
+      TPST_HIP(ctx, mipp_scalars(s, dW.u(), nullptr, len, 0, C, Sc.u()));
+      TPST_HIP(ctx, fbt_msm<Fq>(ctx->arena, s, tA, Sc.u(), g, (Xyzz<Fq>*)xa.p));
+      TPST_HIP(ctx, xyzz_to_affine_mont<Fq>(s, (Xyzz<Fq>*)xa.p, Ar.u(), len));
+      Acur = Ar.u();
+      Hcur = Hr.u();
+    } else {
+      TPST_HIP(ctx, upload(W));
+    }
+    // u_l = a[:s] ^ y[s:], u_r = a[s:] ^ y[:s]  (mipp.rs:66-75): cross-term groups
+    {
+      FbGroups g;
+      g.groups = 2;
+      g.members = C / len * split;
+      g.L = len;
+      g.D = split;
+      TPST_HIP(ctx, mipp_scalars(s, dW.u(), Y.u(), len, split, C, Sc.u()));
+      TPST_HIP(ctx, fbt_msm<Fq>(ctx->arena, s, tA, Sc.u(), g, x1));
+    }
     TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(s, x1, canon.u(), 2));
     // t_l = e(a[:s], h[s:]), t_r = e(a[s:], h[:s]) as one batched launch of
-    // two groups (their final exponentiations run side by side): G2 side is
-    // H with its halves swapped, G1 side is A as is
-    TPST_HIP(ctx, hipMemcpyAsync(H2.p, H.u() + 48 * split, split * 192, hipMemcpyDeviceToDevice, s));
-    TPST_HIP(ctx, hipMemcpyAsync(H2.u() + 48 * split, H.p, split * 192, hipMemcpyDeviceToDevice, s));
-    TPST_HIP(ctx, multi_pairing(ctx->arena, s, A.u(), H2.u(), 2, split, (Fq12*)gts.p));
+    // two groups: G2 side is h with its halves swapped
+    TPST_HIP(ctx, hipMemcpyAsync(H2.p, Hcur + 48 * split, split * 192, hipMemcpyDeviceToDevice, s));
+    TPST_HIP(ctx, hipMemcpyAsync(H2.u() + 48 * split, Hcur, split * 192, hipMemcpyDeviceToDevice, s));
+    TPST_HIP(ctx, multi_pairing(ctx->arena, s, Acur, H2.u(), 2, split, (Fq12*)gts.p));
     TPST_HIP(ctx, fq12_from_mont(s, (Fq12*)gts.p, canon.u() + 48, 2));
-    uint64_t* ut = proof->comms_u[round][0];
-    TPST_HIP(ctx, hipMemcpyAsync(ut, canon.p, 96, hipMemcpyDeviceToHost, s));
+    TPST_HIP(ctx, hipMemcpyAsync(proof->comms_u[round][0], canon.p, 96, hipMemcpyDeviceToHost, s));
     TPST_HIP(ctx, hipMemcpyAsync(proof->comms_u[round][1], canon.u() + 24, 96, hipMemcpyDeviceToHost, s));
     TPST_HIP(ctx, hipMemcpyAsync(proof->comms_t[round][0], canon.u() + 48, 576, hipMemcpyDeviceToHost, s));
     TPST_HIP(ctx, hipMemcpyAsync(proof->comms_t[round][1], canon.u() + 48 + 144, 576, hipMemcpyDeviceToHost, s));
@@ -768,29 +870,42 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     sp.absorb_bytes(b, 96);
     sp.absorb_bytes((const uint8_t*)proof->comms_t[round][0], 576);
     sp.absorb_bytes((const uint8_t*)proof->comms_t[round][1], 576);
-    uint64_t ci_c[4], c_c[4];
+    uint64_t ci_c[4];
     sp.challenge(ci_c);  // mipp.rs:101
     const Fr c_inv = fr_canon(ci_c);
     const Fr c = fr_inv(c_inv);  // mipp.rs:106
-    fr_out(c, c_c);
-    uint32_t hbuf[24];
-    memcpy(hbuf, c_c, 32);           // c canonical
-    memcpy(hbuf + 8, ci_c, 32);      // c_inv canonical
-    memcpy(hbuf + 16, c_inv.v, 32);  // c_inv Montgomery
-    TPST_HIP(ctx, hipMemcpyAsync(small.p, hbuf, 96, hipMemcpyHostToDevice, s));
-    TPST_HIP(ctx, compress_points<Fq>(s, A.u(), split, small.u()));        // a_l + c a_r
-    TPST_HIP(ctx, compress_fr(s, Y.u(), split, small.u() + 16));           // y_l + c_inv y_r
-    TPST_HIP(ctx, compress_points<Fq2>(s, H.u(), split, small.u() + 8));   // h_l + c_inv h_r
+    // y_l + c_inv y_r (mipp.rs:124-136); a and h folds are implicit in W / Wi
+    TPST_HIP(ctx, hipMemcpyAsync(small.p, c_inv.v, 32, hipMemcpyHostToDevice, s));
+    TPST_HIP(ctx, compress_fr(s, Y.u(), split, small.u()));
+    std::vector<Fr> W2(2 * W.size()), Wi2(2 * Wi.size());
+    for (size_t t = 0; t < W2.size(); t++) {
+      W2[t] = (t & 1) ? mul(W[t >> 1], c) : W[t >> 1];
+      Wi2[t] = (t & 1) ? mul(Wi[t >> 1], c_inv) : Wi[t >> 1];
+    }
+    W.swap(W2);
+    Wi.swap(Wi2);
     TPST_HIP(ctx, hipStreamSynchronize(s));  // small.p is rewritten next round
     xs_inv.push_back(c_inv);
     len = split;
     round++;
   }
-  TPST_HIP(ctx, affine_from_mont<Fq>(s, A.u(), canon.u(), 1));
-  TPST_HIP(ctx, affine_from_mont<Fq2>(s, H.u(), canon.u() + 24, 1));
-  TPST_HIP(ctx, hipMemcpyAsync(proof->final_a, canon.p, 96, hipMemcpyDeviceToHost, s));
-  TPST_HIP(ctx, hipMemcpyAsync(proof->final_h, canon.u() + 24, 192, hipMemcpyDeviceToHost, s));
-  TPST_HIP(ctx, hipStreamSynchronize(s));
+  // final_a = a^(m+1)_0, final_h = h^(m+1)_0 (one group over all C bases)
+  {
+    FbGroups g;
+    g.members = C;
+    TPST_HIP(ctx, upload(W));
+    TPST_HIP(ctx, mipp_scalars(s, dW.u(), nullptr, 1, 0, C, Sc.u()));
+    TPST_HIP(ctx, fbt_msm<Fq>(ctx->arena, s, tA, Sc.u(), g, x1));
+    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(s, x1, canon.u(), 1));
+    TPST_HIP(ctx, hipMemcpyAsync(proof->final_a, canon.p, 96, hipMemcpyDeviceToHost, s));
+    TPST_HIP(ctx, hipStreamSynchronize(s));
+    TPST_HIP(ctx, upload(Wi));
+    TPST_HIP(ctx, mipp_scalars(s, dW.u(), nullptr, 1, 0, C, Sc.u()));
+    TPST_HIP(ctx, fbt_msm<Fq2>(ctx->arena, s, tH, Sc.u(), g, (Xyzz<Fq2>*)xh.p));
+    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq2>(s, (Xyzz<Fq2>*)xh.p, canon.u() + 24, 1));
+    TPST_HIP(ctx, hipMemcpyAsync(proof->final_h, canon.u() + 24, 192, hipMemcpyDeviceToHost, s));
+    TPST_HIP(ctx, hipStreamSynchronize(s));
+  }
   // p_h evaluations from the challenges (mipp.rs:159-180), then rs and open_g1
   if (m > 0) {
     std::vector<uint32_t> evals(C * 8);
@@ -812,7 +927,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     TPST_HIP(ctx, dr.alloc(m * 32));
     TPST_HIP(ctx, hipMemcpyAsync(de.p, evals.data(), C * 32, hipMemcpyHostToDevice, s));
     TPST_HIP(ctx, hipMemcpyAsync(dr.p, rs.data(), m * 32, hipMemcpyHostToDevice, s));
-    int rc = pst_open_dev<Fq>(ctx, st->pg_pair, st->nv - m, de.u(), m, dr.u(), x1 + 4);
+    int rc = pst_open_fbt<Fq>(ctx, st, st->t_pgp.u(), st->nv - m, de.u(), m, dr.u(), x1 + 4);
     if (rc) return rc;
     TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(s, x1 + 4, canon.u(), m));
     TPST_HIP(ctx, hipMemcpyAsync(proof->pst_proof_h, canon.p, (size_t)m * 96, hipMemcpyDeviceToHost, s));
@@ -828,7 +943,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     TPST_HIP(ctx, hipMemcpyAsync(da.p, arev.data(), k * 32, hipMemcpyHostToDevice, s));
     TPST_HIP(ctx, fr_to_mont(s, da.u(), da.u(), k));
     Xyzz<Fq2>* x2 = (Xyzz<Fq2>*)xy.p + 4;
-    int rc = pst_open_dev<Fq2>(ctx, st->ph_pair, st->nv - k, p->q.u(), k, da.u(), x2);
+    int rc = pst_open_fbt<Fq2>(ctx, st, st->t_php.u(), st->nv - k, p->q.u(), k, da.u(), x2);
     if (rc) return rc;
     TPST_HIP(ctx, xyzz_to_affine_canonical<Fq2>(s, x2, canon.u(), k));
     TPST_HIP(ctx, hipMemcpyAsync(proof->pst_proof, canon.p, (size_t)k * 192, hipMemcpyDeviceToHost, s));

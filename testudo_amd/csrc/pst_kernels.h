@@ -32,6 +32,11 @@ template <class F>
 hipError_t compress_points(hipStream_t s, uint32_t* d_v, size_t split, const uint32_t* d_k);
 hipError_t compress_fr(hipStream_t s, uint32_t* d_y, size_t split, const uint32_t* d_kmont);
 
+// MIPP scalars over the original bases (Montgomery W, y; canonical out):
+// y == nullptr: out[k] = W[k / len]; else out[k] = W[k / len] * y[(k % len + split) % len]
+hipError_t mipp_scalars(hipStream_t s, const uint32_t* d_W, const uint32_t* d_y, size_t len, size_t split, size_t n,
+                        uint32_t* d_out);
+
 // out[i] = k_i * P for a fixed affine (Montgomery) point P at d_p; scalars canonical
 template <class F>
 hipError_t fixed_base_mul(hipStream_t s, const uint32_t* d_p, const uint32_t* d_scalars, size_t n, uint32_t* d_out);
