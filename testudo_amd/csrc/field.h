@@ -35,6 +35,8 @@ struct FqCfg {
   static TPST_HD uint32_t r2(int i) { return params::FQ_R2[i]; }
   static TPST_HD uint32_t pm2(int i) { return params::FQ_PM2[i]; }
   static TPST_HD uint32_t r3(int i) { return params::FQ_R3[i]; }
+  static TPST_HD uint32_t invk(int i) { return params::FQ_INVK[i]; }
+  static constexpr int INV_ITERS = params::FQ_INV_ITERS;
   static constexpr uint32_t INV = params::FQ_INV;
   static constexpr bool P0_IS_ONE = true;  // p = 1 mod 2^32 -> m = -t0
 };
@@ -46,6 +48,8 @@ struct FrCfg {
   static TPST_HD uint32_t r2(int i) { return params::FR_R2[i]; }
   static TPST_HD uint32_t pm2(int i) { return params::FR_PM2[i]; }
   static TPST_HD uint32_t r3(int i) { return params::FR_R3[i]; }
+  static TPST_HD uint32_t invk(int i) { return params::FR_INVK[i]; }
+  static constexpr int INV_ITERS = params::FR_INV_ITERS;
   static constexpr uint32_t INV = params::FR_INV;
   static constexpr bool P0_IS_ONE = true;  // r = 1 mod 2^32
 };
@@ -262,51 +266,117 @@ TPST_HD Fp<C> from_mont(const Fp<C>& a) {  // Montgomery -> canonical
   return mul(a, one);
 }
 
-// Inverse by binary extended Euclid on the canonical integer (variable time:
-// the MSM / pairing values are public), then one Montgomery product by R^3:
-// (aR)^-1 * R^3 / R = a^-1 R.  ~2*log2(p) shift/subtract steps instead of the
-// ~570 dependent multiplies of Fermat.  a == 0 -> 0.
-template <class C>
-TPST_HD void limbs_shr1(uint32_t* x, uint32_t top) {
+// ---------------------------------------------------------------- inverse --
+// Constant-flow modular inverse: Pornin's optimised binary GCD (eprint
+// 2020/972, Alg. 2, k = 32).  Each outer iteration runs 31 divsteps on 64-bit
+// approximations of (a, b) (low 31 bits + top 33 bits), then applies the
+// accumulated 2x2 matrix to the full-width a, b and to the Bezout
+// coefficients u, v (mod m).  No data-dependent branches: every lane of a wave
+// follows the same path (the previous binary GCD diverged and cost ~1 ms per
+// wave of 64 different inputs).  Result v 2^-t is fixed up, together with
+// the Montgomery factors, by one product with K = 2^-t R^3.  a == 0 -> 0.
+//
+// x*|fx| +/- y*|fy| for signed fx, fy (|f| <= 2^31): magnitude in r[N+2], returns sign
+template <int N>
+TPST_HD bool lincomb(const uint32_t* x, int64_t fx, const uint32_t* y, int64_t fy, uint32_t* r) {
+  const bool sx = fx < 0, sy = fy < 0;
+  const uint32_t mx = (uint32_t)(sx ? -fx : fx), my = (uint32_t)(sy ? -fy : fy);
+  uint32_t p1[N + 1], p2[N + 1];
+  uint64_t c1 = 0, c2 = 0;
 #pragma unroll
-  for (int i = 0; i < C::N - 1; i++) x[i] = (x[i] >> 1) | (x[i + 1] << 31);
-  x[C::N - 1] = (x[C::N - 1] >> 1) | (top << 31);
-}
-
-// x = x/2 mod p  (x < p)
-template <class C>
-TPST_HD void half_mod(uint32_t* x) {
-  if (x[0] & 1u) {
-    uint64_t c = 0;
+  for (int i = 0; i < N; i++) {
+    c1 += (uint64_t)x[i] * mx;
+    p1[i] = (uint32_t)c1;
+    c1 >>= 32;
+    c2 += (uint64_t)y[i] * my;
+    p2[i] = (uint32_t)c2;
+    c2 >>= 32;
+  }
+  p1[N] = (uint32_t)c1;
+  p2[N] = (uint32_t)c2;
+  // sum and difference, then select
+  uint32_t sm[N + 2], df[N + 1];
+  uint64_t cs = 0;
+  int64_t bd = 0;
 #pragma unroll
-    for (int i = 0; i < C::N; i++) {
-      c += (uint64_t)x[i] + C::p(i);
-      x[i] = (uint32_t)c;
-      c >>= 32;
-    }
-    limbs_shr1<C>(x, (uint32_t)c);
-  } else {
-    limbs_shr1<C>(x, 0u);
+  for (int i = 0; i <= N; i++) {
+    cs += (uint64_t)p1[i] + p2[i];
+    sm[i] = (uint32_t)cs;
+    cs >>= 32;
+    const int64_t d = (int64_t)p1[i] - p2[i] + bd;
+    df[i] = (uint32_t)d;
+    bd = d >> 32;
   }
+  sm[N + 1] = (uint32_t)cs;
+  const bool borrow = bd != 0;
+  // negate df if it went negative
+  const uint32_t nm = borrow ? 0xffffffffu : 0u;
+  uint64_t cn = borrow ? 1u : 0u;
+#pragma unroll
+  for (int i = 0; i <= N; i++) {
+    cn += (uint64_t)(df[i] ^ nm);
+    df[i] = (uint32_t)cn;
+    cn >>= 32;
+  }
+  const bool same = sx == sy;
+#pragma unroll
+  for (int i = 0; i <= N; i++) r[i] = same ? sm[i] : df[i];
+  r[N + 1] = same ? sm[N + 1] : 0u;
+  return same ? sx : (borrow ? sy : sx);
 }
 
 template <class C>
-TPST_HD bool limbs_geq(const uint32_t* a, const uint32_t* b) {
-  for (int i = C::N - 1; i >= 0; i--) {
-    if (a[i] != b[i]) return a[i] > b[i];
-  }
-  return true;
-}
-
-template <class C>
-TPST_HD void limbs_sub(uint32_t* a, const uint32_t* b) {  // a -= b, a >= b
+TPST_HD void inv_matrix_mod(const uint32_t* u, int64_t fu, const uint32_t* v, int64_t fv, uint32_t* out) {
+  constexpr int N = C::N;
+  uint32_t m[N + 2];
+  const bool neg = lincomb<N>(u, fu, v, fv, m);
+  // m < 2^33 p: quotient estimate from the top 4 limbs (error <= 1 either way)
+  double top = 0.0, pd = 0.0;
+#pragma unroll
+  for (int i = N + 1; i >= N - 2; i--) top = top * 4294967296.0 + (double)m[i];
+#pragma unroll
+  for (int i = N - 1; i >= N - 2; i--) pd = pd * 4294967296.0 + (double)C::p(i);
+  double qd = top / pd;  // units: 2^(32 (N-2)) / 2^(32 (N-2))
+  if (qd < 0.0) qd = 0.0;
+  const uint64_t q = (uint64_t)qd;
+  const uint32_t ql = (uint32_t)q, qh = (uint32_t)(q >> 32);
+  // r = m - q p  (signed, N+2 limbs)
   int64_t br = 0;
+  uint64_t cl = 0, ch = 0;
+  uint32_t r[N + 2];
 #pragma unroll
-  for (int i = 0; i < C::N; i++) {
-    const int64_t d = (int64_t)a[i] - b[i] + br;
-    a[i] = (uint32_t)d;
+  for (int i = 0; i < N + 2; i++) {
+    const uint32_t pi = i < N ? C::p(i) : 0u;
+    const uint32_t pim1 = (i >= 1 && i - 1 < N) ? C::p(i - 1) : 0u;
+    cl += (uint64_t)ql * pi;
+    ch += (uint64_t)qh * pim1;
+    const uint32_t sub_l = (uint32_t)cl, sub_h = (uint32_t)ch;
+    cl >>= 32;
+    ch >>= 32;
+    const int64_t d = (int64_t)m[i] - sub_l - sub_h + br;
+    r[i] = (uint32_t)d;
     br = d >> 32;
   }
+  // r in (-p, 2p): fix with one conditional add and one conditional subtract
+  const bool negr = (int32_t)r[N + 1] < 0;
+  {
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      c += (uint64_t)r[i] + (negr ? C::p(i) : 0u);
+      r[i] = (uint32_t)c;
+      c >>= 32;
+    }
+  }
+  Fp<C> rr;
+#pragma unroll
+  for (int i = 0; i < N; i++) rr.v[i] = r[i];
+  reduce_once(rr);
+  // negative combination: p - r (r != 0)
+  const bool nz = !is_zero(rr);
+  Fp<C> nr = sub(Fp<C>::zero(), rr);
+#pragma unroll
+  for (int i = 0; i < N; i++) out[i] = (neg && nz) ? nr.v[i] : rr.v[i];
 }
 
 template <class C>
@@ -317,38 +387,102 @@ TPST_HD bool limbs_is_one(const uint32_t* a) {
   return acc == 0;
 }
 
+// bits [s, s + 33) of x (s >= 0)
 template <class C>
-TPST_NI Fp<C> inv(const Fp<C>& a) {
-  if (is_zero(a)) return a;
-  uint32_t u[C::N], v[C::N];
-  Fp<C> x1 = Fp<C>::zero(), x2 = Fp<C>::zero();
-  x1.v[0] = 1;
+TPST_HD uint64_t bits33(const uint32_t* x, int s) {
+  uint64_t w = 0;
 #pragma unroll
   for (int i = 0; i < C::N; i++) {
-    u[i] = a.v[i];
-    v[i] = C::p(i);
+    const int sh = 32 * i - s;
+    const uint64_t xi = x[i];
+    if (sh >= 0 && sh < 64) w |= xi << sh;
+    if (sh < 0 && sh > -32) w |= xi >> (-sh);
   }
-  while (!limbs_is_one<C>(u) && !limbs_is_one<C>(v)) {
-    while ((u[0] & 1u) == 0) {
-      limbs_shr1<C>(u, 0u);
-      half_mod<C>(x1.v);
-    }
-    while ((v[0] & 1u) == 0) {
-      limbs_shr1<C>(v, 0u);
-      half_mod<C>(x2.v);
-    }
-    if (limbs_geq<C>(u, v)) {
-      limbs_sub<C>(u, v);
-      x1 = sub(x1, x2);
-    } else {
-      limbs_sub<C>(v, u);
-      x2 = sub(x2, x1);
-    }
-  }
-  Fp<C> r3;
+  return w & ((1ull << 33) - 1);
+}
+
+template <class C>
+TPST_NI Fp<C> inv(const Fp<C>& y) {
+  constexpr int N = C::N;
+  uint32_t a[N], b[N], u[N], v[N];
 #pragma unroll
-  for (int i = 0; i < C::N; i++) r3.v[i] = C::r3(i);
-  return mul(limbs_is_one<C>(u) ? x1 : x2, r3);
+  for (int i = 0; i < N; i++) {
+    a[i] = y.v[i];
+    b[i] = C::p(i);
+    u[i] = i == 0 ? 1u : 0u;
+    v[i] = 0;
+  }
+  for (int it = 0; it < C::INV_ITERS; it++) {
+    // n = max(bitlen(a | b), 64); approximations from bits [n - 33, n) and [0, 31)
+    int nb = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      const uint32_t x = a[i] | b[i];
+#if defined(__HIP_DEVICE_COMPILE__)
+      const int bl = x ? 32 - __clz((int)x) : 0;
+#else
+      const int bl = x ? 32 - __builtin_clz(x) : 0;
+#endif
+      nb = x ? 32 * i + bl : nb;
+    }
+    const int n = nb > 64 ? nb : 64;
+    uint64_t ab = (uint64_t)(a[0] & 0x7fffffffu) | (bits33<C>(a, n - 33) << 31);
+    uint64_t bb = (uint64_t)(b[0] & 0x7fffffffu) | (bits33<C>(b, n - 33) << 31);
+    int64_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+#pragma unroll 1
+    for (int j = 0; j < 31; j++) {
+      const uint64_t odd = 0ull - (ab & 1u);
+      const uint64_t sw = odd & (0ull - (uint64_t)(ab < bb));
+      const uint64_t t = (ab ^ bb) & sw;
+      ab ^= t;
+      bb ^= t;
+      const int64_t tf = (f0 ^ f1) & (int64_t)sw, tg = (g0 ^ g1) & (int64_t)sw;
+      f0 ^= tf;
+      f1 ^= tf;
+      g0 ^= tg;
+      g1 ^= tg;
+      ab -= bb & odd;
+      f0 -= f1 & (int64_t)odd;
+      g0 -= g1 & (int64_t)odd;
+      ab >>= 1;
+      f1 += f1;
+      g1 += g1;
+    }
+    // (a, b) <- ((f0 a + g0 b), (f1 a + g1 b)) / 2^31, signs folded into the matrix
+    uint32_t na[N + 2], nbv[N + 2];
+    const bool sa = lincomb<N>(a, f0, b, g0, na);
+    const bool sb = lincomb<N>(a, f1, b, g1, nbv);
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      a[i] = (na[i] >> 31) | (na[i + 1] << 1);
+      b[i] = (nbv[i] >> 31) | (nbv[i + 1] << 1);
+    }
+    if (sa) {
+      f0 = -f0;
+      g0 = -g0;
+    }
+    if (sb) {
+      f1 = -f1;
+      g1 = -g1;
+    }
+    uint32_t nu[N], nv[N];
+    inv_matrix_mod<C>(u, f0, v, g0, nu);
+    inv_matrix_mod<C>(u, f1, v, g1, nv);
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      u[i] = nu[i];
+      v[i] = nv[i];
+    }
+  }
+  // b == gcd == 1 for invertible inputs
+  Fp<C> r;
+#pragma unroll
+  for (int i = 0; i < N; i++) r.v[i] = v[i];
+  Fp<C> k;
+#pragma unroll
+  for (int i = 0; i < N; i++) k.v[i] = C::invk(i);
+  r = mul(r, k);
+  return limbs_is_one<C>(b) ? r : Fp<C>::zero();
 }
 
 // small constant multiples

@@ -4,6 +4,7 @@
 #include "../../include/tpst.h"
 #include "ctx.h"
 #include "device_util.h"
+#include "wave_tower.h"
 
 using namespace tpst;
 
@@ -28,6 +29,120 @@ __global__ void k_mb_madd(int iters, uint32_t* out) {
   store_f<Fq>(out + 12 * (size_t)t, acc.X);
 }
 
+__global__ void k_mb_inv(int iters, uint32_t* out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  Fq a = Fq::one();
+  a.v[0] ^= t * 0x9E3779B9u;
+  a.v[3] ^= t;
+  for (int i = 0; i < iters; i++) {
+    a = inv(a);
+    a.v[1] ^= 1u;
+  }
+  store_f<Fq>(out + 12 * (size_t)t, a);
+}
+
+// one wave running `iters` stages of wave-engine op `op` (wave_tower.h)
+__global__ void __launch_bounds__(64) k_mb_wave(int op, int iters, uint32_t* out) {
+  extern __shared__ uint4 smem4[];
+  wave::lds_t* prog = (wave::lds_t*)(smem4);
+  const uint32_t len = wave::OP_LEN[op];
+  for (uint32_t i = threadIdx.x; i < len; i += 64) prog[i] = wave::BLOB[wave::OP_OFF[op] + i];
+  wave::lds_t* vals = prog + ((len + 3) & ~3u);
+  wave::load_consts(vals, 0);
+  const int base = wave::N_CONSTS;
+  for (int i = threadIdx.x; i < 64 + 4 * 48; i += 64) {
+    Fq v = Fq::one();
+    v.v[0] ^= i;
+    wave::put_slot(vals, base + i, v);
+  }
+  __syncthreads();
+  const wave::Eng e{vals, base, 0};
+  const int A = base + 64, B = A + 48, Cr = B + 48, D = Cr + 48;
+  for (int it = 0; it < iters; it++) wave::run(e, prog, A, B, Cr, D);
+  if (threadIdx.x < 12) out[threadIdx.x] = vals[Cr * wave::SLOT + threadIdx.x];
+}
+
+// the same stage with s_memtime stamps between its parts (lane 0 totals):
+// [0] X/Y forms, [1] Montgomery product, [2] product store + sync,
+// [3] output forms, [4] output reduce + store + sync
+__global__ void __launch_bounds__(64) k_mb_wave_prof(int op, int iters, unsigned long long* out) {
+  extern __shared__ uint4 smem4[];
+  wave::lds_t* prog = (wave::lds_t*)(smem4);
+  const uint32_t len = wave::OP_LEN[op];
+  for (uint32_t i = threadIdx.x; i < len; i += 64) prog[i] = wave::BLOB[wave::OP_OFF[op] + i];
+  wave::lds_t* vals = prog + ((len + 3) & ~3u);
+  wave::load_consts(vals, 0);
+  const int base = wave::N_CONSTS;
+  for (int i = threadIdx.x; i < 64 + 4 * 48; i += 64) {
+    Fq v = Fq::one();
+    v.v[0] ^= i;
+    wave::put_slot(vals, base + i, v);
+  }
+  __syncthreads();
+  const wave::Eng e{vals, base, 0};
+  const int A = base + 64, B = A + 48, Cr = B + 48;
+  unsigned long long acc[5] = {0, 0, 0, 0, 0};
+  const int lane = threadIdx.x;
+  const wave::lds_t* blk = prog;
+  for (int it = 0; it < iters; it++) {
+    const uint32_t hdr = __builtin_amdgcn_readfirstlane(blk[0]);
+    const uint32_t hdr1 = __builtin_amdgcn_readfirstlane(blk[1]);
+    const int np = hdr & 0xff, no = (hdr >> 8) & 0xff, nc = hdr >> 24;
+    const int tx = hdr1 & 0xff, ty = (hdr1 >> 8) & 0xff, tc = (hdr1 >> 16) & 0xff;
+    const uint64_t bases = wave::pack_bases(e, A, B);
+    const wave::lds_t* X = blk + 2;
+    const wave::lds_t* Y = X + tx * np;
+    const wave::lds_t* CH = Y + ty * np;
+    const wave::lds_t* DST = CH + tc * nc + no;
+    unsigned long long t0 = clock64();
+    uint32_t xw[13], yw[13];
+    Fq x, y, pr;
+    if (lane < np) {
+      wave::form(e, X + lane, np, tx, bases, xw);
+      wave::form(e, Y + lane, np, ty, bases, yw);
+#pragma unroll
+      for (int i = 0; i < 12; i++) {
+        x.v[i] = xw[i];
+        y.v[i] = yw[i];
+      }
+    }
+    unsigned long long t1 = clock64();
+    if (lane < np) pr = mul(x, y);
+    unsigned long long t2 = clock64();
+    if (lane < np) wave::put_slot(vals, base + lane, pr);
+    wave::wave_sync();
+    unsigned long long t3 = clock64();
+    uint32_t w[13];
+    if (lane < nc) wave::form(e, CH + lane, nc, tc, bases, w);
+    unsigned long long t4 = clock64();
+    if (lane < no) wave::put_slot(vals, Cr + (DST[lane] & 0xff), wave::reduce_wide(w));
+    wave::wave_sync();
+    unsigned long long t5 = clock64();
+    acc[0] += t1 - t0;
+    acc[1] += t2 - t1;
+    acc[2] += t3 - t2;
+    acc[3] += t4 - t3;
+    acc[4] += t5 - t4;
+  }
+  if (lane == 0)
+    for (int i = 0; i < 5; i++) out[i] = acc[i];
+}
+
+extern "C" int tpst_microbench_wave_phases(tpst_ctx* ctx, int op, int iters, uint64_t* cycles5) {
+  if (!ctx || !cycles5 || op < 0 || op >= wave::N_OPS || iters <= 0) return fail(ctx, TPST_E_ARG, "bad argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  ctx->io.reset();
+  TPST_HIP(ctx, ctx->io.reserve(256));
+  unsigned long long* d = ctx->io.take<unsigned long long>(8);
+  const size_t lds = (((wave::OP_LEN[op] + 3) & ~3u) + (size_t)(wave::N_CONSTS + 64 + 4 * 48) * wave::SLOT) * 4;
+  k_mb_wave_prof<<<1, 64, lds, ctx->stream>>>(op, iters, d);
+  TPST_HIP(ctx, hipGetLastError());
+  TPST_HIP(ctx, hipMemcpyAsync(cycles5, d, 40, hipMemcpyDeviceToHost, ctx->stream));
+  TPST_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return TPST_OK;
+}
+
 extern "C" int tpst_microbench(tpst_ctx* ctx, int kind, size_t threads, int iters, double* ms) {
   if (!ctx || !ms || threads == 0 || iters <= 0) return fail(ctx, TPST_E_ARG, "bad argument");
   std::lock_guard<std::mutex> lk(ctx->mu);
@@ -45,7 +160,13 @@ extern "C" int tpst_microbench(tpst_ctx* ctx, int kind, size_t threads, int iter
     k_mb_fqmul<<<grid, bs, 0, ctx->stream>>>(iters, d);
   else if (kind == 1)
     k_mb_madd<<<grid, bs, 0, ctx->stream>>>(iters, d);
-  else
+  else if (kind == 2)
+    k_mb_inv<<<grid, bs, 0, ctx->stream>>>(iters, d);
+  else if (kind >= 16 && kind < 16 + wave::N_OPS) {
+    const int op = kind - 16;
+    const size_t lds = (((wave::OP_LEN[op] + 3) & ~3u) + (size_t)(wave::N_CONSTS + 64 + 4 * 48) * wave::SLOT) * 4;
+    k_mb_wave<<<1, 64, lds, ctx->stream>>>(op, iters, d);
+  } else
     return fail(ctx, TPST_E_ARG, "unknown microbench kind");
   TPST_HIP(ctx, hipGetLastError());
   TPST_HIP(ctx, hipEventRecord(e1, ctx->stream));

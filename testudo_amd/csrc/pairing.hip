@@ -26,22 +26,17 @@ constexpr int PW = 4;
 constexpr int PW_SLOTS = 64 + 44;
 constexpr int PW_OPS[] = {wave::OP_G2_DBL1, wave::OP_G2_DBL2, wave::OP_G2_DBL3, wave::OP_G2_DBL4,
                           wave::OP_G2_ADD1, wave::OP_G2_ADD2, wave::OP_G2_ADD3, wave::OP_G2_ADD4};
-constexpr int pw_prog_words() {
-  int s = 0;
-  for (int i = 0; i < 8; i++) s += (int)wave::OP_LEN[PW_OPS[i]];
-  return (s + 3) & ~3;
-}
-constexpr int PW_PROG = pw_prog_words();
+constexpr wave::OpSet<8> PW_SET(PW_OPS);
+constexpr int PW_PROG = PW_SET.words;
 constexpr size_t PW_LDS = (size_t)(PW_PROG + (wave::N_CONSTS + PW * PW_SLOTS) * wave::SLOT) * 4;
 static_assert(PW_LDS <= 65536, "prepare kernel LDS");
 
 __global__ void __launch_bounds__(64 * PW) k_g2_prepare_wave(const uint32_t* __restrict__ g2, size_t n,
                                                              LineCoeff* __restrict__ coeffs) {
   extern __shared__ uint4 smem4[];
-  uint32_t* prog = reinterpret_cast<uint32_t*>(smem4);
-  uint32_t* vals = prog + PW_PROG;
-  uint32_t off[8];
-  wave::load_ops(prog, PW_OPS, 8, off);
+  wave::lds_t* prog = (wave::lds_t*)(smem4);
+  wave::lds_t* vals = prog + PW_PROG;
+  wave::load_set(prog, PW_SET);
   wave::load_consts(vals, 0);
   __syncthreads();
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -63,12 +58,14 @@ __global__ void __launch_bounds__(64 * PW) k_g2_prepare_wave(const uint32_t* __r
   Fq* cf = reinterpret_cast<Fq*>(coeffs);
   int idx = 0;
   for (int b = X_BITS - 2; b >= 0; b--) {
-    for (int k = 0; k < 4; k++) wave::run(e, prog + off[k], R, R, R);
+#pragma unroll
+    for (int k = 0; k < 4; k++) wave::run(e, prog + PW_SET.off[k], R, R, R);
     if (lane < 6) cf[((size_t)idx * n + pi) * 6 + lane] = wave::get_slot(vals, R + 6 + lane);
     idx++;
     if ((params::BLS_X >> b) & 1) {
       wave::wave_sync();
-      for (int k = 4; k < 8; k++) wave::run(e, prog + off[k], R, R, R);
+#pragma unroll
+      for (int k = 4; k < 8; k++) wave::run(e, prog + PW_SET.off[k], R, R, R);
       if (lane < 6) cf[((size_t)idx * n + pi) * 6 + lane] = wave::get_slot(vals, R + 6 + lane);
       idx++;
     }
@@ -89,8 +86,9 @@ hipError_t g2_prepare_batch(hipStream_t s, const uint32_t* d_g2, size_t n, LineC
 // bit k's stages run.
 constexpr int MW = 4;                          // waves per workgroup
 constexpr int MW_SLOTS = 64 + 12 + 12 + 14 + 12;  // PROD, F, F2, B (lines + P), D (prepared lines)
-constexpr int MW_PROG = ((int)(wave::OP_LEN[wave::OP_SQR_LP1] + wave::OP_LEN[wave::OP_SQR_LP2] +
-                               wave::OP_LEN[wave::OP_MUL034]) + 3) & ~3;
+constexpr int MW_OPS[] = {wave::OP_SQR_LP1, wave::OP_SQR_LP2, wave::OP_MUL034};
+constexpr wave::OpSet<3> MW_SET(MW_OPS);
+constexpr int MW_PROG = MW_SET.words;
 constexpr size_t MW_LDS = (size_t)(MW_PROG + MW * MW_SLOTS * wave::SLOT) * 4;
 static_assert(MW_LDS <= 65536, "Miller kernel LDS");
 
@@ -99,11 +97,9 @@ __global__ void __launch_bounds__(64 * MW) k_miller_wave(const uint32_t* __restr
                                                          const LineCoeff* __restrict__ coeffs, size_t np,
                                                          Fq12* __restrict__ partial) {
   extern __shared__ uint4 smem4[];
-  uint32_t* prog = reinterpret_cast<uint32_t*>(smem4);
-  uint32_t* vals = prog + MW_PROG;
-  const int ops[3] = {wave::OP_SQR_LP1, wave::OP_SQR_LP2, wave::OP_MUL034};
-  uint32_t off[3];
-  wave::load_ops(prog, ops, 3, off);
+  wave::lds_t* prog = (wave::lds_t*)(smem4);
+  wave::lds_t* vals = prog + MW_PROG;
+  wave::load_set(prog, MW_SET);
   __syncthreads();
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const size_t pi = (size_t)blockIdx.x * MW + w;
@@ -135,10 +131,13 @@ __global__ void __launch_bounds__(64 * MW) k_miller_wave(const uint32_t* __restr
       if (lane < 6 || nadd) pre = cf[((size_t)(nidx + (lane >= 6)) * np + pi) * 6 + lane % 6];
     }
     wave::wave_sync();
-    wave::run(e, prog + off[add ? 1 : 0], F, B, F2, D);
-    wave::run(e, prog + off[2], F2, D, F);
+    if (add)
+      wave::run(e, prog + MW_SET.off[1], F, B, F2, D);
+    else
+      wave::run(e, prog + MW_SET.off[0], F, B, F2, D);
+    wave::run(e, prog + MW_SET.off[2], F2, D, F);
     if (add) {
-      wave::run(e, prog + off[2], F, D + 6, F2);
+      wave::run(e, prog + MW_SET.off[2], F, D + 6, F2);
       const int t = F;
       F = F2;
       F2 = t;
@@ -156,26 +155,22 @@ constexpr int FE_OPS[] = {wave::OP_F12_MUL, wave::OP_CYC_SQR, wave::OP_FROB1, wa
                           wave::OP_INV1,    wave::OP_INV2,    wave::OP_INV3,  wave::OP_INV4,  wave::OP_INV5,
                           wave::OP_INV6,    wave::OP_INV7};
 constexpr int N_FE_OPS = sizeof(FE_OPS) / sizeof(FE_OPS[0]);
-constexpr int fe_prog_words() {
-  int s = 0;
-  for (int i = 0; i < N_FE_OPS; i++) s += (int)wave::OP_LEN[FE_OPS[i]];
-  return (s + 3) & ~3;
-}
-constexpr int FW_PROG = fe_prog_words();
+constexpr wave::OpSet<N_FE_OPS> FE_SET(FE_OPS);
+constexpr int FW_PROG = FE_SET.words;
 constexpr size_t FW_LDS = (size_t)(FW_PROG + (wave::N_CONSTS + FW * FW_SLOTS + FE_SLOTS) * wave::SLOT) * 4;
 static_assert(FW_LDS <= 65536, "final-exponentiation kernel LDS");
 
 enum { FE_MUL, FE_CYC, FE_FROB1, FE_FROB2, FE_CONJ, FE_INV1 };
 
-__device__ int fe_exp_by_x(const wave::Eng& e, const uint32_t* const* op, int src, int r1, int r2) {
+__device__ int fe_exp_by_x(const wave::Eng& e, const wave::lds_t* prog, int src, int r1, int r2) {
   int cur = src;
   for (int b = X_BITS - 2; b >= 0; b--) {
     int nxt = cur == r1 ? r2 : r1;
-    wave::run(e, op[FE_CYC], cur, 0, nxt);
+    wave::run(e, prog + FE_SET.off[FE_CYC], cur, 0, nxt);
     cur = nxt;
     if ((params::BLS_X >> b) & 1) {
       nxt = cur == r1 ? r2 : r1;
-      wave::run(e, op[FE_MUL], cur, src, nxt);
+      wave::run(e, prog + FE_SET.off[FE_MUL], cur, src, nxt);
       cur = nxt;
     }
   }
@@ -184,59 +179,56 @@ __device__ int fe_exp_by_x(const wave::Eng& e, const uint32_t* const* op, int sr
 
 // f (register F) -> f^(3(p^12-1)/r); returns the result register.  Same chain
 // as final_exponentiation() in pairing.h (eprint 2020/875).
-__device__ int fe_final_exp(const wave::Eng& e, const uint32_t* const* op, int F, int regs, int I) {
+__device__ int fe_final_exp(const wave::Eng& e, const wave::lds_t* prog, int F, int regs, int I) {
   const int lane = threadIdx.x & 63;
-  int R[10];
-  for (int i = 0; i < 10; i++) R[i] = regs + 12 * i;
+#define R(i) (regs + 12 * (i))
   // f^-1 through the tower norms, one Fq inversion on lane 0
-  wave::run(e, op[FE_INV1 + 0], F, 0, I + 0);        // t = c0^2 - v c1^2
-  wave::run(e, op[FE_INV1 + 1], I + 0, 0, I + 6);    // Fq6 adjugate c'
-  wave::run(e, op[FE_INV1 + 2], I + 6, I + 0, I + 12);  // Fq6 norm t'
-  wave::run(e, op[FE_INV1 + 3], I + 12, 0, I + 14);  // Fq2 norm n
+  wave::run(e, prog + FE_SET.off[FE_INV1 + 0], F, 0, I + 0);        // t = c0^2 - v c1^2
+  wave::run(e, prog + FE_SET.off[FE_INV1 + 1], I + 0, 0, I + 6);    // Fq6 adjugate c'
+  wave::run(e, prog + FE_SET.off[FE_INV1 + 2], I + 6, I + 0, I + 12);  // Fq6 norm t'
+  wave::run(e, prog + FE_SET.off[FE_INV1 + 3], I + 12, 0, I + 14);  // Fq2 norm n
   if (lane == 0) wave::put_slot(e.lds, I + 15, inv(wave::get_slot(e.lds, I + 14)));
   wave::wave_sync();
-  wave::run(e, op[FE_INV1 + 4], I + 12, I + 15, I + 16);  // t'^-1
-  wave::run(e, op[FE_INV1 + 5], I + 6, I + 16, I + 18);   // t^-1
-  wave::run(e, op[FE_INV1 + 6], F, I + 18, R[0]);         // f^-1
+  wave::run(e, prog + FE_SET.off[FE_INV1 + 4], I + 12, I + 15, I + 16);  // t'^-1
+  wave::run(e, prog + FE_SET.off[FE_INV1 + 5], I + 6, I + 16, I + 18);   // t^-1
+  wave::run(e, prog + FE_SET.off[FE_INV1 + 6], F, I + 18, R(0));         // f^-1
   // easy part
-  wave::run(e, op[FE_CONJ], F, 0, R[1]);
-  wave::run(e, op[FE_MUL], R[1], R[0], R[2]);  // r = conj(f) f^-1
-  wave::run(e, op[FE_FROB2], R[2], 0, R[1]);
-  wave::run(e, op[FE_MUL], R[1], R[2], R[3]);  // r = r^(p^2) r
+  wave::run(e, prog + FE_SET.off[FE_CONJ], F, 0, R(1));
+  wave::run(e, prog + FE_SET.off[FE_MUL], R(1), R(0), R(2));  // r = conj(f) f^-1
+  wave::run(e, prog + FE_SET.off[FE_FROB2], R(2), 0, R(1));
+  wave::run(e, prog + FE_SET.off[FE_MUL], R(1), R(2), R(3));  // r = r^(p^2) r
   // hard part
-  wave::run(e, op[FE_CYC], R[3], 0, R[4]);  // y0
-  int t = fe_exp_by_x(e, op, R[3], R[5], R[6]);
-  wave::run(e, op[FE_CONJ], R[3], 0, R[7]);  // y2 = conj(r)
-  wave::run(e, op[FE_MUL], t, R[7], R[8]);   // y1 = y1 y2
-  t = fe_exp_by_x(e, op, R[8], R[5], R[6]);  // y2
-  wave::run(e, op[FE_CONJ], R[8], 0, R[7]);
-  wave::run(e, op[FE_MUL], R[7], t, R[9]);   // y1 = conj(y1) y2
-  t = fe_exp_by_x(e, op, R[9], R[5], R[6]);  // y2
-  wave::run(e, op[FE_FROB1], R[9], 0, R[7]);
-  wave::run(e, op[FE_MUL], R[7], t, R[8]);   // y1 = frob(y1) y2
-  wave::run(e, op[FE_MUL], R[3], R[4], R[0]);  // r = r y0
-  const int y0 = fe_exp_by_x(e, op, R[8], R[5], R[6]);
-  const int y2 = fe_exp_by_x(e, op, y0, y0 == R[5] ? R[6] : R[5], R[1]);
-  wave::run(e, op[FE_FROB2], R[8], 0, R[2]);  // y0 = frob2(y1)
-  wave::run(e, op[FE_CONJ], R[8], 0, R[3]);
-  wave::run(e, op[FE_MUL], R[3], y2, R[4]);   // y1 = conj(y1) y2
-  wave::run(e, op[FE_MUL], R[4], R[2], R[7]);  // y1 = y1 y0
-  wave::run(e, op[FE_MUL], R[0], R[7], R[9]);  // r = r y1
-  return R[9];
+  wave::run(e, prog + FE_SET.off[FE_CYC], R(3), 0, R(4));  // y0
+  int t = fe_exp_by_x(e, prog, R(3), R(5), R(6));
+  wave::run(e, prog + FE_SET.off[FE_CONJ], R(3), 0, R(7));  // y2 = conj(r)
+  wave::run(e, prog + FE_SET.off[FE_MUL], t, R(7), R(8));   // y1 = y1 y2
+  t = fe_exp_by_x(e, prog, R(8), R(5), R(6));  // y2
+  wave::run(e, prog + FE_SET.off[FE_CONJ], R(8), 0, R(7));
+  wave::run(e, prog + FE_SET.off[FE_MUL], R(7), t, R(9));   // y1 = conj(y1) y2
+  t = fe_exp_by_x(e, prog, R(9), R(5), R(6));  // y2
+  wave::run(e, prog + FE_SET.off[FE_FROB1], R(9), 0, R(7));
+  wave::run(e, prog + FE_SET.off[FE_MUL], R(7), t, R(8));   // y1 = frob(y1) y2
+  wave::run(e, prog + FE_SET.off[FE_MUL], R(3), R(4), R(0));  // r = r y0
+  const int y0 = fe_exp_by_x(e, prog, R(8), R(5), R(6));
+  const int y2 = fe_exp_by_x(e, prog, y0, y0 == R(5) ? R(6) : R(5), R(1));
+  wave::run(e, prog + FE_SET.off[FE_FROB2], R(8), 0, R(2));  // y0 = frob2(y1)
+  wave::run(e, prog + FE_SET.off[FE_CONJ], R(8), 0, R(3));
+  wave::run(e, prog + FE_SET.off[FE_MUL], R(3), y2, R(4));   // y1 = conj(y1) y2
+  wave::run(e, prog + FE_SET.off[FE_MUL], R(4), R(2), R(7));  // y1 = y1 y0
+  wave::run(e, prog + FE_SET.off[FE_MUL], R(0), R(7), R(9));  // r = r y1
+  return R(9);
+#undef R
 }
 
 __global__ void __launch_bounds__(64 * FW) k_final_wave(const Fq12* __restrict__ partial, size_t T,
                                                         Fq12* __restrict__ out) {
   extern __shared__ uint4 smem4[];
   __shared__ int acc_slot[FW];
-  uint32_t* prog = reinterpret_cast<uint32_t*>(smem4);
-  uint32_t* vals = prog + FW_PROG;
-  uint32_t off[N_FE_OPS];
-  wave::load_ops(prog, FE_OPS, N_FE_OPS, off);
+  wave::lds_t* prog = (wave::lds_t*)(smem4);
+  wave::lds_t* vals = prog + FW_PROG;
+  wave::load_set(prog, FE_SET);
   wave::load_consts(vals, 0);
   __syncthreads();
-  const uint32_t* op[N_FE_OPS];
-  for (int i = 0; i < N_FE_OPS; i++) op[i] = prog + off[i];
   const int w = threadIdx.x >> 6;
   const size_t g = blockIdx.x;
   const int base = wave::N_CONSTS + w * FW_SLOTS;
@@ -248,7 +240,7 @@ __global__ void __launch_bounds__(64 * FW) k_final_wave(const Fq12* __restrict__
       wave::load_f12(vals, acc, partial + g * T + k);
     } else {
       wave::load_f12(vals, in, partial + g * T + k);
-      wave::run(e, op[FE_MUL], acc, in, tmp);
+      wave::run(e, prog + FE_SET.off[FE_MUL], acc, in, tmp);
       const int t = acc;
       acc = tmp;
       tmp = t;
@@ -259,13 +251,13 @@ __global__ void __launch_bounds__(64 * FW) k_final_wave(const Fq12* __restrict__
   __syncthreads();
   if (w != 0) return;
   for (int v = 1; v < FW; v++) {
-    wave::run(e, op[FE_MUL], acc, acc_slot[v], tmp);
+    wave::run(e, prog + FE_SET.off[FE_MUL], acc, acc_slot[v], tmp);
     const int t = acc;
     acc = tmp;
     tmp = t;
   }
   const int fe = wave::N_CONSTS + FW * FW_SLOTS;
-  const int r = fe_final_exp(e, op, acc, fe, fe + 120);
+  const int r = fe_final_exp(e, prog, acc, fe, fe + 120);
   wave::store_f12(vals, r, out + g);
 }
 

@@ -629,27 +629,48 @@ def main():
                  for k, lin in (sorted(lst.items()) if isinstance(lst, dict) else enumerate(lst))]
         no = len(olist)
         assert no <= 64
-        terms, info_x, info_y, info_o = [], [], [], []
-        hdr_len = 1 + 2 * np_ + 2 * no
-
-        def put(lin, info):
-            info.append((hdr_len + len(terms)) << 8 | len(lin))
-            for (kind, i), c in sorted(lin.items()):
-                terms.append(enc_term(kind, i, c))
-        for x, y in pg.products:
-            put(x, info_x)
-            put(y, info_y)
+        # long output forms are split into chunks summed by separate lanes
+        # (phase 2a), then combined per output (phase 2b): smallest chunk
+        # length that fits all chunks in one wave
+        lens_o = [max(1, len(lin)) for _, lin in olist]
+        tmax = 4
+        while sum(-(-n // tmax) for n in lens_o) > 64:
+            tmax += 1
+        chunks, info_o = [], []
         for _, lin in olist:
-            put(lin, info_o)
+            items = sorted(lin.items())
+            nch = max(1, -(-len(items) // tmax))
+            info_o.append(len(chunks) << 8 | nch)
+            per = -(-len(items) // nch) if items else 0
+            for c in range(nch):
+                chunks.append(items[c * per:(c + 1) * per])
+        nc = len(chunks)
+        assert nc <= 64
+        # term lists padded to a per-op uniform length (zero words = 0 * A[0])
+        # and stored term-major: term j of lane l at [j * lanes + l]
+        xs = [sorted(x.items()) for x, _ in pg.products]
+        ys = [sorted(y.items()) for _, y in pg.products]
+        tx = max((len(v) for v in xs), default=0)
+        ty = max((len(v) for v in ys), default=0)
+        tc = max((len(v) for v in chunks), default=0)
+        assert max(tx, ty, tc) <= 8, (name, tx, ty, tc)
+
+        def major(lists, t):
+            out = []
+            for j in range(t):
+                for items in lists:
+                    out.append(enc_term(items[j][0][0], items[j][0][1], items[j][1]) if j < len(items) else 0)
+            return out
         maxw = max((lin.weight() for _, lin in olist), default=0)
         assert maxw < 1024, (name, maxw)
-        block = [np_ | no << 8 | need_red << 16] + info_x + info_y + info_o + [d for d, _ in olist] + terms
+        block = ([np_ | no << 8 | need_red << 16 | nc << 24, tx | ty << 8 | tc << 16] + major(xs, tx) + major(ys, ty) +
+                 major(chunks, tc) + info_o + [d for d, _ in olist])
         offs.append(len(blob))
         lens.append(len(block))
         blob += block
         names.append(name)
-        stats.append("//   %-10s products %2d  outputs %2d  max out weight %3d  reduce_xy %d  words %4d" % (
-            name, np_, no, maxw, need_red, len(block)))
+        stats.append("//   %-10s products %2d (terms %d x %d)  outputs %2d  chunks %2d (<= %d terms)  max weight %3d  words %4d"
+                     % (name, np_, tx, ty, no, nc, tc, maxw, len(block)))
     lines += stats
     lines.append("enum OpId {%s, N_OPS};" % ", ".join("OP_" + n for n in names))
     lines.append("static constexpr uint32_t OP_OFF[N_OPS] = {%s};" % ", ".join(map(str, offs)))
