@@ -209,7 +209,7 @@ def main():
         dist.destroy_process_group()
 
 
-def pst_leg(ctx, log_n):
+def pst_leg(ctx, log_n, reps=5):
     """sqrt-PST commit + open at 2^log_n variables (BASELINE configs[2]),
     timed like benches/pst.rs:52-62: eval (get_q) before the open timer."""
     from testudo_amd import sqrt_pst as S
@@ -222,20 +222,29 @@ def pst_leg(ctx, log_n):
     pl = S.Polynomial.from_evaluations(ctx, Z)
     v = pl.eval(pt)
     ctx.synchronize()
-    t = time.perf_counter()
-    comms, T = pl.commit()
-    commit_s = time.perf_counter() - t
-    tr = S.PoseidonTranscript()
-    t = time.perf_counter()
-    U, pst_proof, mipp = pl.open(tr, comms, pt, T)
-    open_s = time.perf_counter() - t
+    # the first commit+open of the process (cold: code objects load, scratch
+    # arenas grow) is reported separately; then the median of `reps` warm runs
+    runs = []
+    for _ in range(reps + 1):
+        t = time.perf_counter()
+        comms, T = pl.commit()
+        commit_s = time.perf_counter() - t
+        tr = S.PoseidonTranscript()
+        t = time.perf_counter()
+        U, pst_proof, mipp = pl.open(tr, comms, pt, T)
+        open_s = time.perf_counter() - t
+        runs.append((commit_s, open_s))
+    cold = runs[0]
+    warm = sorted(runs[1:], key=lambda r: r[0] + r[1])[len(runs[1:]) // 2]
     t = time.perf_counter()
     ok = S.verify(ctx, S.PoseidonTranscript(), U, pt, v, pst_proof, mipp, T)
     verify_s = time.perf_counter() - t
-    return {"log_n": log_n, "commit_s": round(commit_s, 4), "open_s": round(open_s, 4),
-            "commit_plus_open_s": round(commit_s + open_s, 4), "verify_s": round(verify_s, 4),
-            "srs_setup_s": round(setup_s, 3), "verified": ok,
-            "note": "host-pointer API: commit time includes H2D of nothing (Z resident after from_evaluations)"}
+    return {"log_n": log_n, "commit_s": round(warm[0], 4), "open_s": round(warm[1], 4),
+            "commit_plus_open_s": round(warm[0] + warm[1], 4), "reps": reps,
+            "first_call": {"commit_s": round(cold[0], 4), "open_s": round(cold[1], 4)},
+            "verify_s": round(verify_s, 4), "srs_setup_s": round(setup_s, 3), "verified": ok,
+            "note": "host-pointer API: Z resident in HBM after from_evaluations; eval (get_q) before "
+                    "the open timer as in benches/pst.rs:50-62; SRS tables built in srs_setup"}
 
 
 def sharded_leg(ctx, log_n, dist, dev):

@@ -238,6 +238,8 @@ struct tpst_poly {
   bool has_q = false;
 };
 
+static int srs_fbt(tpst_ctx* ctx, SrsState* st, int odd);
+
 static std::unique_ptr<SrsState>& srs_slot(tpst_ctx* ctx) {
   static std::mutex mu;
   static std::vector<std::pair<tpst_ctx*, std::unique_ptr<SrsState>>> slots;
@@ -296,6 +298,12 @@ static int srs_install(tpst_ctx* ctx, int nv, const uint64_t* flat) {
     const size_t m = (size_t)1 << (nv - odd);
     TPST_HIP(ctx, st->hprep[odd].alloc(m * N_LINE_COEFFS * sizeof(LineCoeff)));
     TPST_HIP(ctx, g2_prepare_batch(s, st->ph[odd]->u(), m, (LineCoeff*)st->hprep[odd].p));
+  }
+  // fixed-base tables of the opening (a function of the key only, like the
+  // cached G2Prepared above): built here so that no open pays for them
+  for (int odd = 0; odd < 2 && odd < nv; odd++) {
+    int rc = srs_fbt(ctx, st.get(), odd);
+    if (rc) return rc;
   }
   TPST_HIP(ctx, hipStreamSynchronize(s));
   srs_slot(ctx) = std::move(st);
@@ -669,7 +677,8 @@ extern "C" int tpst_poly_ipp(tpst_ctx* ctx, int n, const uint64_t* comms, uint64
 // MIPP round's folds / cross terms are grouped MSMs over the ORIGINAL bases
 // with scalars that are products of the challenges so far.
 
-// lazily tabulate the SRS (fbt.h) for opening polynomials of parity `odd`
+// tabulate the SRS (fbt.h) for opening polynomials of parity `odd` (at SRS
+// install; the open path re-checks and is a no-op then)
 static int srs_fbt(tpst_ctx* ctx, SrsState* st, int odd) {
   hipStream_t s = ctx->stream;
   const int nv = st->nv;

@@ -2,7 +2,7 @@
 import sys
 import time
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from testudo_amd.engine import Context  # noqa: E402
 from testudo_amd import sqrt_pst as S  # noqa: E402
 
