@@ -142,6 +142,13 @@ int tpst_poly_commit_dev(tpst_ctx* ctx, tpst_poly* p, void* d_comms, void* d_T);
  * gathered commitment list (sqrt_pst.rs:128-143) -> T. */
 int tpst_poly_commit_rows(tpst_ctx* ctx, tpst_poly* p, size_t r0, size_t r1, uint64_t* comms);
 int tpst_poly_ipp(tpst_ctx* ctx, int n, const uint64_t* comms, uint64_t* T);
+/* Same row range with the IPP split across ranks: also returns this share's
+ * Miller-loop product prod_{r0<=i<r1} ml(C_i, h_i) BEFORE final
+ * exponentiation (canonical Fq12, 72 u64).  T = FE(product of every rank's
+ * partial) via tpst_gt_final_exp_product (sqrt_pst.rs:128-143 split by rows). */
+int tpst_poly_commit_rows_partial(tpst_ctx* ctx, tpst_poly* p, size_t r0, size_t r1, uint64_t* comms,
+                                  uint64_t* miller);
+int tpst_gt_final_exp_product(tpst_ctx* ctx, const uint64_t* partials, size_t k, uint64_t* T);
 /* Polynomial::open (sqrt_pst.rs:168-230); the transcript is updated in place */
 int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, const uint64_t* comms,
                    const uint64_t* point, const uint64_t* T, tpst_open_proof* proof);

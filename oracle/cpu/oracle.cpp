@@ -531,7 +531,7 @@ static Fq12 final_exp(const Fq12& f) {
   return r * y1;
 }
 
-static Fq12 multi_pairing(const Aff<Fq>* g1, const Aff<Fq2>* g2, size_t n) {
+static Fq12 miller_product(const Aff<Fq>* g1, const Aff<Fq2>* g2, size_t n) {
   // chunks of 4 pairs share f, chunks run in parallel (bls12/mod.rs)
   std::vector<Aff<Fq>> ps;
   std::vector<Aff<Fq2>> qs;
@@ -556,7 +556,11 @@ static Fq12 multi_pairing(const Aff<Fq>* g1, const Aff<Fq2>* g2, size_t n) {
   }
   Fq12 f = Fq12::one();
   for (auto& x : parts) f = f * x;
-  return final_exp(f);
+  return f;
+}
+
+static Fq12 multi_pairing(const Aff<Fq>* g1, const Aff<Fq2>* g2, size_t n) {
+  return final_exp(miller_product(g1, g2, n));
 }
 
 // --------------------------------------------------------- encodings -----
@@ -819,6 +823,27 @@ int orc_multi_pairing(const u64* g1, const u64* g2, size_t n, u64* out) {
     b[i] = g2_in(g2 + 24 * i);
   }
   multi_pairing(a.data(), b.data(), n).to_canon(out);
+  return 0;
+}
+
+// prod of the Miller loops of n pairs, before final exponentiation (the
+// per-rank IPP partial of the row-sharded commit)
+int orc_miller_product(const u64* g1, const u64* g2, size_t n, u64* out) {
+  std::vector<Aff<Fq>> a(n);
+  std::vector<Aff<Fq2>> b(n);
+  for (size_t i = 0; i < n; i++) {
+    a[i] = g1_in(g1 + 12 * i);
+    b[i] = g2_in(g2 + 24 * i);
+  }
+  miller_product(a.data(), b.data(), n).to_canon(out);
+  return 0;
+}
+
+// FE(prod of k canonical Fq12)
+int orc_gt_final_exp_product(const u64* parts, size_t k, u64* out) {
+  Fq12 f = Fq12::one();
+  for (size_t i = 0; i < k; i++) f = f * Fq12::from_canon(parts + 72 * i);
+  final_exp(f).to_canon(out);
   return 0;
 }
 

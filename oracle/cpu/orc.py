@@ -47,6 +47,8 @@ def load():
         "orc_g2_msm": (i, [_u64p, _u64p, sz, _u64p, i]),
         "orc_g1_msm_batch": (i, [_u64p, sz, _u64p, sz, sz, sz, _u64p]),
         "orc_multi_pairing": (i, [_u64p, _u64p, sz, _u64p]),
+        "orc_miller_product": (i, [_u64p, _u64p, sz, _u64p]),
+        "orc_gt_final_exp_product": (i, [_u64p, sz, _u64p]),
         "orc_g1_mul_gen": (i, [_u64p, sz, _u64p]),
         "orc_g2_mul_gen": (i, [_u64p, sz, _u64p]),
         "orc_srs_setup": (vp, [i, C.c_uint64]),
@@ -119,6 +121,23 @@ def multi_pairing(g1, g2):
     g2 = np.ascontiguousarray(g2, dtype=np.uint64)
     out = np.zeros(72, dtype=np.uint64)
     lib.orc_multi_pairing(_p(g1), _p(g2), len(g1), _p(out))
+    return out
+
+
+def miller_product(g1, g2):
+    lib = load()
+    g1 = np.ascontiguousarray(g1, dtype=np.uint64)
+    g2 = np.ascontiguousarray(g2, dtype=np.uint64)
+    out = np.zeros(72, dtype=np.uint64)
+    lib.orc_miller_product(_p(g1), _p(g2), len(g1), _p(out))
+    return out
+
+
+def gt_final_exp_product(parts):
+    lib = load()
+    parts = np.ascontiguousarray(parts, dtype=np.uint64).reshape(-1, 72)
+    out = np.zeros(72, dtype=np.uint64)
+    lib.orc_gt_final_exp_product(_p(parts), len(parts), _p(out))
     return out
 
 

@@ -1,8 +1,10 @@
 """world_size-2 gloo tests on CPU of the multi-rank paths:
 
 * the row-sharded commit orchestration (testudo_amd/distributed.py) with the
-  C++ oracle standing in for the per-rank GPU compute -- the gathered
-  commitment list and T must equal the single-process commit bit for bit;
+  C++ oracle standing in for the per-rank GPU compute (row MSMs + unreduced
+  Miller-loop partial per rank, one final exponentiation on rank 0) -- the
+  gathered commitment list and T must equal the single-process commit bit for
+  bit;
 * bench.py's timing aggregation (barrier + max over ranks).
 """
 import os
@@ -52,13 +54,11 @@ def _worker(rank, world, port, n, q):
         hvec = flat[hstart:hstart + C * 24].reshape(C, 24)
         Z, _ = orc.fr_stream(0x7E57D0, 1 << n)
 
-        def commit_rows(r0, r1):
-            return orc.g1_msm_batch(pg0, Z[r0:].reshape(-1), r1 - r0, 1, C)
+        def commit_rows_partial(r0, r1):
+            cm = orc.g1_msm_batch(pg0, Z[r0:].reshape(-1), r1 - r0, 1, C)
+            return cm, orc.miller_product(cm, hvec[r0:r1])
 
-        def ipp(comms):
-            return orc.multi_pairing(comms, hvec)
-
-        comms, T = sharded_commit(n, commit_rows, ipp, dist, torch.device("cpu"))
+        comms, T = sharded_commit(n, commit_rows_partial, orc.gt_final_exp_product, dist, torch.device("cpu"))
         if rank == 0:
             c2, T2 = orc.pst_commit(srs, Z, n)
             q.put((bool(np.array_equal(comms, c2)), bool(np.array_equal(T, T2))))

@@ -228,6 +228,32 @@ def test_commit_rows_and_ipp_match_full_commit(ctx):
         assert np.array_equal(S.ipp(ctx, n, comms), T)
 
 
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_commit_rows_partial_world_split(ctx, world):
+    """Row-sharded commit with the IPP split by rows: each
+    share's Miller-loop partial equals the C++ oracle's unreduced product of
+    the same pairs, and FE(prod of the shares) == T of the full commit."""
+    from testudo_amd import sqrt_pst as S
+    n = 11
+    nv = (n + 1) // 2
+    S.srs_setup(ctx, nv, 0x7E57D1)
+    flat = S.srs_export(ctx, nv)
+    C, Rn = 1 << (n // 2), 1 << nv
+    off = 36 + Rn * 12  # powers_of_h[0]; n odd -> powers_of_h[1]
+    off += Rn * 24 + (Rn // 2) * 12
+    hvec = flat[off:off + C * 24].reshape(C, 24)
+    Z, _ = S.fr_stream(0x7E57D0 + world, 1 << n)
+    pl = S.Polynomial.from_evaluations(ctx, Z)
+    comms, T = pl.commit()
+    R = C // world
+    shares = [pl.commit_rows_partial(r, r + R) for r in range(0, C, R)]
+    assert np.array_equal(np.concatenate([c for c, _ in shares]), comms)
+    ml = np.stack([m for _, m in shares])
+    assert np.array_equal(ml[0], orc.miller_product(comms[:R], hvec[:R]))
+    assert np.array_equal(S.gt_final_exp_product(ctx, ml), T)
+    assert np.array_equal(orc.gt_final_exp_product(ml), T)
+
+
 @pytest.mark.parametrize("g2", [False, True])
 def test_fixed_base_grouped_msm_vs_oracle(ctx, g2):
     """csrc/fbt.h lookup-table MSM: plain (one group), MIPP-fold groups

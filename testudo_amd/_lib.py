@@ -52,6 +52,8 @@ PROTOTYPES = [
     ("tpst_poly_commit_dev", C.c_int, [_vp, _vp, _vp, _vp]),
     ("tpst_poly_commit_rows", C.c_int, [_vp, _vp, _sz, _sz, _u64p]),
     ("tpst_poly_ipp", C.c_int, [_vp, C.c_int, _u64p, _u64p]),
+    ("tpst_poly_commit_rows_partial", C.c_int, [_vp, _vp, _sz, _sz, _u64p, _u64p]),
+    ("tpst_gt_final_exp_product", C.c_int, [_vp, _u64p, _sz, _u64p]),
     ("tpst_poly_open", C.c_int, [_vp, _vp, _vp, _u64p, _u64p, _u64p, _vp]),
     ("tpst_pst_verify", C.c_int, [_vp, _vp, C.c_int, _u64p, _u64p, _u64p, _vp]),
     ("tpst_profile_enable", C.c_int, [_vp, C.c_int]),

@@ -221,7 +221,7 @@ __device__ int fe_final_exp(const wave::Eng& e, const wave::lds_t* prog, int F, 
 }
 
 __global__ void __launch_bounds__(64 * FW) k_final_wave(const Fq12* __restrict__ partial, size_t T,
-                                                        Fq12* __restrict__ out) {
+                                                        Fq12* __restrict__ out, int do_final) {
   extern __shared__ uint4 smem4[];
   __shared__ int acc_slot[FW];
   wave::lds_t* prog = (wave::lds_t*)(smem4);
@@ -256,28 +256,104 @@ __global__ void __launch_bounds__(64 * FW) k_final_wave(const Fq12* __restrict__
     acc = tmp;
     tmp = t;
   }
+  if (!do_final) {  // Miller-loop product only (row-sharded IPP partial)
+    wave::store_f12(vals, acc, out + g);
+    return;
+  }
   const int fe = wave::N_CONSTS + FW * FW_SLOTS;
   const int r = fe_final_exp(e, prog, acc, fe, fe + 120);
   wave::store_f12(vals, r, out + g);
 }
 
+// ---- parallel tree product of Miller partials -----------------------------
+// One wave per output: out[g][j] = prod of partials [g][j*CH .. j*CH+CH) (the
+// tail chunk shorter).  Keeps k_final_wave's serial product short: without it
+// a 4096-pair IPP would be 1024 dependent Fq12 products per wave.
+constexpr int RW = 4;
+constexpr int RW_SLOTS = 64 + 36;
+constexpr int RW_OPS[] = {wave::OP_F12_MUL};
+constexpr wave::OpSet<1> RW_SET(RW_OPS);
+constexpr int RW_PROG = RW_SET.words;
+constexpr size_t RW_LDS = (size_t)(RW_PROG + (wave::N_CONSTS + RW * RW_SLOTS) * wave::SLOT) * 4;
+constexpr size_t RW_CHUNK = 8;
+static_assert(RW_LDS <= 65536, "tree-product kernel LDS");
+
+__global__ void __launch_bounds__(64 * RW) k_f12_chunk_prod(const Fq12* __restrict__ in, size_t groups, size_t n,
+                                                            size_t nout, Fq12* __restrict__ out) {
+  extern __shared__ uint4 smem4[];
+  wave::lds_t* prog = (wave::lds_t*)(smem4);
+  wave::lds_t* vals = prog + RW_PROG;
+  wave::load_set(prog, RW_SET);
+  wave::load_consts(vals, 0);
+  __syncthreads();
+  const int w = threadIdx.x >> 6;
+  const size_t o = (size_t)blockIdx.x * RW + w;
+  if (o >= groups * nout) return;
+  const size_t g = o / nout, j = o % nout;
+  const size_t k0 = j * RW_CHUNK, k1 = (k0 + RW_CHUNK < n) ? k0 + RW_CHUNK : n;
+  const int base = wave::N_CONSTS + w * RW_SLOTS;
+  const wave::Eng e{vals, base, 0};
+  int acc = base + 64, in_r = base + 76, tmp = base + 88;
+  wave::load_f12(vals, acc, in + g * n + k0);
+  for (size_t k = k0 + 1; k < k1; k++) {
+    wave::load_f12(vals, in_r, in + g * n + k);
+    wave::run(e, prog + RW_SET.off[0], acc, in_r, tmp);
+    const int t = acc;
+    acc = tmp;
+    tmp = t;
+  }
+  wave::store_f12(vals, acc, out + o);
+}
+
+// groups x n Miller partials -> groups x n' (n' <= 4 FW-wave shares) by
+// chunked tree products; returns the buffer holding them and sets n
+static hipError_t tree_partials(Arena& ar, hipStream_t s, Fq12*& partial, size_t groups, size_t& n) {
+  while (n > 2 * FW) {
+    const size_t nout = (n + RW_CHUNK - 1) / RW_CHUNK;
+    Fq12* nxt = ar.take<Fq12>(groups * nout);
+    k_f12_chunk_prod<<<grid_for(groups * nout, RW), 64 * RW, RW_LDS, s>>>(partial, groups, n, nout, nxt);
+    TPST_TRY(hipGetLastError());
+    partial = nxt;
+    n = nout;
+  }
+  return hipSuccess;
+}
+
+size_t multi_pairing_scratch(size_t groups, size_t n) {
+  size_t tot = Arena::need(groups * (n ? n : 1), sizeof(Fq12));
+  while (n > 2 * FW) {
+    n = (n + RW_CHUNK - 1) / RW_CHUNK;
+    tot += Arena::need(groups * n, sizeof(Fq12));
+  }
+  return tot + 1024;
+}
+
 hipError_t multi_pairing_prepared(Arena& ar, hipStream_t s, const uint32_t* d_g1, const uint32_t* d_g2,
-                                  const LineCoeff* d_coeffs, size_t groups, size_t n, Fq12* d_out) {
+                                  const LineCoeff* d_coeffs, size_t groups, size_t n, Fq12* d_out, bool final_exp) {
   if (!groups) return hipSuccess;
   const size_t np = groups * n;
   Fq12* partial = ar.take<Fq12>(np ? np : 1);
   if (np) {
     k_miller_wave<<<grid_for(np, MW), 64 * MW, MW_LDS, s>>>(d_g1, d_g2, d_coeffs, np, partial);
     TPST_TRY(hipGetLastError());
+    TPST_TRY(tree_partials(ar, s, partial, groups, n));
   }
-  k_final_wave<<<(unsigned)groups, 64 * FW, FW_LDS, s>>>(partial, n, d_out);
+  k_final_wave<<<(unsigned)groups, 64 * FW, FW_LDS, s>>>(partial, n, d_out, final_exp ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t gt_product_final(Arena& ar, hipStream_t s, const Fq12* d_partials, size_t groups, size_t n, Fq12* d_out) {
+  if (!groups) return hipSuccess;
+  Fq12* partial = const_cast<Fq12*>(d_partials);
+  if (n) TPST_TRY(tree_partials(ar, s, partial, groups, n));
+  k_final_wave<<<(unsigned)groups, 64 * FW, FW_LDS, s>>>(partial, n, d_out, 1);
   return hipGetLastError();
 }
 
 hipError_t multi_pairing(Arena& ar, hipStream_t s, const uint32_t* d_g1, const uint32_t* d_g2, size_t groups,
                          size_t n, Fq12* d_out) {
   const size_t np = groups * n;
-  size_t need = Arena::need(np * N_LINE_COEFFS, sizeof(LineCoeff)) + Arena::need(np ? np : groups, sizeof(Fq12)) + 4096;
+  size_t need = Arena::need(np * N_LINE_COEFFS, sizeof(LineCoeff)) + multi_pairing_scratch(groups, n) + 4096;
   ar.reset();
   TPST_TRY(ar.reserve(need));
   LineCoeff* coeffs = ar.take<LineCoeff>(np * N_LINE_COEFFS);

@@ -16,8 +16,17 @@ hipError_t g2_prepare_batch(hipStream_t s, const uint32_t* d_g2, size_t n, LineC
 // d_g1: groups*n affine G1 (Montgomery); d_coeffs: prepared G2 of the same
 // pairs, coefficient-major with row length groups*n; d_g2 only for the
 // infinity test.  Output Montgomery Fq12 per group.
+// final_exp = false: the Miller-loop product of each group only (unreduced GT
+// partial of a row-sharded IPP, finished by gt_product_final).  Scratch from
+// `ar`: multi_pairing_scratch(groups, n) bytes.
 hipError_t multi_pairing_prepared(Arena& ar, hipStream_t s, const uint32_t* d_g1, const uint32_t* d_g2,
-                                  const LineCoeff* d_coeffs, size_t groups, size_t n, Fq12* d_out);
+                                  const LineCoeff* d_coeffs, size_t groups, size_t n, Fq12* d_out,
+                                  bool final_exp = true);
+size_t multi_pairing_scratch(size_t groups, size_t n);
+
+// groups x n Montgomery Fq12 partials -> groups final-exponentiated products
+// (uses `ar` for the tree levels, <= multi_pairing_scratch(groups, n))
+hipError_t gt_product_final(Arena& ar, hipStream_t s, const Fq12* d_partials, size_t groups, size_t n, Fq12* d_out);
 
 // convenience: prepare + pair
 hipError_t multi_pairing(Arena& ar, hipStream_t s, const uint32_t* d_g1, const uint32_t* d_g2, size_t groups,

@@ -572,9 +572,8 @@ static int poly_commit_dev(tpst_ctx* ctx, tpst_poly* p, uint32_t* d_comms_mont, 
   TPST_HIP(ctx, msm_batch(ctx->arena, s, st->tables, p->d_Z, C, 1, C, rows));
   TPST_HIP(ctx, xyzz_to_affine_mont<Fq>(s, rows, d_comms_mont, C));
   const LineCoeff* hp = (const LineCoeff*)st->hprep[p->odd].p;
-  const size_t need = Arena::need(C, sizeof(Fq12)) + 4096;
   ctx->arena.reset();
-  TPST_HIP(ctx, ctx->arena.reserve(need));
+  TPST_HIP(ctx, ctx->arena.reserve(multi_pairing_scratch(1, C)));
   TPST_HIP(ctx, multi_pairing_prepared(ctx->arena, s, d_comms_mont, st->ph[p->odd]->u(), hp, 1, C, d_T));
   return TPST_OK;
 }
@@ -661,11 +660,80 @@ extern "C" int tpst_poly_ipp(tpst_ctx* ctx, int n, const uint64_t* comms, uint64
   TPST_HIP(ctx, hipMemcpyAsync(up.p, comms, C * 96, hipMemcpyHostToDevice, s));
   TPST_HIP(ctx, points_to_mont<Fq>(s, up.u(), cm.u(), C));
   ctx->arena.reset();
-  TPST_HIP(ctx, ctx->arena.reserve(Arena::need(C, sizeof(Fq12)) + 4096));
+  TPST_HIP(ctx, ctx->arena.reserve(multi_pairing_scratch(1, C)));
   TPST_HIP(ctx, multi_pairing_prepared(ctx->arena, s, cm.u(), st->ph[odd]->u(), (const LineCoeff*)st->hprep[odd].p, 1,
                                        C, (Fq12*)tt.p));
   TPST_HIP(ctx, fq12_from_mont(s, (Fq12*)tt.p, out.u(), 1));
   TPST_HIP(ctx, hipMemcpyAsync(T, out.p, 576, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipStreamSynchronize(s));
+  return TPST_OK;
+}
+
+// Row-sharded commit with the IPP split across ranks: the
+// MSMs of rows [r0, r1) AND the Miller-loop product of their pairs
+// prod_{r0 <= i < r1} ml(C_i, h_i) before final exponentiation (canonical
+// Fq12, 72 u64).  Rank 0 finishes T = FE(prod over ranks) with
+// tpst_gt_final_exp_product, so no rank runs more than its share of Miller loops.
+extern "C" int tpst_poly_commit_rows_partial(tpst_ctx* ctx, tpst_poly* p, size_t r0, size_t r1, uint64_t* comms,
+                                             uint64_t* miller) {
+  if (!ctx || !p || !comms || !miller || r1 < r0) return fail(ctx, TPST_E_ARG, "bad argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  SrsState* st = srs_of(ctx);
+  if (!st) return fail(ctx, TPST_E_STATE, "no SRS loaded");
+  if (st->nv != p->m_row) return fail(ctx, TPST_E_ARG, "SRS num_vars != ceil(n/2)");
+  const size_t C = (size_t)1 << p->m_col;
+  if (r1 > C) return fail(ctx, TPST_E_ARG, "row range out of bounds");
+  const size_t R = r1 - r0;
+  hipStream_t s = ctx->stream;
+  if (R == 0) {  // empty share: comms untouched, partial = 1
+    memset(miller, 0, 576);
+    miller[0] = 1;
+    return TPST_OK;
+  }
+  DevBuf rows, cm, out, hsub, tt;
+  TPST_HIP(ctx, rows.alloc(R * sizeof(Xyzz<Fq>)));
+  TPST_HIP(ctx, cm.alloc(R * 96));
+  TPST_HIP(ctx, out.alloc(R * 96 + 576));
+  TPST_HIP(ctx, tt.alloc(sizeof(Fq12)));
+  TPST_HIP(ctx, msm_batch(ctx->arena, s, st->tables, p->d_Z + 8 * r0, R, 1, C, (Xyzz<Fq>*)rows.p));
+  TPST_HIP(ctx, xyzz_to_affine_mont<Fq>(s, (Xyzz<Fq>*)rows.p, cm.u(), R));
+  // this rank's h_i and their prepared lines: the coefficient-major cache has
+  // row length C, so the R-pair slice is re-prepared (R G2 points, one launch)
+  const uint32_t* h = st->ph[p->odd]->u() + 48 * r0;
+  const size_t need = Arena::need(R * N_LINE_COEFFS, sizeof(LineCoeff)) + multi_pairing_scratch(1, R) + 4096;
+  ctx->arena.reset();
+  TPST_HIP(ctx, ctx->arena.reserve(need));
+  LineCoeff* lc = ctx->arena.take<LineCoeff>(R * N_LINE_COEFFS);
+  TPST_HIP(ctx, g2_prepare_batch(s, h, R, lc));
+  TPST_HIP(ctx, multi_pairing_prepared(ctx->arena, s, cm.u(), h, lc, 1, R, (Fq12*)tt.p, false));
+  TPST_HIP(ctx, affine_from_mont<Fq>(s, cm.u(), out.u(), R));
+  TPST_HIP(ctx, fq12_from_mont(s, (Fq12*)tt.p, out.u() + 24 * R, 1));
+  TPST_HIP(ctx, hipMemcpyAsync(comms, out.p, R * 96, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipMemcpyAsync(miller, out.u() + 24 * R, 576, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipStreamSynchronize(s));
+  return TPST_OK;
+}
+
+// T = FE(prod_k partials[k]) for k Miller-loop partials (canonical Fq12 each)
+extern "C" int tpst_gt_final_exp_product(tpst_ctx* ctx, const uint64_t* partials, size_t k, uint64_t* T) {
+  if (!ctx || (!partials && k) || !T) return fail(ctx, TPST_E_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  DevBuf up, out;
+  const size_t kk = k ? k : 1;
+  TPST_HIP(ctx, up.alloc(kk * sizeof(Fq12)));
+  TPST_HIP(ctx, out.alloc(sizeof(Fq12) + 576));
+  if (k) {
+    TPST_HIP(ctx, hipMemcpyAsync(up.p, partials, k * 576, hipMemcpyHostToDevice, s));
+    TPST_HIP(ctx, points_to_mont<Fq>(s, up.u(), up.u(), 6 * k));  // 12 Fq = 6 "points"
+  }
+  ctx->arena.reset();
+  TPST_HIP(ctx, ctx->arena.reserve(multi_pairing_scratch(1, k)));
+  TPST_HIP(ctx, gt_product_final(ctx->arena, s, (const Fq12*)up.p, 1, k, (Fq12*)out.p));
+  TPST_HIP(ctx, fq12_from_mont(s, (Fq12*)out.p, out.u() + sizeof(Fq12) / 4, 1));
+  TPST_HIP(ctx, hipMemcpyAsync(T, out.u() + sizeof(Fq12) / 4, 576, hipMemcpyDeviceToHost, s));
   TPST_HIP(ctx, hipStreamSynchronize(s));
   return TPST_OK;
 }

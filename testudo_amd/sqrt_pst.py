@@ -143,6 +143,15 @@ class Polynomial:
         self.ctx.check(self.ctx.lib.tpst_poly_commit_rows(self.ctx.h, self.h, r0, r1, ptr(out)), "commit_rows")
         return out
 
+    def commit_rows_partial(self, r0: int, r1: int):
+        """Rows [r0, r1) of sqrt_pst.rs:121-125 plus their share of the IPP
+        (sqrt_pst.rs:128-143) as an unreduced Miller-loop product (72,)."""
+        out = np.zeros((r1 - r0, 12), dtype=np.uint64)
+        ml = np.zeros(72, dtype=np.uint64)
+        self.ctx.check(self.ctx.lib.tpst_poly_commit_rows_partial(self.ctx.h, self.h, r0, r1, ptr(out), ptr(ml)),
+                       "commit_rows_partial")
+        return out, ml
+
     def commit_dev(self, d_comms: int, d_T: int):
         self.ctx.check(self.ctx.lib.tpst_poly_commit_dev(self.ctx.h, self.h, C.c_void_p(d_comms),
                                                          C.c_void_p(d_T)), "commit_dev")
@@ -185,6 +194,14 @@ def ipp(ctx: Context, n: int, comms) -> np.ndarray:
     """T = prod e(C_i, h_i) for a full (gathered) commitment list."""
     T = np.zeros(72, dtype=np.uint64)
     ctx.check(ctx.lib.tpst_poly_ipp(ctx.h, n, ptr(_u64(comms, (-1, 12))), ptr(T)), "ipp")
+    return T
+
+
+def gt_final_exp_product(ctx: Context, partials) -> np.ndarray:
+    """T = final_exponentiation(prod of the ranks' Miller-loop partials)."""
+    partials = _u64(partials, (-1, 72))
+    T = np.zeros(72, dtype=np.uint64)
+    ctx.check(ctx.lib.tpst_gt_final_exp_product(ctx.h, ptr(partials), len(partials), ptr(T)), "gt_final_exp_product")
     return T
 
 

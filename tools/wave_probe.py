@@ -3,7 +3,10 @@ and the lone-wave Fq multiply for reference."""
 import re
 import sys
 
-sys.path.insert(0, ".")
+import os
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.chdir(ROOT)
 from testudo_amd.engine import Context  # noqa: E402
 
 ops = re.findall(r"OP_(\w+)", open("testudo_amd/csrc/wave_ops.inc").read().split("enum OpId {")[1].split("}")[0])
