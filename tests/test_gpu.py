@@ -212,6 +212,25 @@ def test_commit_homomorphism_n20(ctx):
         assert np.array_equal(comms[i], ctx.g1_msm(pg0, row))
 
 
+def test_commit_homomorphism_n23_long_chunks(ctx):
+    """Batch commit at 2^23 (2048 rows x 4096): the accumulation runs 256-entry
+    chunks (buckets of ~44 entries straddle chunk and workgroup boundaries,
+    finished in-workgroup or by the workgroup fixup) and the bucket reduction
+    runs L = 16 segments; sampled rows == the K2 MSM of the same row."""
+    from testudo_amd import sqrt_pst as S
+    n = 23
+    S.srs_setup(ctx, 12, 0x7E57D1)
+    flat = S.srs_export(ctx, 12)
+    pg0 = flat[36:36 + 4096 * 12].reshape(4096, 12)
+    Z, _ = S.fr_stream(0x7E57D0 + 23, 1 << n)
+    pl = S.Polynomial.from_evaluations(ctx, Z)
+    comms, T = pl.commit()
+    C = 1 << (n // 2)
+    for i in (0, 1, 1000, C - 1):
+        assert np.array_equal(comms[i], ctx.g1_msm(pg0, Z[i::C])), i
+    del pl
+
+
 def test_commit_rows_and_ipp_match_full_commit(ctx):
     """The per-rank pieces of the sharded commit:
     row blocks concatenate to the full comm_list and ipp(comm_list) == T."""

@@ -1,4 +1,5 @@
 // Pippenger MSM kernels for gfx950 (see msm.h for the pipeline).
+#include <cstdlib>
 #include <hipcub/hipcub.hpp>
 #include "device_util.h"
 #include "msm.h"
@@ -27,8 +28,22 @@ static inline int bit_length(uint64_t v) {
 static inline int num_windows_bits(int c, int bits) { return (bits + c - 1) / c; }
 static inline int num_windows(int c) { return num_windows_bits(c, 254); }
 
-// entries per thread in the balanced bucket accumulation
-constexpr uint32_t ACC_CHUNK = 32;
+// entries per thread in the balanced bucket accumulation: 2^lg with lg the
+// largest in [5, 8] that still leaves >= TPST_ACC_WAVES (default 8) waves per
+// SIMD.  Long chunks matter for the batch commit, whose buckets (~44 entries
+// at 2^24) would otherwise nearly all straddle chunk boundaries.
+static int acc_chunk_lg(size_t m) {
+  static const size_t threads = [] {
+    const char* e = getenv("TPST_ACC_WAVES");
+    const int w = e ? atoi(e) : 0;
+    return (size_t)(w > 0 ? w : 8) * 64 * 1024;  // 1024 SIMDs (256 CUs x 4)
+  }();
+  int lg = 5;
+  while (lg < 8 && (m >> (lg + 1)) >= threads) lg++;
+  return lg;
+}
+constexpr int ACC_BLOCK_LG = 6;  // chunks (threads) per accumulation workgroup: one wave
+constexpr int ACC_BLOCK = 1 << ACC_BLOCK_LG;
 
 // c-bit window of an nw-word canonical scalar starting at bit `off`
 __device__ __forceinline__ uint32_t window_bits(const uint32_t* s, int nw, int off, int c) {
@@ -177,64 +192,93 @@ __device__ __forceinline__ Affine<F> fetch_point(const uint32_t* bases, const ui
   return p;
 }
 
-// Balanced bucket accumulation over the key-sorted entries: thread t owns
-// entries [t*CH, (t+1)*CH).  A bucket lying wholly inside the chunk is
-// written directly; the chunk's first / last segment of a bucket that crosses
-// the chunk boundary goes to part[2t] (bucket began earlier) / part[2t+1]
-// (bucket continues), summed by k_bucket_fixup.  The next point is loaded
-// before the current mixed add runs (software prefetch).
+// Balanced bucket accumulation over the key-sorted entries: thread t owns the
+// chunk of entries [t 2^lg, (t+1) 2^lg).  A bucket lying wholly inside the
+// chunk is stored directly.  A bucket crossing chunk boundaries is finished by
+// its owner (the chunk holding its first entry): the owner keeps its tail
+// piece in registers while every later chunk parks its leading piece in
+// part[t]; after the workgroup barrier the owner adds the pieces of the
+// following chunks of its workgroup (still in L2) and stores the bucket.  Only
+// the bucket crossing the workgroup's last chunk is left to k_bucket_fixup
+// (its owner's partial goes to bpart[workgroup]), so the fixup runs one thread
+// per workgroup instead of one per bucket.  The next point is loaded before
+// the current mixed add runs (software prefetch).
 template <class F>
-__global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
+__global__ void __launch_bounds__(ACC_BLOCK, (sizeof(F) > 48 ? 1 : 2))
     k_bucket_acc_chunk(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals, size_t m,
                        uint32_t sent, const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend,
                        const uint32_t* __restrict__ bases, const uint32_t* __restrict__ phib, uint32_t nbase,
-                       Xyzz<F>* __restrict__ buckets, Xyzz<F>* __restrict__ part) {
-  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t c0 = t * ACC_CHUNK;
-  if (c0 >= m) return;
-  const size_t c1 = (c0 + ACC_CHUNK < m) ? c0 + ACC_CHUNK : m;
-  uint32_t key = keys[c0];
-  Affine<F> pt;
-  if (key < sent) pt = fetch_point<F>(bases, phib, nbase, vals[c0]);
-  Xyzz<F> acc = Xyzz<F>::inf();
-  for (size_t e = c0; e < c1; e++) {
-    uint32_t key_n = sent;
-    Affine<F> pt_n;
-    if (e + 1 < c1) {
-      key_n = keys[e + 1];
-      if (key_n < sent) pt_n = fetch_point<F>(bases, phib, nbase, vals[e + 1]);
-    }
-    if (key < sent) {
-      acc = add_affine(acc, pt);
-      if (key_n != key) {
-        const bool starts = bstart[key] >= c0;
-        const bool ends = bend[key] <= c1;
-        if (starts && ends)
-          store_xyzz(buckets, key, acc);
-        else
-          store_xyzz(part, 2 * t + (starts ? 1 : 0), acc);
-        acc = Xyzz<F>::inf();
+                       int lg, Xyzz<F>* __restrict__ buckets, Xyzz<F>* __restrict__ part,
+                       Xyzz<F>* __restrict__ bpart) {
+  const size_t t = (size_t)blockIdx.x * ACC_BLOCK + threadIdx.x;
+  const size_t c0 = t << lg;
+  uint32_t tail_key = sent;
+  Xyzz<F> tail = Xyzz<F>::inf();
+  if (c0 < m) {
+    const size_t c1 = (c0 + ((size_t)1 << lg) < m) ? c0 + ((size_t)1 << lg) : m;
+    uint32_t key = keys[c0];
+    Affine<F> pt;
+    if (key < sent) pt = fetch_point<F>(bases, phib, nbase, vals[c0]);
+    Xyzz<F> acc = Xyzz<F>::inf();
+    for (size_t e = c0; e < c1; e++) {
+      uint32_t key_n = sent;
+      Affine<F> pt_n;
+      if (e + 1 < c1) {
+        key_n = keys[e + 1];
+        if (key_n < sent) pt_n = fetch_point<F>(bases, phib, nbase, vals[e + 1]);
       }
+      if (key < sent) {
+        acc = add_affine(acc, pt);
+        if (key_n != key) {
+          const bool starts = bstart[key] >= c0;
+          const bool ends = bend[key] <= c1;
+          if (starts && ends) {
+            store_xyzz(buckets, key, acc);
+          } else if (starts) {  // only the chunk's last segment can continue
+            tail = acc;
+            tail_key = key;
+          } else {  // only the chunk's first segment can have begun earlier
+            store_xyzz(part, t, acc);
+          }
+          acc = Xyzz<F>::inf();
+        }
+      }
+      key = key_n;
+      pt = pt_n;
     }
-    key = key_n;
-    pt = pt_n;
   }
+  __threadfence_block();
+  __syncthreads();
+  if (tail_key >= sent) return;
+  const size_t t1 = ((size_t)bend[tail_key] - 1) >> lg;  // chunk of the bucket's last entry
+  const size_t tb = (size_t)blockIdx.x * ACC_BLOCK + (ACC_BLOCK - 1);
+  const size_t stop = t1 < tb ? t1 : tb;
+  for (size_t u = t + 1; u <= stop; u++) tail = add(tail, load_xyzz(part, u));
+  if (t1 <= tb)
+    store_xyzz(buckets, tail_key, tail);
+  else
+    store_xyzz(bpart, blockIdx.x, tail);
 }
 
-// buckets that cross chunk boundaries: tail of the first chunk + heads of the rest
+// buckets crossing a workgroup boundary: thread B finishes the bucket holding
+// workgroup B's last entry when that bucket began in B -- its owner's partial
+// plus the leading pieces of the chunks after B up to the bucket's last one
 template <class F>
 __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
-    k_bucket_fixup(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend, size_t nbk,
-                   const Xyzz<F>* __restrict__ part, Xyzz<F>* __restrict__ buckets) {
-  const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nbk) return;
-  const uint32_t s = bstart[b], e = bend[b];
-  if (e <= s) return;
-  const size_t t0 = s / ACC_CHUNK, t1 = (e - 1) / ACC_CHUNK;
-  if (t0 == t1) return;
-  Xyzz<F> acc = load_xyzz(part, 2 * t0 + 1);
-  for (size_t t = t0 + 1; t <= t1; t++) acc = add(acc, load_xyzz(part, 2 * t));
-  store_xyzz(buckets, b, acc);
+    k_bucket_fixup(const uint32_t* __restrict__ keys, size_t m, uint32_t sent, const uint32_t* __restrict__ bstart,
+                   const uint32_t* __restrict__ bend, int lg, size_t nblk, const Xyzz<F>* __restrict__ part,
+                   const Xyzz<F>* __restrict__ bpart, Xyzz<F>* __restrict__ buckets) {
+  const size_t B = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (B + 1 >= nblk) return;
+  const int lb = lg + ACC_BLOCK_LG;
+  const size_t e = (B + 1) << lb;  // first entry of workgroup B + 1
+  if (e >= m) return;
+  const uint32_t key = keys[e];
+  if (key >= sent || keys[e - 1] != key || ((size_t)bstart[key] >> lb) != B) return;
+  const size_t t1 = ((size_t)bend[key] - 1) >> lg;
+  Xyzz<F> acc = load_xyzz(bpart, B);
+  for (size_t u = (B + 1) << ACC_BLOCK_LG; u <= t1; u++) acc = add(acc, load_xyzz(part, u));
+  store_xyzz(buckets, key, acc);
 }
 
 // segment t of group g: sum_{b in seg} (b+1) * S_b with b the bucket index
@@ -347,9 +391,20 @@ hipError_t xyzz_to_affine_canonical(hipStream_t s, const Xyzz<F>* d_in, uint32_t
 
 // reduce `groups` bucket sets of nb buckets each into one point per group:
 // short weighted segments (L = 4) then two tree passes
+// segment length of the weighted bucket reduction: short segments (L = 4)
+// when the groups are few (latency-bound: many short chains); longer ones when
+// there are enough segments to fill the chip anyway (throughput-bound: every
+// segment pays one scalar multiplication by its offset, so fewer, longer
+// segments do less work) -- the 4096-row commit at 2^24 runs L = 32
+static uint32_t reduce_seg_len(size_t groups, uint32_t nb) {
+  uint32_t L = 4;
+  while (L < 32 && 2 * L <= nb && groups * (nb / (2 * L)) >= ((size_t)1 << 18)) L *= 2;
+  return nb >= L ? L : nb;
+}
+
 template <class F>
 static size_t reduce_scratch(size_t groups, uint32_t nb) {
-  const uint32_t L = nb >= 4 ? 4 : nb;
+  const uint32_t L = reduce_seg_len(groups, nb);
   const size_t nseg = groups * (nb / L);
   return Arena::need(nseg, sizeof(Xyzz<F>)) + Arena::need(nseg / 64 + groups + 1, sizeof(Xyzz<F>));
 }
@@ -357,7 +412,7 @@ static size_t reduce_scratch(size_t groups, uint32_t nb) {
 template <class F>
 static hipError_t reduce_buckets(Arena& ar, hipStream_t s, const Xyzz<F>* d_buckets, size_t groups, uint32_t nb,
                                  Xyzz<F>* d_group_out) {
-  const uint32_t L = nb >= 4 ? 4 : nb;
+  const uint32_t L = reduce_seg_len(groups, nb);
   const uint32_t S = nb / L;
   const size_t nseg = groups * S;
   Xyzz<F>* seg = ar.take<Xyzz<F>>(nseg);
@@ -393,9 +448,12 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   size_t sort_bytes = 0;
   TPST_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                               (uint32_t*)nullptr, (uint32_t*)nullptr, (int)m, 0, end_bit, s));
-  const size_t nchunk = (m + ACC_CHUNK - 1) / ACC_CHUNK;
+  const int lg = acc_chunk_lg(m);
+  const size_t nchunk = (m + ((size_t)1 << lg) - 1) >> lg;
+  const size_t nblk = (nchunk + ACC_BLOCK - 1) / ACC_BLOCK;
   size_t need = Arena::need(m, 4) * 4 + Arena::need(nbk, 4) * 2 + Arena::need(nbk, sizeof(Xyzz<F>)) +
-                Arena::need(2 * nchunk, sizeof(Xyzz<F>)) + reduce_scratch<F>(W, nb) +
+                Arena::need(nchunk, sizeof(Xyzz<F>)) + Arena::need(nblk, sizeof(Xyzz<F>)) +
+                reduce_scratch<F>(W, nb) +
                 Arena::need(W, sizeof(Xyzz<F>)) + Arena::need(glv ? n * 24 : 1, 4) + Arena::need(sort_bytes, 1) +
                 8192;
   ar.reset();
@@ -407,7 +465,8 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   uint32_t* bstart = ar.take<uint32_t>(nbk);
   uint32_t* bend = ar.take<uint32_t>(nbk);
   Xyzz<F>* buckets = ar.take<Xyzz<F>>(nbk);
-  Xyzz<F>* part = ar.take<Xyzz<F>>(2 * nchunk);
+  Xyzz<F>* part = ar.take<Xyzz<F>>(nchunk);
+  Xyzz<F>* bpart = ar.take<Xyzz<F>>(nblk);
   Xyzz<F>* win = ar.take<Xyzz<F>>(W);
   uint32_t* phib = ar.take<uint32_t>(glv ? n * 24 : 1);
   void* tmp = ar.take<char>(sort_bytes);
@@ -434,10 +493,10 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   TPST_TRY(hipGetLastError());
   pf->end(ST_BOUNDS, s);
   pf->begin(ST_BUCKET_ACC, s);
-  k_bucket_acc_chunk<F><<<grid_for(nchunk, 64), 64, 0, s>>>(keys2, vals2, m, sent, bstart, bend, d_bases, phib,
-                                                            (uint32_t)n, buckets, part);
+  k_bucket_acc_chunk<F><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys2, vals2, m, sent, bstart, bend, d_bases, phib,
+                                                              (uint32_t)n, lg, buckets, part, bpart);
   TPST_TRY(hipGetLastError());
-  k_bucket_fixup<F><<<grid_for(nbk, 64), 64, 0, s>>>(bstart, bend, nbk, part, buckets);
+  k_bucket_fixup<F><<<grid_for(nblk, 64), 64, 0, s>>>(keys2, m, sent, bstart, bend, lg, nblk, part, bpart, buckets);
   TPST_TRY(hipGetLastError());
   pf->end(ST_BUCKET_ACC, s);
   pf->begin(ST_REDUCE, s);
@@ -649,32 +708,38 @@ hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint3
   const size_t m = rows * N * (size_t)W;
   if (m >= (1ull << 32)) return hipErrorInvalidValue;  // entry offsets are u32
   const size_t nbk = rows * nb;
-  const size_t nchunk = (m + ACC_CHUNK - 1) / ACC_CHUNK;
+  const int lg = acc_chunk_lg(m);
+  const size_t nchunk = (m + ((size_t)1 << lg) - 1) >> lg;
+  const size_t nblk = (nchunk + ACC_BLOCK - 1) / ACC_BLOCK;
   size_t need = 2 * Arena::need(m, 4) + 2 * Arena::need(nbk, 4) + Arena::need(nbk, sizeof(Xyzz<Fq>)) +
-                Arena::need(2 * nchunk, sizeof(Xyzz<Fq>)) + reduce_scratch<Fq>(rows, nb) + 4096;
+                Arena::need(nchunk, sizeof(Xyzz<Fq>)) + Arena::need(nblk, sizeof(Xyzz<Fq>)) +
+                reduce_scratch<Fq>(rows, nb) + 4096;
   ar.reset();
   TPST_TRY(ar.reserve(need));
   uint32_t* keys = ar.take<uint32_t>(m);
   uint32_t* entries = ar.take<uint32_t>(m);
-  Xyzz<Fq>* part = ar.take<Xyzz<Fq>>(2 * nchunk);
+  Xyzz<Fq>* part = ar.take<Xyzz<Fq>>(nchunk);
+  Xyzz<Fq>* bpart = ar.take<Xyzz<Fq>>(nblk);
   uint32_t* bstart = ar.take<uint32_t>(nbk);
   uint32_t* bend = ar.take<uint32_t>(nbk);
   Xyzz<Fq>* buckets = ar.take<Xyzz<Fq>>(nbk);
-  unsigned nblk = (unsigned)rows;
+  const unsigned nrow_blk = (unsigned)rows;
   Profiler* pf = ar.prof;
   Profiler dummy;
   if (!pf) pf = &dummy;
   pf->begin(ST_BATCH_SORT, s);
   TPST_TRY(hipMemsetAsync(buckets, 0, nbk * sizeof(Xyzz<Fq>), s));  // ZZ = 0 == infinity
-  k_batch_sort<<<nblk, 256, nb * sizeof(uint32_t), s>>>(d_scalars, rows, N, row_stride, col_stride, c, W, keys,
+  k_batch_sort<<<nrow_blk, 256, nb * sizeof(uint32_t), s>>>(d_scalars, rows, N, row_stride, col_stride, c, W, keys,
                                                         entries, bstart, bend);
   TPST_TRY(hipGetLastError());
   pf->end(ST_BATCH_SORT, s);
   pf->begin(ST_BUCKET_ACC, s);
-  k_bucket_acc_chunk<Fq><<<grid_for(nchunk, 64), 64, 0, s>>>(keys, entries, m, (uint32_t)nbk, bstart, bend,
-                                                             t.d_table, nullptr, 0x7fffffffu, buckets, part);
+  k_bucket_acc_chunk<Fq><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys, entries, m, (uint32_t)nbk, bstart, bend,
+                                                               t.d_table, nullptr, 0x7fffffffu, lg, buckets, part,
+                                                               bpart);
   TPST_TRY(hipGetLastError());
-  k_bucket_fixup<Fq><<<grid_for(nbk, 64), 64, 0, s>>>(bstart, bend, nbk, part, buckets);
+  k_bucket_fixup<Fq><<<grid_for(nblk, 64), 64, 0, s>>>(keys, m, (uint32_t)nbk, bstart, bend, lg, nblk, part, bpart,
+                                                       buckets);
   TPST_TRY(hipGetLastError());
   pf->end(ST_BUCKET_ACC, s);
   pf->begin(ST_REDUCE, s);
