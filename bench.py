@@ -1,30 +1,42 @@
 """Benchmark: BLS12-377 G1 MSM throughput on MI355X (BASELINE.json configs[1]),
-plus the sqrt-PST commit+open seconds at 2^20 variables (configs[2]) on N=1.
+plus the sqrt-PST commit+open seconds at 2^20 (configs[2]) and 2^24
+(configs[3]) variables, with the C++ CPU restatement timed beside them.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
 A step = one variable-base G1 MSM over 2^20 points (canonical Fr scalars,
 Montgomery affine bases, both resident in HBM before the timed region) -- the
-`msm_unchecked` of sqrt_pst.rs:198 / mipp.rs:393 at BASELINE's size.  With
-N > 1 (launched by torch.distributed.run, one process per GPU) every rank
-runs its own independent MSMs (weak scaling, no data-path collective); the
-timed region is bracketed by barrier + synchronize and the max over ranks is
-taken.  Rank 0 prints ONE JSON line.
+`msm_unchecked` of sqrt_pst.rs:198 / mipp.rs:393 at BASELINE's size.
 
-roofline: the dominant kernel is bucket accumulation (k_bucket_acc); its
-duration is measured with HIP events on the library's own stream over the
-timed region (tpst_profile_*).  Algorithmic bytes per MSM = 128 B per
-scalar-point pair (32 B Fr + 96 B affine G1).  The kernel is
-integer-VALU bound, so the HBM fraction is small by construction; the
-`compute` object reports Fq-multiplies/s against the measured
-microbenchmark peak.  cpu_baseline: the C++ oracle (arkworks-shaped
-Pippenger, oracle/cpu) timed on the host on the same 2^20 workload.
+N > 1: one process per GPU.  Run directly (`--gpus N` without WORLD_SIZE in
+the environment) this script starts `torch.distributed.run` with N ranks as a
+child process before it touches the GPU and relays its exit code; launched
+by torch.distributed.run it reads RANK / LOCAL_RANK / WORLD_SIZE.  Every rank
+runs its own MSMs (weak scaling, no data-path collective); the timed region
+is bracketed by barrier + synchronize, the max over ranks is taken, and rank 0
+prints ONE JSON line.  The 2^24 leg shards the commit's rows over the ranks:
+each rank uploads only its column block of Z (one 2D copy), commits its rows
+and the Miller loops of their IPP pairs, one RCCL all-gather moves [row
+commitments | Miller partial], rank 0 runs the final exponentiation and the
+(transcript-sequential) open.
+
+roofline: the dominant kernel is bucket accumulation (k_bucket_acc_chunk +
+its fixup); its duration is measured with HIP events on the library's own
+stream over the timed region (tpst_profile_*).  Algorithmic bytes per MSM =
+128 B per scalar-point pair (32 B Fr + 96 B affine G1).  The
+kernel is integer-VALU bound ("bound": "valu-int32"), so the HBM fraction is
+small by construction; `traffic` is the rocprofv3 PMC HBM bytes per launch of
+the same kernel (profiles/, FETCH_SIZE x2 + WRITE_SIZE per the gfx950
+correction), `compute` the VALU issue rate from SQ_INSTS_VALU and the Fq-mul
+rate against the measured microbenchmark peak.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -36,8 +48,10 @@ sys.path.insert(0, ROOT)
 METRIC = "PST commit+open sec, 2^20-var poly BLS12-377; G1 MSM Mscalar/s at 1/2/4/8 GPU"
 LOG_N = 20
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
+VALU_PEAK_WAVE_INSTS = 256 * 4 * 0.5 * 2.4e9  # CUs x SIMDs x (1 wave-instr / 2 cycles) x 2.4 GHz
 BYTES_PER_PAIR = 128           # 32 B scalar + 96 B affine base
 SEED = 0x7E57D0
+PMC_FILE = os.path.join(ROOT, "profiles", "r02", "pmc_bucket_acc_chunk.json")
 
 
 def parse():
@@ -49,17 +63,96 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--no-pst", action="store_true", help="skip the sqrt-PST commit+open leg")
     ap.add_argument("--pst-log-n", type=int, default=20)
-    ap.add_argument("--no-sharded", action="store_true", help="skip the row-sharded 2^24 commit leg")
+    ap.add_argument("--no-sharded", action="store_true", help="skip the 2^24 (row-sharded) commit+open leg")
     ap.add_argument("--sharded-log-n", type=int, default=24)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: exercise the launcher / rendezvous / timing plumbing only (gloo)")
     return ap.parse_args()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch(args):
+    """--gpus N from a plain invocation: start N ranks under torch.distributed.run
+    as a CHILD process (nothing here has touched the GPU) and return its code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr", "127.0.0.1", "--master-port=%d" % _free_port(), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", str(max(1, _cpu_threads() // args.gpus)))
+    return subprocess.run(cmd, env=env).returncode
+
+
+def _cpu_threads():
+    """Cores this job may use: the affinity mask, capped by OMP_NUM_THREADS when
+    the environment sets it (the GPU box gives each GPU job a 16-core share)."""
+    n = os.cpu_count() or 1
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return n
 
 
 def fq_mults_per_madd():
     return 12  # 8M + 2S + the modular adds ~ 2 mult-equivalents
 
 
+def _max_over_ranks(dist, dev, x):
+    import torch
+    if dist is None:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def dry_run(args):
+    """CPU rehearsal of the multi-rank plumbing (tests/test_distributed.py):
+    gloo rendezvous, barrier-bracketed timing, max over ranks, one JSON line."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    else:
+        dist = None
+    for _ in range(args.warmup):
+        time.sleep(0.001)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.001 * (1 + rank))  # ranks finish at different times: the max must win
+    if dist:
+        dist.barrier()
+    el = _max_over_ranks(dist, "cpu", time.perf_counter() - t0)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": 0.0, "unit": "Mscalar/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": round(el / max(args.steps, 1) * 1e3, 4),
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dry_run": True,
+                          "config": {"workload": "dry run (no GPU)"}}), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch(args)
+    if args.dry_run:
+        return dry_run(args)
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -108,26 +201,20 @@ def main():
     t1 = time.perf_counter()
     ctx.profile(False)
     stages = ctx.profile_read()
-    elapsed = t1 - t0
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = _max_over_ranks(dist, dev, t1 - t0)
 
     # correctness spot check of this rank's result against the size-independent
     # property MSM(b_i G) = (sum s_i b_i) G, verified with the library's
     # generator multiplication (a different code path from the MSM)
     out = d_out.cpu().numpy().view(np.uint64)
-    from testudo_amd.encoding import limbs_to_int, fr_array
+    from testudo_amd.encoding import fr_array
     R = 0x12AB655E9A2CA55660B44D1E5C37B00159AA76FED00000010A11800000000001
     s_int = sc.astype(object)
     b_int = bk.astype(object)
     sv = s_int[:, 0] + (s_int[:, 1] << 64) + (s_int[:, 2] << 128) + (s_int[:, 3] << 192)
     bv = b_int[:, 0] + (b_int[:, 1] << 64) + (b_int[:, 2] << 128) + (b_int[:, 3] << 192)
     tot = int(np.dot(sv, bv) % R)
-    expect = ctx.g1_mul_generator(fr_array([tot]))[0]
-    parity_ok = bool(np.array_equal(out, expect))
-    del limbs_to_int
+    parity_ok = bool(np.array_equal(out, ctx.g1_mul_generator(fr_array([tot]))[0]))
 
     sharded = None
     if dist is not None and not args.no_sharded:  # every rank takes part
@@ -139,7 +226,7 @@ def main():
         if dist:
             dist.barrier()
             dist.destroy_process_group()
-        return
+        return 0
 
     ms_step = elapsed / args.steps * 1e3
     value = world * n * args.steps / elapsed / 1e6  # Mscalar/s, whole job
@@ -147,23 +234,31 @@ def main():
     acc_avg_ms = acc_ms / max(acc_cnt, 1)
     alg_bytes = n * BYTES_PER_PAIR + 96
     achieved = alg_bytes / (acc_avg_ms * 1e-3) / 1e9
-    # traffic: HBM bytes per launch from the committed rocprofv3 PMC summary
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_bucket_acc.json")
-    if os.path.exists(pmc_path):
+    pmc = None
+    if os.path.exists(PMC_FILE):
         try:
-            traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+            pmc = json.load(open(PMC_FILE))
+        except ValueError:
+            pmc = None
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     # compute roof: measured Fq-mult peak vs achieved in the dominant kernel
     mb_threads = 256 * 16 * 64
     mb_iters = 200
     ctx.microbench(0, mb_threads, 10)  # warm: first launch loads the code object
     peak_fqmul = mb_threads * mb_iters / (min(ctx.microbench(0, mb_threads, mb_iters) for _ in range(3)) * 1e-3)
     c_bits = 16
-    windows = (254 + c_bits - 1) // c_bits
-    madds = n * windows
+    windows = 8  # GLV: two 127-bit halves, 8 signed 16-bit windows each
+    madds = 2 * n * windows
     achieved_fqmul = madds * fq_mults_per_madd() / (acc_avg_ms * 1e-3)
+    compute = {"bound": "valu-int32", "kernel": "k_bucket_acc_chunk<Fq>",
+               "achieved_fq_mul_per_s": achieved_fqmul, "peak_fq_mul_per_s_measured": peak_fqmul,
+               "frac": round(achieved_fqmul / peak_fqmul, 4),
+               "fq_mul_per_madd": fq_mults_per_madd()}
+    if pmc and pmc.get("valu_insts_per_launch"):
+        rate = pmc["valu_insts_per_launch"] / (acc_avg_ms * 1e-3)
+        compute.update({"valu_wave_insts_per_launch": pmc["valu_insts_per_launch"],
+                        "valu_issue_per_s": rate, "valu_issue_peak_per_s": VALU_PEAK_WAVE_INSTS,
+                        "valu_issue_frac": round(rate / VALU_PEAK_WAVE_INSTS, 4)})
 
     result = {
         "metric": METRIC,
@@ -184,16 +279,16 @@ def main():
                    "parallelism": "independent MSM per rank" if world > 1 else "1 GPU"},
         "parity_ok": parity_ok,
         "stages_ms_per_step": {k: round(v[0] / max(v[1], 1), 4) for k, v in stages.items() if v[1]},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "roofline": {"bound": "valu-int32", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-                     "kernel": "k_bucket_acc<Fq>", "alg_bytes_per_launch": alg_bytes,
-                     "kernel_avg_ms": round(acc_avg_ms, 4)},
-        **({"pst_2p24": sharded} if sharded is not None else {}),
-        "compute": {"bound": "valu-int32", "kernel": "k_bucket_acc<Fq>",
-                    "achieved_fq_mul_per_s": achieved_fqmul, "peak_fq_mul_per_s_measured": peak_fqmul,
-                    "frac": round(achieved_fqmul / peak_fqmul, 4)},
+                     "traffic_source": (os.path.relpath(PMC_FILE, ROOT) if pmc else None),
+                     "kernel": "k_bucket_acc_chunk<Fq> (+ k_bucket_fixup)", "alg_bytes_per_launch": alg_bytes,
+                     "kernel_avg_ms": round(acc_avg_ms, 4),
+                     "note": "HBM column secondary: the kernel is bound by 32-bit integer VALU issue"},
+        "compute": compute,
     }
-
+    if sharded is not None:
+        result["pst_2p24"] = sharded
     if not args.no_pst and world == 1:
         result["pst"] = pst_leg(ctx, args.pst_log_n)
     if dist is None and not args.no_sharded:
@@ -202,16 +297,19 @@ def main():
         except Exception as e:  # never lose the bench line to the secondary leg
             result["pst_2p24"] = {"error": repr(e)}
     if not args.no_cpu and world == 1:
-        result["cpu_baseline"] = cpu_leg(ctx, bk, sc, out)
+        result["cpu_baseline"] = cpu_leg(ctx, bk, sc, out, result)
     print(json.dumps(result), flush=True)
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 def pst_leg(ctx, log_n, reps=5):
     """sqrt-PST commit + open at 2^log_n variables (BASELINE configs[2]),
-    timed like benches/pst.rs:52-62: eval (get_q) before the open timer."""
+    timed like benches/pst.rs:52-62 (eval / get_q before the open timer).
+    Also reported: the H2D upload of Z (from_evaluations, BASELINE.md's
+    GPU-time definition includes it) and commit+open including it."""
     from testudo_amd import sqrt_pst as S
     nv = (log_n + 1) // 2
     t = time.perf_counter()
@@ -219,21 +317,23 @@ def pst_leg(ctx, log_n, reps=5):
     setup_s = time.perf_counter() - t
     Z, k = S.fr_stream(SEED, 1 << log_n)
     pt, _ = S.fr_stream(SEED, log_n, k)
-    pl = S.Polynomial.from_evaluations(ctx, Z)
-    v = pl.eval(pt)
-    ctx.synchronize()
     # the first commit+open of the process (cold: code objects load, scratch
     # arenas grow) is reported separately; then the median of `reps` warm runs
     runs = []
     for _ in range(reps + 1):
+        ctx.synchronize()
+        t = time.perf_counter()
+        pl = S.Polynomial.from_evaluations(ctx, Z)
+        h2d_s = time.perf_counter() - t
         t = time.perf_counter()
         comms, T = pl.commit()
         commit_s = time.perf_counter() - t
+        v = pl.eval(pt)
         tr = S.PoseidonTranscript()
         t = time.perf_counter()
         U, pst_proof, mipp = pl.open(tr, comms, pt, T)
         open_s = time.perf_counter() - t
-        runs.append((commit_s, open_s))
+        runs.append((commit_s, open_s, h2d_s))
     cold = runs[0]
     warm = sorted(runs[1:], key=lambda r: r[0] + r[1])[len(runs[1:]) // 2]
     t = time.perf_counter()
@@ -241,30 +341,43 @@ def pst_leg(ctx, log_n, reps=5):
     verify_s = time.perf_counter() - t
     return {"log_n": log_n, "commit_s": round(warm[0], 4), "open_s": round(warm[1], 4),
             "commit_plus_open_s": round(warm[0] + warm[1], 4), "reps": reps,
+            "h2d_s": round(warm[2], 4), "commit_open_incl_h2d_s": round(warm[0] + warm[1] + warm[2], 4),
             "first_call": {"commit_s": round(cold[0], 4), "open_s": round(cold[1], 4)},
             "verify_s": round(verify_s, 4), "srs_setup_s": round(setup_s, 3), "verified": ok,
-            "note": "host-pointer API: Z resident in HBM after from_evaluations; eval (get_q) before "
-                    "the open timer as in benches/pst.rs:50-62; SRS tables built in srs_setup"}
+            "note": "Z resident in HBM for commit_s/open_s (benches/pst.rs:48-62: the polynomial is built before "
+                    "the timers); h2d_s = from_evaluations from pageable host memory; eval before the open timer; "
+                    "SRS tables built in srs_setup"}
 
 
 def sharded_leg(ctx, log_n, dist, dev):
     """sqrt-PST commit + open at 2^log_n variables (BASELINE configs[3]).
-    N > 1: the row MSMs AND the IPP's Miller loops are sharded by rows over
-    the ranks (one RCCL all-gather of [row commitments | Miller partial],
-    one final exponentiation on rank 0); the open (transcript-sequential
-    MIPP + PST open) runs on rank 0.  N = 1: the plain
-    single-GPU commit + open."""
-    import torch
+    N > 1: every rank uploads only its column block of Z and commits its rows
+    AND their share of the IPP's Miller loops (one RCCL all-gather of [row
+    commitments | Miller partial], one final exponentiation on rank 0); the
+    open (transcript-sequential MIPP + PST open) runs on rank
+    0, which also holds the whole Z for it.  N = 1: the plain commit + open."""
     from testudo_amd import sqrt_pst as S
-    from testudo_amd.distributed import sharded_commit
+    from testudo_amd.distributed import shard_rows, sharded_commit
     nv = (log_n + 1) // 2
     t = time.perf_counter()
     S.srs_setup(ctx, nv, SEED + 1)
     setup_s = time.perf_counter() - t
     Z, k = S.fr_stream(SEED, 1 << log_n)
     pt, _ = S.fr_stream(SEED, log_n, k)
-    pl = S.Polynomial.from_evaluations(ctx, Z)
     rank = dist.get_rank() if dist else 0
+    world = dist.get_world_size() if dist else 1
+    r0, r1 = shard_rows(1 << (log_n // 2), world, rank)
+    t = time.perf_counter()
+    pl = S.Polynomial.from_evaluations(ctx, Z)
+    h2d_full_s = time.perf_counter() - t
+    shard = pl
+    h2d_s = h2d_full_s
+    if dist and rank != 0:  # the rank-local column block only
+        del pl
+        t = time.perf_counter()
+        shard = S.Polynomial.from_evaluations_cols(ctx, Z, r0, r1)
+        h2d_s = time.perf_counter() - t
+        pl = None
     if rank == 0:
         v = pl.eval(pt)
     reps = 2
@@ -275,19 +388,14 @@ def sharded_leg(ctx, log_n, dist, dev):
         ctx.synchronize()
         t = time.perf_counter()
         if dist:
-            comms, T = sharded_commit(log_n, pl.commit_rows_partial, lambda m: S.gt_final_exp_product(ctx, m),
+            comms, T = sharded_commit(log_n, shard.commit_rows_partial, lambda m: S.gt_final_exp_product(ctx, m),
                                       dist, dev)
         else:
             comms, T = pl.commit()
         ctx.synchronize()
         if dist:
             dist.barrier()
-        el = time.perf_counter() - t
-        if dist:
-            tt = torch.tensor([el], dtype=torch.float64, device=dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            el = float(tt.item())
-        commits.append(el)
+        commits.append(_max_over_ranks(dist, dev, time.perf_counter() - t))
         if rank == 0:
             t = time.perf_counter()
             U, pst_proof, mipp = pl.open(S.PoseidonTranscript(), comms, pt, T)
@@ -297,36 +405,77 @@ def sharded_leg(ctx, log_n, dist, dev):
     if rank != 0:
         return None
     ok = S.verify(ctx, S.PoseidonTranscript(), U, pt, v, pst_proof, mipp, T)
-    world = dist.get_world_size() if dist else 1
     c, o = min(commits[1:]), min(opens[1:])
     return {"log_n": log_n, "commit_s": round(c, 4), "open_s": round(o, 4), "commit_plus_open_s": round(c + o, 4),
             "first_call": {"commit_s": round(commits[0], 4), "open_s": round(opens[0], 4)},
-            "ranks": world, "rows_per_rank": (1 << (log_n // 2)) // world, "verified": ok,
+            "ranks": world, "rows_per_rank": r1 - r0, "verified": ok,
+            "h2d_s_rank0_full": round(h2d_full_s, 4), "h2d_s_rank0_shard": round(h2d_s, 4),
             "srs_setup_s": round(setup_s, 3),
-            "exchange": ("RCCL all_gather of [96-B row commitments | 576-B Miller partial] per rank, "
-                         "final exponentiation + open on rank 0") if dist else "none"}
+            "exchange": ("per-rank column-block upload; RCCL all_gather of [96-B row commitments | 576-B Miller "
+                         "partial] per rank; final exponentiation + open on rank 0") if dist else "none"}
 
 
-def cpu_leg(ctx, bk, sc, gpu_out):
-    """C++ CPU oracle (arkworks-shaped msm_bigint_wnaf, windows in parallel)
-    on the same 2^20 MSM, on this host's cores."""
+def cpu_leg(ctx, bk, sc, gpu_out, result):
+    """C++ CPU restatement (oracle/cpu: arkworks-shaped msm_bigint_wnaf,
+    OpenMP) on this host's cores: the 2^20 MSM in full, the 2^20 sqrt-PST
+    commit + open in full, and a bounded row sample of the 2^24 commit."""
     sys.path.insert(0, os.path.join(ROOT, "oracle", "cpu"))
     import orc
-    threads = min(16, os.cpu_count() or 1)
+    from testudo_amd import sqrt_pst as S
+    threads = _cpu_threads()
     lib = orc.load()
     lib.orc_set_threads(threads)
     n = len(sc)
     bases = ctx.g1_mul_generator(bk)  # canonical affine, same points as the GPU run
-    reps = 2
     t = time.perf_counter()
-    for _ in range(reps):
-        out = orc.g1_msm(bases, sc, parallel=True)
-    dt = (time.perf_counter() - t) / reps
-    return {"value": round(n / dt / 1e6, 4), "unit": "Mscalar/s", "cores": threads, "kind": "port",
-            "sample": "full 2^%d-point G1 MSM x%d reps (C++ restatement of ark-ec msm_bigint_wnaf, "
-                      "OpenMP over windows), %.2f s per MSM" % (int(np.log2(n)), reps, dt),
-            "matches_gpu": bool(np.array_equal(out, gpu_out))}
+    out = orc.g1_msm(bases, sc, parallel=True)
+    dt = time.perf_counter() - t
+    res = {"value": round(n / dt / 1e6, 4), "unit": "Mscalar/s", "cores": threads, "kind": "port",
+           "sample": "full 2^%d-point G1 MSM (C++ restatement of ark-ec msm_bigint_wnaf, OpenMP over windows), "
+                     "%.2f s" % (int(np.log2(n)), dt),
+           "matches_gpu": bool(np.array_equal(out, gpu_out))}
+    # sqrt-PST 2^20 commit + open, same inputs as the GPU leg
+    try:
+        lg = 20
+        srs = orc.SRS((lg + 1) // 2, SEED + 1)
+        Z, k = orc.fr_stream(SEED, 1 << lg)
+        pt, _ = orc.fr_stream(SEED, lg, k)
+        t = time.perf_counter()
+        comms, T = orc.pst_commit(srs, Z, lg)
+        c_s = time.perf_counter() - t
+        t = time.perf_counter()
+        orc.pst_open(srs, Z, lg, pt, comms)
+        o_s = time.perf_counter() - t
+        gpu = result.get("pst", {})
+        res["pst"] = {"log_n": lg, "commit_s": round(c_s, 3), "open_s": round(o_s, 3),
+                      "commit_plus_open_s": round(c_s + o_s, 3), "cores": threads,
+                      "gpu_speedup": (round((c_s + o_s) / gpu["commit_plus_open_s"], 1)
+                                      if gpu.get("commit_plus_open_s") else None),
+                      "sample": "full 2^20 commit + open (open includes get_q, as orc.pst_open computes it)"}
+        del Z
+        # 2^24: 256 of the 4096 row MSMs + their Miller loops, scaled by 16
+        lg = 24
+        nv = (lg + 1) // 2
+        srs = orc.SRS(nv, SEED + 1)
+        flat = srs.export()
+        Nr = 1 << nv
+        C = 1 << (lg // 2)
+        pg0 = flat[36:36 + Nr * 12].reshape(Nr, 12)
+        hv = flat[36 + Nr * 12:36 + Nr * 36].reshape(Nr, 24)[:C]
+        rows = 256
+        Zs, _ = orc.fr_stream(SEED + 24, rows * Nr)  # a sample block of the same shape (row-major)
+        t = time.perf_counter()
+        cm = orc.g1_msm_batch(pg0, Zs, rows, Nr, 1)
+        orc.miller_product(cm, hv[:rows])
+        s_s = time.perf_counter() - t
+        res["pst_2p24_commit"] = {"log_n": lg, "rows_sampled": rows, "rows_total": C,
+                                  "commit_s_extrapolated": round(s_s * C / rows, 2), "sample_s": round(s_s, 2),
+                                  "cores": threads,
+                                  "sample": "256 of 4096 row MSMs (4096 points each) + their Miller loops, x16"}
+    except Exception as e:  # the headline CPU line must survive
+        res["pst_error"] = repr(e)
+    return res
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -66,6 +66,39 @@ int tpst_g2_msm(tpst_ctx* ctx, const uint64_t* bases, size_t n_bases, const uint
  * canonical Fr (8 u32 each), d_out one canonical affine G1 */
 int tpst_g1_msm_dev(tpst_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, void* d_out);
 
+/* Length-checked form: mipp.rs:385-394 `multiexponentiation` returns
+ * Err(InvalidIPVectorLength) when the lengths differ -> TPST_E_ARG here. */
+int tpst_g1_multiexp(tpst_ctx* ctx, const uint64_t* bases, size_t n_bases, const uint64_t* scalars,
+                     size_t n_scalars, uint64_t* out);
+int tpst_g2_multiexp(tpst_ctx* ctx, const uint64_t* bases, size_t n_bases, const uint64_t* scalars,
+                     size_t n_scalars, uint64_t* out);
+
+/* ---- shared-base batch MSM and Pedersen/Hyrax commitments -----------------
+ * A generator set = MultiCommitGens {n, G[n], h} (commitments.rs:9-15),
+ * uploaded once (K1 window tables built here).  h may be NULL when only the
+ * batch MSM is used. */
+typedef struct tpst_gens tpst_gens;
+int tpst_gens_load(tpst_ctx* ctx, const uint64_t* G, size_t n, const uint64_t* h, tpst_gens** out);
+void tpst_gens_free(tpst_gens* gens);
+/* out[r] = sum_{j < cols} scalars[r*row_stride + j*col_stride] * G[j] for
+ * r < rows (canonical affine G1 each); cols must equal gens->n.  The strides
+ * let one call consume a row split of Z without a host transpose: this is
+ * the whole par_iter row loop of sqrt_pst.rs:121-125 / dense_mlpoly.rs:323-327
+ * in one launch. */
+int tpst_g1_msm_batch(tpst_ctx* ctx, const tpst_gens* gens, const uint64_t* scalars, size_t rows, size_t cols,
+                      size_t row_stride, size_t col_stride, uint64_t* out);
+int tpst_g1_msm_batch_dev(tpst_ctx* ctx, const tpst_gens* gens, const void* d_scalars, size_t rows, size_t cols,
+                          size_t row_stride, size_t col_stride, void* d_out);
+/* PedersenCommit::commit_slice (commitments.rs:79-86): msm(G, scalars) + h * blind;
+ * n must equal gens->n (the reference assert_eq!s, here TPST_E_ARG). */
+int tpst_pedersen_commit_slice(tpst_ctx* ctx, const tpst_gens* gens, const uint64_t* scalars, size_t n,
+                               const uint64_t* blind, uint64_t* out);
+/* DensePolynomial::commit_inner (dense_mlpoly.rs:314-329): n_rows = |blinds|
+ * rows of R = n_z / n_rows contiguous evaluations, row i -> commit_slice(Z[R i ..
+ * R (i+1)], blinds[i]); out = n_rows canonical affine G1. */
+int tpst_pedersen_commit_rows(tpst_ctx* ctx, const tpst_gens* gens, const uint64_t* Z, size_t n_z,
+                              const uint64_t* blinds, size_t n_rows, uint64_t* out);
+
 /* ---- fixed-base grouped MSM (csrc/fbt.h) --------------------------------
  * Builds the 64-window x 8-multiple lookup table of the n bases, then
  * out[g] = sum over k in group g of scalars[k] * bases[k] for L/D groups,
@@ -131,6 +164,12 @@ uint64_t tpst_fr_stream(uint64_t seed, size_t n, uint64_t start, uint64_t* out);
  * The row split is a strided view of Z on the device (no host transpose). */
 int tpst_poly_from_evaluations(tpst_ctx* ctx, const uint64_t* Z, int n, tpst_poly** out);
 int tpst_poly_from_evaluations_dev(tpst_ctx* ctx, const void* d_Z, int n, tpst_poly** out);
+/* Rank-local shard: upload only the columns [c0, c1) of the
+ * strided view (for every j: Z[j 2^m_col + c0 .. j 2^m_col + c1), one 2D copy).
+ * Such a handle serves tpst_poly_commit_rows[_partial] for rows inside
+ * [c0, c1); eval / commit / open need the whole polynomial (TPST_E_STATE). */
+int tpst_poly_from_evaluations_cols(tpst_ctx* ctx, const uint64_t* Z, int n, size_t c0, size_t c1,
+                                    tpst_poly** out);
 void tpst_poly_free(tpst_poly* p);
 /* Polynomial::eval (sqrt_pst.rs:105-115); computes and caches q, chi(b) */
 int tpst_poly_eval(tpst_ctx* ctx, tpst_poly* p, const uint64_t* point, uint64_t* out_v);
@@ -149,12 +188,34 @@ int tpst_poly_ipp(tpst_ctx* ctx, int n, const uint64_t* comms, uint64_t* T);
 int tpst_poly_commit_rows_partial(tpst_ctx* ctx, tpst_poly* p, size_t r0, size_t r1, uint64_t* comms,
                                   uint64_t* miller);
 int tpst_gt_final_exp_product(tpst_ctx* ctx, const uint64_t* partials, size_t k, uint64_t* T);
-/* Polynomial::open (sqrt_pst.rs:168-230); the transcript is updated in place */
+/* Polynomial::open (sqrt_pst.rs:168-230); the transcript is updated in place.
+ * U = MSM(comms, chi(b)) over the caller's comm_list (sqrt_pst.rs:198). */
 int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, const uint64_t* comms,
                    const uint64_t* point, const uint64_t* T, tpst_open_proof* proof);
-/* Polynomial::verify (sqrt_pst.rs:232-264): TPST_OK if valid, TPST_E_VERIFY if not */
+/* Polynomial::verify (sqrt_pst.rs:232-264): TPST_OK if valid, TPST_E_VERIFY if
+ * not, including any proof element that is non-canonical, off its curve or
+ * outside the prime-order subgroup (checked before the transcript absorbs it). */
 int tpst_pst_verify(tpst_ctx* ctx, tpst_transcript* tr, int n, const uint64_t* point, const uint64_t* v,
                     const uint64_t* T, const tpst_open_proof* proof);
+
+/* ---- MultilinearPC single calls (ark-poly-commit fork) --
+ * Against the loaded SRS; a polynomial of nv <= ck.nv variables uses level
+ * ck.nv - nv.  evals: 2^nv canonical Fr (to_evaluations order); point: nv Fr,
+ * LSB-first (as MultilinearPC takes it, cf. a_rev at sqrt_pst.rs:218-225).
+ * commit  (sqrt_pst.rs:124)  -> g_product (G1)
+ * commit_g2 (mipp.rs:133)     -> h_product (G2)
+ * open    (sqrt_pst.rs:225)   -> nv G2 proofs;  open_g1 (mipp.rs:144) -> nv G1
+ * check   (sqrt_pst.rs:261)   -> TPST_OK / TPST_E_VERIFY
+ * check_2 (mipp.rs:307)       -> TPST_OK / TPST_E_VERIFY
+ * The checks reject non-canonical, off-curve or non-subgroup inputs. */
+int tpst_mlpc_commit(tpst_ctx* ctx, const uint64_t* evals, int nv, uint64_t* g_product);
+int tpst_mlpc_commit_g2(tpst_ctx* ctx, const uint64_t* evals, int nv, uint64_t* h_product);
+int tpst_mlpc_open(tpst_ctx* ctx, const uint64_t* evals, int nv, const uint64_t* point, uint64_t* proofs);
+int tpst_mlpc_open_g1(tpst_ctx* ctx, const uint64_t* evals, int nv, const uint64_t* point, uint64_t* proofs);
+int tpst_mlpc_check(tpst_ctx* ctx, int nv, const uint64_t* comm, const uint64_t* point, const uint64_t* value,
+                    const uint64_t* proofs);
+int tpst_mlpc_check_2(tpst_ctx* ctx, int nv, const uint64_t* comm_h, const uint64_t* point, const uint64_t* value,
+                      const uint64_t* proofs);
 
 /* ---- utilities ----------------------------------------------------------- */
 /* out[i] = scalars[i] * G1 generator (affine, canonical); synthetic bases */

@@ -247,9 +247,11 @@ def pst_open_g1(srs, evals, point):
 
 def pst_check(srs, comm, point, value, proofs):
     """MultilinearPC::check (circuit_verifier.rs:245-314):
-    e(C - g^v, h) == prod e(g_mask[i] - g^{pt_i}, pi_i)."""
+    e(C - g^v, h) == prod e(g_mask[nv-len+i] - g^{pt_i}, pi_i)."""
     left = pairing(g1_add(comm, g1_neg(g1_mul(srs.g, value))), srs.h)
-    lefts = [g1_add(srs.g_mask[i], g1_neg(g1_mul(srs.g, point[i]))) for i in range(len(point))]
+    # level offset as in check_2 (0 for the full-level polynomials sqrt_pst.rs:261 checks)
+    off = srs.nv - len(point)
+    lefts = [g1_add(srs.g_mask[off + i], g1_neg(g1_mul(srs.g, point[i]))) for i in range(len(point))]
     return left == multi_pairing(lefts, proofs)
 
 

@@ -113,3 +113,24 @@ def test_bench_max_over_ranks_gloo_world2():
     for p in procs:
         p.join(timeout=60)
     assert res[0] == res[1] and res[0] >= 0.1
+
+
+def test_bench_launcher_spawns_ranks_dry_run():
+    """`python bench.py --gpus 2` (no WORLD_SIZE) starts torch.distributed.run
+    with 2 ranks as a child process; with --dry-run the ranks rendezvous over
+    gloo, time barrier-bracketed steps, take the max over ranks (rank 1 is the
+    slower one) and rank 0 alone prints one JSON line."""
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "5",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["dry_run"] and d["steps"] == 5
+    assert d["ms_per_step"] >= 2.0  # rank 1 sleeps 2 ms per step: the max over ranks is reported

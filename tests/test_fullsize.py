@@ -1,0 +1,87 @@
+"""Parity at the BASELINE sizes (configs[2]: n = 20, configs[3]: n = 24 on one
+GPU) against fixtures the C++ CPU oracle produced over the bench's exact
+inputs (oracle/gen_fullsize.py, shaped like benches/pst.rs:48-62), plus the
+reference's own known-answer test through the device eval.
+
+Every output of Polynomial::{commit, eval, open} (sqrt_pst.rs:105-230) is
+compared bit-exact: T, v, U, the PST proof and every MippProof element in
+full, the 2^m_col-point comm_list by SHA-256 digest and sampled rows.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+import golden_io as G
+from testudo_amd.encoding import fr_array, limbs_to_int
+
+R = 0x12AB655E9A2CA55660B44D1E5C37B00159AA76FED00000010A11800000000001
+
+
+def _arr(hexs, shape):
+    return np.frombuffer(bytes.fromhex(hexs), dtype=np.uint64).reshape(shape)
+
+
+def test_fullsize_fixture_inputs_cpu():
+    """The committed fixtures name the bench's inputs: the point is the stream
+    continuation after Z and the recorded eval matches the CPU oracle."""
+    import orc
+    d = G.load("fullsize_n20.json")
+    n = d["n"]
+    Z, k = orc.fr_stream(d["seed_z"], 1 << n)
+    pt, _ = orc.fr_stream(d["seed_z"], n, k)
+    assert np.array_equal(pt, _arr(d["point"], (n, 4)))
+    assert np.array_equal(orc.pst_eval(Z, n, pt), _arr(d["eval"], (4,)))
+    assert {"n": 24, "srs_nv": 12}.items() <= G.load("fullsize_n24.json").items()
+
+
+@pytest.mark.gpu
+def test_reference_kat_dense_eval_gpu(ctx):
+    """dense_mlpoly.rs:609-623 (Z = [1, 2, 1, 4], r = [4, 3] -> 28) through
+    Polynomial::from_evaluations + eval on the device."""
+    from testudo_amd import sqrt_pst as S
+    d = G.load("kat_dense_eval.json")
+    pl = S.Polynomial.from_evaluations(ctx, fr_array(d["Z"]))
+    assert limbs_to_int(pl.eval(fr_array(d["r"]))) == d["eval"] == 28
+
+
+def _check_fullsize(ctx, n):
+    from testudo_amd import sqrt_pst as S
+    d = G.load("fullsize_n%d.json" % n)
+    m_col, m_row = n // 2, n - n // 2
+    S.srs_setup(ctx, d["srs_nv"], d["seed_srs"])
+    Z, k = S.fr_stream(d["seed_z"], 1 << n)
+    pt, _ = S.fr_stream(d["seed_z"], n, k)
+    assert np.array_equal(pt, _arr(d["point"], (n, 4)))
+    pl = S.Polynomial.from_evaluations(ctx, Z)
+    del Z
+    comms, T = pl.commit()
+    assert hashlib.sha256(comms.tobytes()).hexdigest() == d["comms_sha256"]
+    for r, h in zip(d["comms_rows"], d["comms_sampled"]):
+        assert np.array_equal(comms[r], _arr(h, (12,))), r
+    assert np.array_equal(T, _arr(d["T"], (72,)))
+    v = pl.eval(pt)
+    assert np.array_equal(v, _arr(d["eval"], (4,)))
+    U, pst_proof, mipp = pl.open(S.PoseidonTranscript(), comms, pt, T)
+    assert np.array_equal(U, _arr(d["U"], (12,)))
+    assert np.array_equal(pst_proof, _arr(d["pst_proof"], (m_row, 24)))
+    assert np.array_equal(mipp.comms_t, _arr(d["comms_t"], (m_col, 2, 72)))
+    assert np.array_equal(mipp.comms_u, _arr(d["comms_u"], (m_col, 2, 12)))
+    assert np.array_equal(mipp.final_a, _arr(d["final_a"], (12,)))
+    assert np.array_equal(mipp.final_h, _arr(d["final_h"], (24,)))
+    assert np.array_equal(mipp.pst_proof_h, _arr(d["pst_proof_h"], (m_col, 12)))
+    assert S.verify(ctx, S.PoseidonTranscript(), U, pt, v, pst_proof, mipp, T)
+    bad = fr_array([(limbs_to_int(v) + 1) % R])[0]
+    assert not S.verify(ctx, S.PoseidonTranscript(), U, pt, bad, pst_proof, mipp, T)
+
+
+@pytest.mark.gpu
+def test_fullsize_commit_open_n20(ctx):
+    """BASELINE configs[2]: 2^20-variable commit + open, bit-exact."""
+    _check_fullsize(ctx, 20)
+
+
+@pytest.mark.gpu
+def test_fullsize_commit_open_n24(ctx):
+    """BASELINE configs[3] on one GPU: 2^24-variable commit + open, bit-exact."""
+    _check_fullsize(ctx, 24)

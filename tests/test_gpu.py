@@ -196,20 +196,39 @@ def test_sqrt_pst_vs_cpu_oracle(ctx, n):
 
 
 def test_commit_homomorphism_n20(ctx):
-    """BASELINE config 3 size (2^20, 1024 x 1024): every row commitment
-    C_i == MSM(powers_of_g[0], row_i) (checked for a sample of rows by the
-    K2 path) and c_u == commit(q) (sqrt_pst.rs:206 invariant) via eval."""
+    """BASELINE config 3 size (2^20, 1024 x 1024), size-independent checks:
+    sampled row commitments C_i == K2 MSM(powers_of_g[0], row_i); T == the IPP
+    of the returned comm_list; and the sqrt_pst.rs:206 invariant
+    c_u = MSM(comm_list, chi(b)) == commit(q) with q = Z^T chi(b) computed
+    here on the host with Python integers."""
     from testudo_amd import sqrt_pst as S
     n = 20
+    C = N = 1 << 10
     S.srs_setup(ctx, 10, 0x7E57D1)
     flat = S.srs_export(ctx, 10)
-    pg0 = flat[36:36 + 1024 * 12].reshape(1024, 12)
+    pg0 = flat[36:36 + N * 12].reshape(N, 12)
     Z, k = S.fr_stream(0x7E57D0, 1 << n)
+    pt, _ = S.fr_stream(0x7E57D0, n, k)
     pl = S.Polynomial.from_evaluations(ctx, Z)
     comms, T = pl.commit()
     for i in (0, 1, 517, 1023):
         row = Z[i::1024]
         assert np.array_equal(comms[i], ctx.g1_msm(pg0, row))
+    assert np.array_equal(S.ipp(ctx, n, comms), T)
+    # chi(b), b = point[m_row..], MSB-first (sqrt_pst.rs:152-166)
+    b = [limbs_to_int(x) for x in pt[10:]]
+    chis = [1] * C
+    for i in range(C):
+        for j in range(10):
+            bit = (i >> (9 - j)) & 1
+            chis[i] = chis[i] * (b[j] if bit else (1 - b[j])) % O.R
+    zi = Z.astype(object)
+    zv = (zi[:, 0] + (zi[:, 1] << 64) + (zi[:, 2] << 128) + (zi[:, 3] << 192)).reshape(N, C)
+    q = [int(x) % O.R for x in zv.dot(np.array(chis, dtype=object))]
+    pl.eval(pt)
+    U, _, _ = pl.open(S.PoseidonTranscript(), comms, pt, T)
+    assert np.array_equal(U, ctx.g1_msm(pg0, fr_array(q)))
+    assert np.array_equal(U, ctx.g1_msm(comms, fr_array(chis)))
 
 
 def test_commit_homomorphism_n23_long_chunks(ctx):
@@ -292,3 +311,32 @@ def test_fixed_base_grouped_msm_vs_oracle(ctx, g2):
         for g in range(L // D):
             idx = [(m // D) * L + g * D + m % D for m in range(n // L * D)]
             assert np.array_equal(got[g], ref_msm(bases[idx], s[idx])), (L, D, g)
+
+
+@pytest.mark.parametrize("n,world", [(12, 4), (13, 2)])
+def test_column_slice_upload_matches_full_commit(ctx, n, world):
+    """Multi-GPU shard upload: a rank that uploads only its
+    column block [c0, c1) of the strided view (one 2D copy) commits exactly
+    the same rows and Miller partial as the whole-polynomial handle; the
+    operations that need all of Z refuse a slice."""
+    from testudo_amd import TpstError
+    from testudo_amd import sqrt_pst as S
+    nv = (n + 1) // 2
+    S.srs_setup(ctx, nv, 0x7E57D1)
+    Z, _ = S.fr_stream(0x7E57D0 + 3 * n, 1 << n)
+    full = S.Polynomial.from_evaluations(ctx, Z)
+    comms, T = full.commit()
+    C = 1 << (n // 2)
+    R = C // world
+    parts = []
+    for g in range(world):
+        sl = S.Polynomial.from_evaluations_cols(ctx, Z, g * R, (g + 1) * R)
+        c, ml = sl.commit_rows_partial(g * R, (g + 1) * R)
+        c2, ml2 = full.commit_rows_partial(g * R, (g + 1) * R)
+        assert np.array_equal(c, comms[g * R:(g + 1) * R]) and np.array_equal(ml, ml2)
+        parts.append(ml)
+        with pytest.raises(TpstError):
+            sl.commit_rows(0 if g else R, (g + 2) * R if g + 2 <= world else C)  # outside the slice
+        with pytest.raises(TpstError):
+            sl.eval(np.zeros((n, 4), dtype=np.uint64))
+    assert np.array_equal(S.gt_final_exp_product(ctx, np.stack(parts)), T)

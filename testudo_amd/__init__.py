@@ -5,4 +5,4 @@ include/tpst.h); this package is the host-side binding and the mirror of the
 reference's sqrt-PST surface (``Polynomial.from_evaluations / commit / open /
 verify``, sqrt_pst.rs:14-265).
 """
-from .engine import Context, TpstError  # noqa: F401
+from .engine import Context, Gens, TpstError  # noqa: F401

@@ -27,6 +27,14 @@ PROTOTYPES = [
     ("tpst_g1_msm", C.c_int, [_vp, _u64p, _sz, _u64p, _sz, _u64p]),
     ("tpst_g2_msm", C.c_int, [_vp, _u64p, _sz, _u64p, _sz, _u64p]),
     ("tpst_g1_msm_dev", C.c_int, [_vp, _vp, _vp, _sz, _vp]),
+    ("tpst_g1_multiexp", C.c_int, [_vp, _u64p, _sz, _u64p, _sz, _u64p]),
+    ("tpst_g2_multiexp", C.c_int, [_vp, _u64p, _sz, _u64p, _sz, _u64p]),
+    ("tpst_gens_load", C.c_int, [_vp, _u64p, _sz, _u64p, C.POINTER(_vp)]),
+    ("tpst_gens_free", None, [_vp]),
+    ("tpst_g1_msm_batch", C.c_int, [_vp, _vp, _u64p, _sz, _sz, _sz, _sz, _u64p]),
+    ("tpst_g1_msm_batch_dev", C.c_int, [_vp, _vp, _vp, _sz, _sz, _sz, _sz, _vp]),
+    ("tpst_pedersen_commit_slice", C.c_int, [_vp, _vp, _u64p, _sz, _u64p, _u64p]),
+    ("tpst_pedersen_commit_rows", C.c_int, [_vp, _vp, _u64p, _sz, _u64p, _sz, _u64p]),
     ("tpst_g1_msm_fixed", C.c_int, [_vp, _u64p, _sz, _u64p, _sz, _sz, _u64p]),
     ("tpst_g2_msm_fixed", C.c_int, [_vp, _u64p, _sz, _u64p, _sz, _sz, _u64p]),
     ("tpst_multi_pairing", C.c_int, [_vp, _u64p, _u64p, _sz, _u64p]),
@@ -46,6 +54,7 @@ PROTOTYPES = [
     ("tpst_fr_stream", C.c_uint64, [C.c_uint64, _sz, C.c_uint64, _u64p]),
     ("tpst_poly_from_evaluations", C.c_int, [_vp, _u64p, C.c_int, C.POINTER(_vp)]),
     ("tpst_poly_from_evaluations_dev", C.c_int, [_vp, _vp, C.c_int, C.POINTER(_vp)]),
+    ("tpst_poly_from_evaluations_cols", C.c_int, [_vp, _u64p, C.c_int, _sz, _sz, C.POINTER(_vp)]),
     ("tpst_poly_free", None, [_vp]),
     ("tpst_poly_eval", C.c_int, [_vp, _vp, _u64p, _u64p]),
     ("tpst_poly_commit", C.c_int, [_vp, _vp, _u64p, _u64p]),
@@ -56,6 +65,12 @@ PROTOTYPES = [
     ("tpst_gt_final_exp_product", C.c_int, [_vp, _u64p, _sz, _u64p]),
     ("tpst_poly_open", C.c_int, [_vp, _vp, _vp, _u64p, _u64p, _u64p, _vp]),
     ("tpst_pst_verify", C.c_int, [_vp, _vp, C.c_int, _u64p, _u64p, _u64p, _vp]),
+    ("tpst_mlpc_commit", C.c_int, [_vp, _u64p, C.c_int, _u64p]),
+    ("tpst_mlpc_commit_g2", C.c_int, [_vp, _u64p, C.c_int, _u64p]),
+    ("tpst_mlpc_open", C.c_int, [_vp, _u64p, C.c_int, _u64p, _u64p]),
+    ("tpst_mlpc_open_g1", C.c_int, [_vp, _u64p, C.c_int, _u64p, _u64p]),
+    ("tpst_mlpc_check", C.c_int, [_vp, C.c_int, _u64p, _u64p, _u64p, _u64p]),
+    ("tpst_mlpc_check_2", C.c_int, [_vp, C.c_int, _u64p, _u64p, _u64p, _u64p]),
     ("tpst_profile_enable", C.c_int, [_vp, C.c_int]),
     ("tpst_profile_reset", C.c_int, [_vp]),
     ("tpst_profile_read", C.c_int, [_vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),

@@ -78,6 +78,7 @@ static int msm_host(tpst_ctx* ctx, const uint64_t* bases, size_t nb, const uint6
   std::lock_guard<std::mutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   const size_t n = nb < ns ? nb : ns;  // msm_unchecked truncates
+  if (n > MSM_MAX_POINTS) return fail(ctx, TPST_E_ARG, "MSM longer than 2^27 points: split it");
   constexpr size_t PW = 2 * Words<F>::n;  // u32 per affine point
   ctx->io.reset();
   TPST_HIP(ctx, ctx->io.reserve(Arena::need(n * PW, 4) * 2 + Arena::need(n * 8, 4) + 4096 +
@@ -103,6 +104,19 @@ static int msm_host(tpst_ctx* ctx, const uint64_t* bases, size_t nb, const uint6
 extern "C" int tpst_g1_msm(tpst_ctx* ctx, const uint64_t* bases, size_t n_bases, const uint64_t* scalars,
                            size_t n_scalars, uint64_t* out) {
   return msm_host<Fq>(ctx, bases, n_bases, scalars, n_scalars, out);
+}
+
+// multiexponentiation (mipp.rs:385-394): lengths must agree
+extern "C" int tpst_g1_multiexp(tpst_ctx* ctx, const uint64_t* bases, size_t n_bases, const uint64_t* scalars,
+                                size_t n_scalars, uint64_t* out) {
+  if (n_bases != n_scalars) return fail(ctx, TPST_E_ARG, "InvalidIPVectorLength");
+  return msm_host<Fq>(ctx, bases, n_bases, scalars, n_scalars, out);
+}
+
+extern "C" int tpst_g2_multiexp(tpst_ctx* ctx, const uint64_t* bases, size_t n_bases, const uint64_t* scalars,
+                                size_t n_scalars, uint64_t* out) {
+  if (n_bases != n_scalars) return fail(ctx, TPST_E_ARG, "InvalidIPVectorLength");
+  return msm_host<Fq2>(ctx, bases, n_bases, scalars, n_scalars, out);
 }
 
 extern "C" int tpst_g2_msm(tpst_ctx* ctx, const uint64_t* bases, size_t n_bases, const uint64_t* scalars,
@@ -159,6 +173,7 @@ extern "C" int tpst_g2_msm_fixed(tpst_ctx* ctx, const uint64_t* bases, size_t n,
 
 extern "C" int tpst_g1_msm_dev(tpst_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, void* d_out) {
   if (!ctx || !d_out || (n && (!d_bases || !d_scalars))) return fail(ctx, TPST_E_ARG, "null argument");
+  if (n > MSM_MAX_POINTS) return fail(ctx, TPST_E_ARG, "MSM longer than 2^27 points: split it");
   std::lock_guard<std::mutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   ctx->io.reset();

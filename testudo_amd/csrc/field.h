@@ -490,6 +490,13 @@ template <class C>
 TPST_HD Fp<C> mul3(const Fp<C>& a) { return add(dbl(a), a); }
 
 // ------------------------------------------------------------------ Fq2 ---
+// Translation units whose G2 code is not on a hot path (msm_g2.hip: the
+// verifier's and the C-ABI's variable-base G2 MSMs) define TPST_FQ2_ATTR as
+// TPST_NI before including this header: one out-of-line Fq2 product instead of
+// three inlined Montgomery products per call site keeps their build in seconds.
+#ifndef TPST_FQ2_ATTR
+#define TPST_FQ2_ATTR TPST_HD
+#endif
 struct Fq2 {
   Fq c0, c1;
   static TPST_HD Fq2 zero() { return {Fq::zero(), Fq::zero()}; }
@@ -506,14 +513,14 @@ TPST_HD Fq2 mul3(const Fq2& a) { return {mul3(a.c0), mul3(a.c1)}; }
 TPST_HD Fq mul5(const Fq& a) { return add(dbl(dbl(a)), a); }
 TPST_HD Fq2 conj(const Fq2& a) { return {a.c0, neg(a.c1)}; }
 
-TPST_HD Fq2 mul(const Fq2& a, const Fq2& b) {
+TPST_FQ2_ATTR Fq2 mul(const Fq2& a, const Fq2& b) {
   const Fq v0 = mul(a.c0, b.c0);
   const Fq v1 = mul(a.c1, b.c1);
   const Fq s = mul(add(a.c0, a.c1), add(b.c0, b.c1));
   return {sub(v0, mul5(v1)), sub(sub(s, v0), v1)};
 }
 
-TPST_HD Fq2 sqr(const Fq2& a) {
+TPST_FQ2_ATTR Fq2 sqr(const Fq2& a) {
   // (a0 + a1 u)^2 = a0^2 - 5 a1^2 + 2 a0 a1 u
   const Fq v0 = mul(a.c0, a.c1);
   // (a0 + a1)(a0 - 5 a1) = a0^2 - 5a1^2 - 4 a0 a1

@@ -58,6 +58,11 @@ struct Arena {
   void release();
 };
 
+// Longest variable-base MSM one call accepts: the sort runs over
+// m = 2 W n < 2^31 (key, value) entries (int-sized for hipCUB, u32 bucket
+// bounds).  msm_var returns hipErrorInvalidValue beyond it.
+constexpr size_t MSM_MAX_POINTS = (size_t)1 << 27;
+
 // window size used for a variable-base MSM of n points
 int msm_window_bits(size_t n);
 

@@ -436,12 +436,14 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
     Xyzz<F> inf = Xyzz<F>::inf();
     return hipMemcpyAsync(d_out, &inf, sizeof(inf), hipMemcpyHostToDevice, s);
   }
+  if (n > MSM_MAX_POINTS) return hipErrorInvalidValue;
   constexpr bool kGlv = sizeof(F) == sizeof(Fq);  // G1: phi(x, y) = (beta x, y)
   const bool glv = kGlv && n >= 64;
   const int c = msm_window_bits(glv ? 2 * n : n);
   const int W = glv ? num_windows_bits(c, 128) : num_windows(c);
   const uint32_t nb = 1u << (c - 1);
   const size_t m = (size_t)(glv ? 2 : 1) * W * n;
+  if (m >= ((size_t)1 << 31)) return hipErrorInvalidValue;
   const size_t nbk = (size_t)W * nb;
   const uint32_t sent = (uint32_t)nbk;  // zero digits; sorts after every bucket key
   const int end_bit = bit_length(sent);

@@ -191,6 +191,41 @@ void g1_bytes(const uint64_t* p, uint8_t* b) {  // ark serialize Compress::No
 // host Fr helpers
 Fr fr_inv(const Fr& a) { return inv(a); }
 
+// ---- proof-element validation (the reference's elements are typed arkworks
+// values, validated when deserialized; here they arrive as raw limbs) ----
+bool limbs_lt(const uint64_t* a, const uint32_t* mod32, int n64) {
+  for (int i = n64 - 1; i >= 0; i--) {
+    const uint64_t mi = (uint64_t)mod32[2 * i] | ((uint64_t)mod32[2 * i + 1] << 32);
+    if (a[i] != mi) return a[i] < mi;
+  }
+  return false;
+}
+bool fq_ok(const uint64_t* a) { return limbs_lt(a, params::FQ_P, 6); }
+bool fr_ok(const uint64_t* a) { return limbs_lt(a, params::FR_P, 4); }
+bool all_zero(const uint64_t* a, int n) {
+  for (int i = 0; i < n; i++)
+    if (a[i]) return false;
+  return true;
+}
+// canonical coordinates, on the curve, and r * P == O (prime-order subgroup)
+template <class F>
+bool point_valid(const uint64_t* p) {
+  constexpr int NQ = sizeof(F) / sizeof(Fq);  // Fq coordinates per F
+  for (int k = 0; k < 2 * NQ; k++)
+    if (!fq_ok(p + 6 * k)) return false;
+  if (all_zero(p, 12 * NQ)) return true;  // infinity
+  Affine<F> a;
+  Fq* c = reinterpret_cast<Fq*>(&a);
+  for (int k = 0; k < 2 * NQ; k++) c[k] = fq_canon(p + 6 * k);
+  if (!on_curve(a)) return false;
+  return is_inf(scalar_mul(a, params::FR_P, 253));
+}
+bool gt_ok(const uint64_t* f) {
+  for (int k = 0; k < 12; k++)
+    if (!fq_ok(f + 6 * k)) return false;
+  return true;
+}
+
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
@@ -234,6 +269,10 @@ struct tpst_poly {
   int n, m_col, m_row, odd;
   DevBuf Zown;
   const uint32_t* d_Z = nullptr;  // canonical Fr
+  // column slice (multi-GPU shard): only columns [col0,
+  // col0 + ncols) of the strided view are resident, as an N x ncols block;
+  // ncols == 0 means the whole polynomial
+  size_t col0 = 0, ncols = 0;
   DevBuf q, chis;                 // Montgomery
   bool has_q = false;
 };
@@ -505,6 +544,52 @@ extern "C" int tpst_poly_from_evaluations(tpst_ctx* ctx, const uint64_t* Z, int 
   return TPST_OK;
 }
 
+// rank-local upload of the columns [c0, c1) of the strided view: for every
+// j < 2^m_row the run Z[j 2^m_col + c0 .. j 2^m_col + c1) -- one 2D copy, no
+// host transpose, (c1 - c0) / 2^m_col of the bytes
+extern "C" int tpst_poly_from_evaluations_cols(tpst_ctx* ctx, const uint64_t* Z, int n, size_t c0, size_t c1,
+                                               tpst_poly** out) {
+  if (!ctx || !Z || !out) return fail(ctx, TPST_E_ARG, "null argument");
+  auto p = std::make_unique<tpst_poly>();
+  if (poly_dims(n, p->m_col, p->m_row, p->odd)) return fail(ctx, TPST_E_ARG, "bad num_vars");
+  const size_t C = (size_t)1 << p->m_col, N = (size_t)1 << p->m_row;
+  if (c0 >= c1 || c1 > C) return fail(ctx, TPST_E_ARG, "bad column range");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  p->ctx = ctx;
+  p->n = n;
+  p->col0 = c0;
+  p->ncols = c1 - c0;
+  TPST_HIP(ctx, p->Zown.alloc(N * p->ncols * 32));
+  TPST_HIP(ctx, hipMemcpy2DAsync(p->Zown.p, p->ncols * 32, Z + 4 * c0, C * 32, p->ncols * 32, N,
+                                 hipMemcpyHostToDevice, ctx->stream));
+  TPST_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  p->d_Z = p->Zown.u();
+  *out = p.release();
+  return TPST_OK;
+}
+
+// base pointer and column stride of rows [r0, r1) in the resident block
+static int poly_rows_view(tpst_ctx* ctx, const tpst_poly* p, size_t r0, size_t r1, const uint32_t** base,
+                          size_t* cs) {
+  const size_t C = (size_t)1 << p->m_col;
+  if (!p->ncols) {
+    if (r1 > C) return fail(ctx, TPST_E_ARG, "row range out of bounds");
+    *base = p->d_Z + 8 * r0;
+    *cs = C;
+    return TPST_OK;
+  }
+  if (r0 < p->col0 || r1 > p->col0 + p->ncols) return fail(ctx, TPST_E_ARG, "rows outside the resident column slice");
+  *base = p->d_Z + 8 * (r0 - p->col0);
+  *cs = p->ncols;
+  return TPST_OK;
+}
+
+static int poly_need_full(tpst_ctx* ctx, const tpst_poly* p) {
+  return p->ncols ? fail(ctx, TPST_E_STATE, "operation needs the whole polynomial (this handle holds a column slice)")
+                  : TPST_OK;
+}
+
 extern "C" int tpst_poly_from_evaluations_dev(tpst_ctx* ctx, const void* d_Z, int n, tpst_poly** out) {
   if (!ctx || !d_Z || !out) return fail(ctx, TPST_E_ARG, "null argument");
   auto p = std::make_unique<tpst_poly>();
@@ -539,6 +624,7 @@ static int poly_get_q(tpst_ctx* ctx, tpst_poly* p, const uint64_t* point) {
 extern "C" int tpst_poly_eval(tpst_ctx* ctx, tpst_poly* p, const uint64_t* point, uint64_t* out_v) {
   if (!ctx || !p || !point || !out_v) return fail(ctx, TPST_E_ARG, "null argument");
   std::lock_guard<std::mutex> lk(ctx->mu);
+  if (int rc = poly_need_full(ctx, p)) return rc;
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   if (!p->has_q) {
     int rc = poly_get_q(ctx, p, point);
@@ -581,6 +667,7 @@ static int poly_commit_dev(tpst_ctx* ctx, tpst_poly* p, uint32_t* d_comms_mont, 
 extern "C" int tpst_poly_commit(tpst_ctx* ctx, tpst_poly* p, uint64_t* comms, uint64_t* T) {
   if (!ctx || !p || !comms || !T) return fail(ctx, TPST_E_ARG, "null argument");
   std::lock_guard<std::mutex> lk(ctx->mu);
+  if (int rc = poly_need_full(ctx, p)) return rc;
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   const size_t C = (size_t)1 << p->m_col;
   DevBuf cm, tt, out;
@@ -602,6 +689,7 @@ extern "C" int tpst_poly_commit(tpst_ctx* ctx, tpst_poly* p, uint64_t* comms, ui
 extern "C" int tpst_poly_commit_dev(tpst_ctx* ctx, tpst_poly* p, void* d_comms, void* d_T) {
   if (!ctx || !p || !d_comms || !d_T) return fail(ctx, TPST_E_ARG, "null argument");
   std::lock_guard<std::mutex> lk(ctx->mu);
+  if (int rc = poly_need_full(ctx, p)) return rc;
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   const size_t C = (size_t)1 << p->m_col;
   ctx->io.reset();
@@ -624,15 +712,16 @@ extern "C" int tpst_poly_commit_rows(tpst_ctx* ctx, tpst_poly* p, size_t r0, siz
   SrsState* st = srs_of(ctx);
   if (!st) return fail(ctx, TPST_E_STATE, "no SRS loaded");
   if (st->nv != p->m_row) return fail(ctx, TPST_E_ARG, "SRS num_vars != ceil(n/2)");
-  const size_t C = (size_t)1 << p->m_col;
-  if (r1 > C) return fail(ctx, TPST_E_ARG, "row range out of bounds");
+  const uint32_t* zb;
+  size_t cs;
+  if (int rc = poly_rows_view(ctx, p, r0, r1, &zb, &cs)) return rc;
   const size_t R = r1 - r0;
   if (R == 0) return TPST_OK;
   hipStream_t s = ctx->stream;
   DevBuf rows, out;
   TPST_HIP(ctx, rows.alloc(R * sizeof(Xyzz<Fq>)));
   TPST_HIP(ctx, out.alloc(R * 96));
-  TPST_HIP(ctx, msm_batch(ctx->arena, s, st->tables, p->d_Z + 8 * r0, R, 1, C, (Xyzz<Fq>*)rows.p));
+  TPST_HIP(ctx, msm_batch(ctx->arena, s, st->tables, zb, R, 1, cs, (Xyzz<Fq>*)rows.p));
   TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(s, (Xyzz<Fq>*)rows.p, out.u(), R));
   TPST_HIP(ctx, hipMemcpyAsync(comms, out.p, R * 96, hipMemcpyDeviceToHost, s));
   TPST_HIP(ctx, hipStreamSynchronize(s));
@@ -682,8 +771,9 @@ extern "C" int tpst_poly_commit_rows_partial(tpst_ctx* ctx, tpst_poly* p, size_t
   SrsState* st = srs_of(ctx);
   if (!st) return fail(ctx, TPST_E_STATE, "no SRS loaded");
   if (st->nv != p->m_row) return fail(ctx, TPST_E_ARG, "SRS num_vars != ceil(n/2)");
-  const size_t C = (size_t)1 << p->m_col;
-  if (r1 > C) return fail(ctx, TPST_E_ARG, "row range out of bounds");
+  const uint32_t* zb;
+  size_t cs;
+  if (int rc = poly_rows_view(ctx, p, r0, r1, &zb, &cs)) return rc;
   const size_t R = r1 - r0;
   hipStream_t s = ctx->stream;
   if (R == 0) {  // empty share: comms untouched, partial = 1
@@ -696,7 +786,7 @@ extern "C" int tpst_poly_commit_rows_partial(tpst_ctx* ctx, tpst_poly* p, size_t
   TPST_HIP(ctx, cm.alloc(R * 96));
   TPST_HIP(ctx, out.alloc(R * 96 + 576));
   TPST_HIP(ctx, tt.alloc(sizeof(Fq12)));
-  TPST_HIP(ctx, msm_batch(ctx->arena, s, st->tables, p->d_Z + 8 * r0, R, 1, C, (Xyzz<Fq>*)rows.p));
+  TPST_HIP(ctx, msm_batch(ctx->arena, s, st->tables, zb, R, 1, cs, (Xyzz<Fq>*)rows.p));
   TPST_HIP(ctx, xyzz_to_affine_mont<Fq>(s, (Xyzz<Fq>*)rows.p, cm.u(), R));
   // this rank's h_i and their prepared lines: the coefficient-major cache has
   // row length C, so the R-pair slice is re-prepared (R G2 points, one launch)
@@ -815,10 +905,13 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   (void)T;  // the reference passes T but the prover does not use it (mipp.rs:38)
   if (!ctx || !p || !tr || !comms || !point || !proof) return fail(ctx, TPST_E_ARG, "null argument");
   std::lock_guard<std::mutex> lk(ctx->mu);
+  if (int rc = poly_need_full(ctx, p)) return rc;
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   SrsState* st = srs_of(ctx);
   if (!st) return fail(ctx, TPST_E_STATE, "no SRS loaded");
   if (st->nv != p->m_row) return fail(ctx, TPST_E_ARG, "SRS num_vars != ceil(n/2)");
+  for (size_t i = 0; i < ((size_t)2 << p->m_col); i++)
+    if (!fq_ok(comms + 6 * i)) return fail(ctx, TPST_E_ARG, "comm_list coordinate >= p");
   if (!p->has_q) {
     int rc = poly_get_q(ctx, p, point);
     if (rc) return rc;
@@ -837,14 +930,13 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   Sponge sp;
   sp.load(tr);
 
-  DevBuf A, Ar, Hr, H2, Y, Sc, qc, dW, xa, xh, xy, gts, small, canon;
+  DevBuf A, Ar, Hr, H2, Y, Sc, dW, xa, xh, xy, gts, small, canon;
   TPST_HIP(ctx, A.alloc(C * 96));
   TPST_HIP(ctx, Ar.alloc(C * 96));
   TPST_HIP(ctx, Hr.alloc(C * 192));
   TPST_HIP(ctx, H2.alloc(C * 192));
   TPST_HIP(ctx, Y.alloc(C * 32));
   TPST_HIP(ctx, Sc.alloc(C * 32));
-  TPST_HIP(ctx, qc.alloc(N * 32));
   TPST_HIP(ctx, dW.alloc(C * 32));
   TPST_HIP(ctx, xa.alloc(C * sizeof(Xyzz<Fq>)));
   TPST_HIP(ctx, xh.alloc(C * sizeof(Xyzz<Fq2>)));
@@ -871,13 +963,15 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   const uint32_t* tA = st->t_A.u();
   const uint32_t* tH = st->t_h[p->odd].u();
 
-  // U = c_u = MSM(comms, chis) = commit(q) = MSM(powers_of_g[0], q)   sqrt_pst.rs:198, 206
+  // U = c_u = MSM(comm_list, chi(b)) over the caller's comm_list (sqrt_pst.rs:198),
+  // on the table just built from it; equals commit(q) for this polynomial's own
+  // comm_list (the :206 invariant, checked by the tests)
   {
-    TPST_HIP(ctx, fr_from_mont(s, p->q.u(), qc.u(), N));
+    TPST_HIP(ctx, fr_from_mont(s, p->chis.u(), Sc.u(), C));
     FbGroups g;
-    g.members = N;
-    g.L = g.D = N;
-    TPST_HIP(ctx, fbt_msm<Fq>(ctx->arena, s, st->t_pg0.u(), qc.u(), g, x1));
+    g.members = C;
+    g.L = g.D = C;
+    TPST_HIP(ctx, fbt_msm<Fq>(ctx->arena, s, tA, Sc.u(), g, x1));
   }
   TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(s, x1, canon.u(), 1));
   TPST_HIP(ctx, hipMemcpyAsync(proof->U, canon.p, 96, hipMemcpyDeviceToHost, s));
@@ -1085,6 +1179,229 @@ static bool gt_is_one(const uint64_t* gt) {
 
 static void push(std::vector<uint64_t>& v, const uint64_t* p, size_t n) { v.insert(v.end(), p, p + n); }
 
+// MultilinearPC::check (circuit_verifier.rs:245-314): for k points pt (LSB-first,
+// canonical Fr) and k G2 proofs,
+//   e(C - g^v, h) * prod_i e(g^{pt_i} - g_mask[nv - k + i], pi_i) == 1.
+// A polynomial of k < ck.nv variables lives on SRS level ck.nv - k, i.e. on
+// the trapdoor coordinates t[ck.nv - k ..], hence the mask offset (the same
+// offset check_2 applies to h_mask, circuit_verifier.rs:214); the reference
+// only checks full-level polynomials (sqrt_pst.rs:261), where it is 0.
+static int mlpc_check_impl(tpst_ctx* ctx, SrsState* st, int k, const uint64_t* comm, const uint64_t* pt,
+                           const uint64_t* v, const uint64_t* proofs) {
+  const uint64_t* flat = st->flat.data();
+  const uint64_t* g = flat;
+  const uint64_t* h = flat + 12;
+  const uint64_t* gmask = flat + tpst_srs_flat_len(st->nv) - 36 * st->nv;
+  const uint64_t one[4] = {1, 0, 0, 0};
+  uint64_t minus1[4], negv[4];
+  fr_out(sub(Fr::zero(), Fr::one()), minus1);
+  fr_out(sub(Fr::zero(), fr_canon(v)), negv);
+  std::vector<uint64_t> g1s, g2s, pts, sc;
+  uint64_t q[12];
+  int rc;
+  push(pts, comm, 12);
+  push(sc, one, 4);
+  push(pts, g, 12);
+  push(sc, negv, 4);
+  if ((rc = small_msm<Fq>(ctx, pts, sc, q))) return rc;
+  push(g1s, q, 12);
+  push(g2s, h, 24);
+  for (int i = 0; i < k; i++) {
+    pts.clear();
+    sc.clear();
+    push(pts, g, 12);
+    push(sc, pt + 4 * i, 4);
+    push(pts, gmask + 12 * (st->nv - k + i), 12);
+    push(sc, minus1, 4);
+    if ((rc = small_msm<Fq>(ctx, pts, sc, q))) return rc;
+    push(g1s, q, 12);
+    push(g2s, proofs + 24 * i, 24);
+  }
+  uint64_t gt[72];
+  if ((rc = pairing_product(ctx, g1s, g2s, gt))) return rc;
+  return gt_is_one(gt) ? TPST_OK : TPST_E_VERIFY;
+}
+
+// check_2 (circuit_verifier.rs:175-243; mipp.rs:307): G2 commitment C_h, k G1
+// proofs,  e(g, C_h - h^v) * prod_i e(pi_i, h^{pt_i} - h_mask[nv - k + i]) == 1
+static int mlpc_check2_impl(tpst_ctx* ctx, SrsState* st, int k, const uint64_t* comm_h, const uint64_t* pt,
+                            const uint64_t* v, const uint64_t* proofs) {
+  const uint64_t* flat = st->flat.data();
+  const uint64_t* g = flat;
+  const uint64_t* h = flat + 12;
+  const uint64_t* hmask = flat + tpst_srs_flat_len(st->nv) - 24 * st->nv;
+  const uint64_t one[4] = {1, 0, 0, 0};
+  uint64_t minus1[4], negv[4];
+  fr_out(sub(Fr::zero(), Fr::one()), minus1);
+  fr_out(sub(Fr::zero(), fr_canon(v)), negv);
+  std::vector<uint64_t> g1s, g2s, pts, sc;
+  uint64_t q[24];
+  int rc;
+  push(pts, comm_h, 24);
+  push(sc, one, 4);
+  push(pts, h, 24);
+  push(sc, negv, 4);
+  if ((rc = small_msm<Fq2>(ctx, pts, sc, q))) return rc;
+  push(g1s, g, 12);
+  push(g2s, q, 24);
+  for (int i = 0; i < k; i++) {
+    pts.clear();
+    sc.clear();
+    push(pts, h, 24);
+    push(sc, pt + 4 * i, 4);
+    push(pts, hmask + 24 * (st->nv - k + i), 24);
+    push(sc, minus1, 4);
+    if ((rc = small_msm<Fq2>(ctx, pts, sc, q))) return rc;
+    push(g1s, proofs + 12 * i, 12);
+    push(g2s, q, 24);
+  }
+  uint64_t gt[72];
+  if ((rc = pairing_product(ctx, g1s, g2s, gt))) return rc;
+  return gt_is_one(gt) ? TPST_OK : TPST_E_VERIFY;
+}
+
+// ------------------------------------------------- MultilinearPC calls ---
+// Single-call forms of the ark-poly-commit fork's MultilinearPC<E> used by the
+// reference: commit (sqrt_pst.rs:124), commit_g2
+// (mipp.rs:133), open (sqrt_pst.rs:225), open_g1 (mipp.rs:144), check
+// (sqrt_pst.rs:261), check_2 (mipp.rs:307).  A polynomial of nv variables uses
+// SRS level ck.nv - nv (the variable-CRS offset); points are LSB-first as
+// MultilinearPC takes them; values canonical.
+static int mlpc_args(tpst_ctx* ctx, SrsState* st, int nv) {
+  if (!st) return fail(ctx, TPST_E_STATE, "no SRS loaded");
+  if (nv < 0 || nv > st->nv) return fail(ctx, TPST_E_ARG, "num_vars > SRS num_vars");
+  return TPST_OK;
+}
+
+template <class F>
+static int mlpc_commit_impl(tpst_ctx* ctx, const uint64_t* evals, int nv, uint64_t* out) {
+  if (!ctx || !evals || !out) return fail(ctx, TPST_E_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  SrsState* st = srs_of(ctx);
+  int rc = mlpc_args(ctx, st, nv);
+  if (rc) return rc;
+  const size_t n = (size_t)1 << nv;
+  const int lvl = st->nv - nv;
+  constexpr size_t PW = 2 * Words<F>::n;
+  const uint32_t* bases;
+  if (lvl < st->nv) {
+    bases = (sizeof(F) == sizeof(Fq) ? st->pg[lvl] : st->ph[lvl])->u();
+  } else {  // nv = 0: the level of one base is g (h), the constant polynomial
+    bases = (sizeof(F) == sizeof(Fq) ? st->g : st->h).u();
+  }
+  hipStream_t s = ctx->stream;
+  DevBuf sc, r, o;
+  TPST_HIP(ctx, sc.alloc(n * 32));
+  TPST_HIP(ctx, r.alloc(sizeof(Xyzz<F>)));
+  TPST_HIP(ctx, o.alloc(PW * 4));
+  TPST_HIP(ctx, hipMemcpyAsync(sc.p, evals, n * 32, hipMemcpyHostToDevice, s));
+  TPST_HIP(ctx, msm_var<F>(ctx->arena, s, bases, sc.u(), n, (Xyzz<F>*)r.p));
+  TPST_HIP(ctx, xyzz_to_affine_canonical<F>(s, (Xyzz<F>*)r.p, o.u(), 1));
+  TPST_HIP(ctx, hipMemcpyAsync(out, o.p, PW * 4, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipStreamSynchronize(s));
+  return TPST_OK;
+}
+
+extern "C" int tpst_mlpc_commit(tpst_ctx* ctx, const uint64_t* evals, int nv, uint64_t* g_product) {
+  return mlpc_commit_impl<Fq>(ctx, evals, nv, g_product);
+}
+
+extern "C" int tpst_mlpc_commit_g2(tpst_ctx* ctx, const uint64_t* evals, int nv, uint64_t* h_product) {
+  return mlpc_commit_impl<Fq2>(ctx, evals, nv, h_product);
+}
+
+template <class F>
+static int mlpc_open_impl(tpst_ctx* ctx, const uint64_t* evals, int nv, const uint64_t* point, uint64_t* proofs) {
+  if (!ctx || !evals || !point || !proofs) return fail(ctx, TPST_E_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  SrsState* st = srs_of(ctx);
+  int rc = mlpc_args(ctx, st, nv);
+  if (rc) return rc;
+  if (nv == 0) return TPST_OK;  // no quotients
+  for (int i = 0; i < nv; i++)
+    if (!fr_ok(point + 4 * i)) return fail(ctx, TPST_E_ARG, "point coordinate >= r");
+  const size_t n = (size_t)1 << nv;
+  constexpr size_t PW = 2 * Words<F>::n;
+  hipStream_t s = ctx->stream;
+  DevBuf ev, pt, r, o;
+  TPST_HIP(ctx, ev.alloc(n * 32));
+  TPST_HIP(ctx, pt.alloc(nv * 32));
+  TPST_HIP(ctx, r.alloc(nv * sizeof(Xyzz<F>)));
+  TPST_HIP(ctx, o.alloc(nv * PW * 4));
+  TPST_HIP(ctx, hipMemcpyAsync(ev.p, evals, n * 32, hipMemcpyHostToDevice, s));
+  TPST_HIP(ctx, hipMemcpyAsync(pt.p, point, nv * 32, hipMemcpyHostToDevice, s));
+  TPST_HIP(ctx, fr_to_mont(s, ev.u(), ev.u(), n));
+  TPST_HIP(ctx, fr_to_mont(s, pt.u(), pt.u(), nv));
+  const uint32_t* table = sizeof(F) == sizeof(Fq) ? st->t_pgp.u() : st->t_php.u();
+  rc = pst_open_fbt<F>(ctx, st, table, st->nv - nv, ev.u(), nv, pt.u(), (Xyzz<F>*)r.p);
+  if (rc) return rc;
+  TPST_HIP(ctx, xyzz_to_affine_canonical<F>(s, (Xyzz<F>*)r.p, o.u(), nv));
+  TPST_HIP(ctx, hipMemcpyAsync(proofs, o.p, nv * PW * 4, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipStreamSynchronize(s));
+  return TPST_OK;
+}
+
+extern "C" int tpst_mlpc_open(tpst_ctx* ctx, const uint64_t* evals, int nv, const uint64_t* point,
+                              uint64_t* proofs) {
+  return mlpc_open_impl<Fq2>(ctx, evals, nv, point, proofs);
+}
+
+extern "C" int tpst_mlpc_open_g1(tpst_ctx* ctx, const uint64_t* evals, int nv, const uint64_t* point,
+                                 uint64_t* proofs) {
+  return mlpc_open_impl<Fq>(ctx, evals, nv, point, proofs);
+}
+
+extern "C" int tpst_mlpc_check(tpst_ctx* ctx, int nv, const uint64_t* comm, const uint64_t* point,
+                               const uint64_t* value, const uint64_t* proofs) {
+  if (!ctx || !comm || !point || !value || (nv && !proofs)) return fail(ctx, TPST_E_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  SrsState* st = srs_of(ctx);
+  int rc = mlpc_args(ctx, st, nv);
+  if (rc) return rc;
+  if (!fr_ok(value) || !point_valid<Fq>(comm)) return fail(ctx, TPST_E_VERIFY, "malformed input");
+  for (int i = 0; i < nv; i++)
+    if (!fr_ok(point + 4 * i) || !point_valid<Fq2>(proofs + 24 * i)) return fail(ctx, TPST_E_VERIFY, "malformed input");
+  return mlpc_check_impl(ctx, st, nv, comm, point, value, proofs);
+}
+
+extern "C" int tpst_mlpc_check_2(tpst_ctx* ctx, int nv, const uint64_t* comm_h, const uint64_t* point,
+                                 const uint64_t* value, const uint64_t* proofs) {
+  if (!ctx || !comm_h || !point || !value || (nv && !proofs)) return fail(ctx, TPST_E_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  SrsState* st = srs_of(ctx);
+  int rc = mlpc_args(ctx, st, nv);
+  if (rc) return rc;
+  if (!fr_ok(value) || !point_valid<Fq2>(comm_h)) return fail(ctx, TPST_E_VERIFY, "malformed input");
+  for (int i = 0; i < nv; i++)
+    if (!fr_ok(point + 4 * i) || !point_valid<Fq>(proofs + 12 * i)) return fail(ctx, TPST_E_VERIFY, "malformed input");
+  return mlpc_check2_impl(ctx, st, nv, comm_h, point, value, proofs);
+}
+
+// Every proof element is validated before the transcript absorbs it (a
+// non-canonical encoding of a point would otherwise change the Fiat-Shamir
+// challenges without changing the point): Fq limbs < p, points on the curve
+// and in the r-torsion, GT coefficients < p, scalars < r.
+static bool proof_valid(const tpst_open_proof* pr, int n, const uint64_t* point, const uint64_t* v,
+                        const uint64_t* T) {
+  for (int i = 0; i < n; i++)
+    if (!fr_ok(point + 4 * i)) return false;
+  if (!fr_ok(v) || !gt_ok(T) || !point_valid<Fq>(pr->U) || !point_valid<Fq>(pr->final_a) ||
+      !point_valid<Fq2>(pr->final_h))
+    return false;
+  for (int i = 0; i < pr->m_col; i++) {
+    if (!point_valid<Fq>(pr->comms_u[i][0]) || !point_valid<Fq>(pr->comms_u[i][1]) || !gt_ok(pr->comms_t[i][0]) ||
+        !gt_ok(pr->comms_t[i][1]) || !point_valid<Fq>(pr->pst_proof_h[i]))
+      return false;
+  }
+  for (int i = 0; i < pr->m_row; i++)
+    if (!point_valid<Fq2>(pr->pst_proof[i])) return false;
+  return true;
+}
+
 extern "C" int tpst_pst_verify(tpst_ctx* ctx, tpst_transcript* tr, int n, const uint64_t* point, const uint64_t* v,
                                const uint64_t* T, const tpst_open_proof* proof) {
   if (!ctx || !tr || !point || !v || !T || !proof) return fail(ctx, TPST_E_ARG, "null argument");
@@ -1095,11 +1412,7 @@ extern "C" int tpst_pst_verify(tpst_ctx* ctx, tpst_transcript* tr, int n, const 
   SrsState* st = srs_of(ctx);
   if (!st) return fail(ctx, TPST_E_STATE, "no SRS loaded");
   if (st->nv != m_row || proof->m_col != m_col || proof->m_row != m_row) return fail(ctx, TPST_E_ARG, "size mismatch");
-  const uint64_t* flat = st->flat.data();
-  const uint64_t* g = flat;
-  const uint64_t* h = flat + 12;
-  const uint64_t* gmask = flat + tpst_srs_flat_len(st->nv) - 36 * st->nv;
-  const uint64_t* hmask = gmask + 12 * st->nv;
+  if (!proof_valid(proof, n, point, v, T)) return fail(ctx, TPST_E_VERIFY, "malformed proof element (non-canonical, off-curve or outside the subgroup)");
   const int m = m_col;
   Sponge sp;
   sp.load(tr);
@@ -1200,58 +1513,19 @@ extern "C" int tpst_pst_verify(tpst_ctx* ctx, tpst_transcript* tr, int n, const 
       if (memcmp(lim, ft + 6 * q, 48) != 0) return TPST_E_VERIFY;
     }
   }
-  // check_2 (mipp.rs:307): e(g, C_h - h^v) * prod e(pi_i, h^{rs_i} - h_mask[nv-m+i]) == 1
+  // check_2 (mipp.rs:307) of final_h at rs with value vh
   {
-    std::vector<uint64_t> g1s, g2s;
-    uint64_t q[24];
-    std::vector<uint64_t> pts, sc;
-    push(pts, proof->final_h, 24);
-    push(sc, canon4(Fr::one()).data(), 4);
-    push(pts, h, 24);
-    push(sc, canon4(negc(vh)).data(), 4);
-    if ((rc = small_msm<Fq2>(ctx, pts, sc, q))) return rc;
-    push(g1s, g, 12);
-    push(g2s, q, 24);
-    for (int i = 0; i < m; i++) {
-      pts.clear();
-      sc.clear();
-      push(pts, h, 24);
-      push(sc, canon4(rs[i]).data(), 4);
-      push(pts, hmask + 24 * (st->nv - m + i), 24);
-      push(sc, canon4(negc(Fr::one())).data(), 4);
-      if ((rc = small_msm<Fq2>(ctx, pts, sc, q))) return rc;
-      push(g1s, proof->pst_proof_h[i], 12);
-      push(g2s, q, 24);
-    }
-    uint64_t gt[72];
-    if ((rc = pairing_product(ctx, g1s, g2s, gt))) return rc;
-    if (!gt_is_one(gt)) return TPST_E_VERIFY;
+    std::vector<uint64_t> rsc(4 * m);
+    for (int i = 0; i < m; i++) fr_out(rs[i], &rsc[4 * i]);
+    uint64_t vhc[4];
+    fr_out(vh, vhc);
+    if ((rc = mlpc_check2_impl(ctx, st, m, proof->final_h, rsc.data(), vhc, &proof->pst_proof_h[0][0]))) return rc;
   }
-  // MultilinearPC::check (sqrt_pst.rs:261): e(U - g^v, h) * prod e(g^{a_i} - g_mask_i, pi_i) == 1
+  // MultilinearPC::check of U at a_rev (sqrt_pst.rs:261)
   {
-    std::vector<uint64_t> g1s, g2s, pts, sc;
-    uint64_t q[12];
-    push(pts, proof->U, 12);
-    push(sc, canon4(Fr::one()).data(), 4);
-    push(pts, g, 12);
-    push(sc, canon4(negc(fr_canon(v))).data(), 4);
-    if ((rc = small_msm<Fq>(ctx, pts, sc, q))) return rc;
-    push(g1s, q, 12);
-    push(g2s, h, 24);
-    for (int i = 0; i < m_row; i++) {
-      pts.clear();
-      sc.clear();
-      push(pts, g, 12);
-      push(sc, point + 4 * (m_row - 1 - i), 4);  // a_rev[i]
-      push(pts, gmask + 12 * i, 12);
-      push(sc, canon4(negc(Fr::one())).data(), 4);
-      if ((rc = small_msm<Fq>(ctx, pts, sc, q))) return rc;
-      push(g1s, q, 12);
-      push(g2s, proof->pst_proof[i], 24);
-    }
-    uint64_t gt[72];
-    if ((rc = pairing_product(ctx, g1s, g2s, gt))) return rc;
-    if (!gt_is_one(gt)) return TPST_E_VERIFY;
+    std::vector<uint64_t> arev(4 * m_row);
+    for (int i = 0; i < m_row; i++) memcpy(&arev[4 * i], point + 4 * (m_row - 1 - i), 32);
+    if ((rc = mlpc_check_impl(ctx, st, m_row, proof->U, arev.data(), v, &proof->pst_proof[0][0]))) return rc;
   }
   sp.store(tr);
   return TPST_OK;

@@ -60,6 +60,17 @@ class Context:
                    "tpst_g2_msm")
         return out
 
+    def multiexp(self, bases: np.ndarray, scalars: np.ndarray, g2: bool = False) -> np.ndarray:
+        """mipp.rs:385-394 `multiexponentiation`: raises on a length mismatch
+        (the reference's Err(InvalidIPVectorLength))."""
+        w = 24 if g2 else 12
+        bases = np.ascontiguousarray(bases, dtype=np.uint64).reshape(-1, w)
+        scalars = np.ascontiguousarray(scalars, dtype=np.uint64).reshape(-1, 4)
+        out = np.zeros(w, dtype=np.uint64)
+        fn = self.lib.tpst_g2_multiexp if g2 else self.lib.tpst_g1_multiexp
+        self.check(fn(self.h, ptr(bases), len(bases), ptr(scalars), len(scalars), ptr(out)), "multiexponentiation")
+        return out
+
     def msm_fixed(self, bases: np.ndarray, scalars: np.ndarray, L: int = 0, D: int = 0, g2: bool = False):
         """Grouped fixed-base MSM (include/tpst.h tpst_g*_msm_fixed): (L/D, 12|24)."""
         w = 24 if g2 else 12
@@ -127,3 +138,58 @@ class Context:
         ms = C.c_double()
         self.check(self.lib.tpst_microbench(self.h, kind, threads, iters, C.byref(ms)), "tpst_microbench")
         return ms.value
+
+
+class Gens:
+    """MultiCommitGens {n, G, h} (commitments.rs:9-15) resident on the device,
+    with PedersenCommit::commit_slice (commitments.rs:79-86), the Hyrax row
+    commitments of DensePolynomial::commit_inner (dense_mlpoly.rs:314-329) and
+    the strided shared-base batch MSM."""
+
+    def __init__(self, ctx: Context, G: np.ndarray, h: np.ndarray = None):
+        self.ctx = ctx
+        G = np.ascontiguousarray(G, dtype=np.uint64).reshape(-1, 12)
+        self.n = len(G)
+        hh = None if h is None else np.ascontiguousarray(h, dtype=np.uint64).reshape(12)
+        handle = C.c_void_p()
+        ctx.check(ctx.lib.tpst_gens_load(ctx.h, ptr(G), self.n, ptr(hh) if hh is not None else None,
+                                         C.byref(handle)), "tpst_gens_load")
+        self.handle = handle
+
+    def close(self):
+        if self.handle:
+            self.ctx.lib.tpst_gens_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def msm_batch(self, scalars: np.ndarray, rows: int, row_stride: int, col_stride: int) -> np.ndarray:
+        scalars = np.ascontiguousarray(scalars, dtype=np.uint64).reshape(-1, 4)
+        out = np.zeros((rows, 12), dtype=np.uint64)
+        if rows and self.n:
+            need = (rows - 1) * row_stride + (self.n - 1) * col_stride + 1
+            if len(scalars) < need:
+                raise TpstError("scalar buffer shorter than the strided view")
+        self.ctx.check(self.ctx.lib.tpst_g1_msm_batch(self.ctx.h, self.handle, ptr(scalars), rows, self.n,
+                                                      row_stride, col_stride, ptr(out)), "tpst_g1_msm_batch")
+        return out
+
+    def commit_slice(self, scalars: np.ndarray, blind: np.ndarray) -> np.ndarray:
+        scalars = np.ascontiguousarray(scalars, dtype=np.uint64).reshape(-1, 4)
+        blind = np.ascontiguousarray(blind, dtype=np.uint64).reshape(4)
+        out = np.zeros(12, dtype=np.uint64)
+        self.ctx.check(self.ctx.lib.tpst_pedersen_commit_slice(self.ctx.h, self.handle, ptr(scalars), len(scalars),
+                                                               ptr(blind), ptr(out)), "commit_slice")
+        return out
+
+    def commit_rows(self, Z: np.ndarray, blinds: np.ndarray) -> np.ndarray:
+        Z = np.ascontiguousarray(Z, dtype=np.uint64).reshape(-1, 4)
+        blinds = np.ascontiguousarray(blinds, dtype=np.uint64).reshape(-1, 4)
+        out = np.zeros((len(blinds), 12), dtype=np.uint64)
+        self.ctx.check(self.ctx.lib.tpst_pedersen_commit_rows(self.ctx.h, self.handle, ptr(Z), len(Z), ptr(blinds),
+                                                              len(blinds), ptr(out)), "commit_inner")
+        return out

@@ -85,6 +85,75 @@ def fr_stream(seed: int, n: int, start: int = 0):
     return out, nxt
 
 
+class MultilinearPC:
+    """The ark-poly-commit fork's MultilinearPC<Bls12_377> calls the reference
+    makes, against the SRS loaded in ``ctx``.  Points are
+    LSB-first (MultilinearPC's order); ``check``/``check_2`` return bool."""
+
+    @staticmethod
+    def commit(ctx: Context, evals) -> np.ndarray:
+        """sqrt_pst.rs:124 -> g_product (12,)."""
+        evals = _u64(evals).reshape(-1, 4)
+        nv = len(evals).bit_length() - 1
+        out = np.zeros(12, dtype=np.uint64)
+        ctx.check(ctx.lib.tpst_mlpc_commit(ctx.h, ptr(evals), nv, ptr(out)), "MultilinearPC::commit")
+        return out
+
+    @staticmethod
+    def commit_g2(ctx: Context, evals) -> np.ndarray:
+        """mipp.rs:133 -> h_product (24,)."""
+        evals = _u64(evals).reshape(-1, 4)
+        nv = len(evals).bit_length() - 1
+        out = np.zeros(24, dtype=np.uint64)
+        ctx.check(ctx.lib.tpst_mlpc_commit_g2(ctx.h, ptr(evals), nv, ptr(out)), "MultilinearPC::commit_g2")
+        return out
+
+    @staticmethod
+    def open(ctx: Context, evals, point) -> np.ndarray:
+        """sqrt_pst.rs:225 -> Proof (nv, 24) G2."""
+        evals = _u64(evals).reshape(-1, 4)
+        nv = len(evals).bit_length() - 1
+        point = _u64(point, (nv, 4))
+        out = np.zeros((nv, 24), dtype=np.uint64)
+        ctx.check(ctx.lib.tpst_mlpc_open(ctx.h, ptr(evals), nv, ptr(point), ptr(out)), "MultilinearPC::open")
+        return out
+
+    @staticmethod
+    def open_g1(ctx: Context, evals, point) -> np.ndarray:
+        """mipp.rs:144 -> ProofG1 (nv, 12)."""
+        evals = _u64(evals).reshape(-1, 4)
+        nv = len(evals).bit_length() - 1
+        point = _u64(point, (nv, 4))
+        out = np.zeros((nv, 12), dtype=np.uint64)
+        ctx.check(ctx.lib.tpst_mlpc_open_g1(ctx.h, ptr(evals), nv, ptr(point), ptr(out)), "MultilinearPC::open_g1")
+        return out
+
+    @staticmethod
+    def _chk(ctx, fn, nv, comm, point, value, proofs, what):
+        rc = fn(ctx.h, nv, ptr(comm), ptr(point), ptr(value), ptr(proofs))
+        if rc == -5:
+            return False
+        ctx.check(rc, what)
+        return True
+
+    @staticmethod
+    def check(ctx: Context, comm, point, value, proofs) -> bool:
+        """sqrt_pst.rs:261."""
+        point = _u64(point).reshape(-1, 4)
+        nv = len(point)
+        return MultilinearPC._chk(ctx, ctx.lib.tpst_mlpc_check, nv, _u64(comm, (12,)), point, _u64(value, (4,)),
+                                  _u64(proofs, (nv, 24)) if nv else np.zeros(24, np.uint64),
+                                  "MultilinearPC::check")
+
+    @staticmethod
+    def check_2(ctx: Context, comm_h, point, value, proofs) -> bool:
+        """mipp.rs:307."""
+        point = _u64(point).reshape(-1, 4)
+        nv = len(point)
+        return MultilinearPC._chk(ctx, ctx.lib.tpst_mlpc_check_2, nv, _u64(comm_h, (24,)), point, _u64(value, (4,)),
+                                  _u64(proofs, (nv, 12)) if nv else np.zeros(12, np.uint64), "MultilinearPC::check_2")
+
+
 class Polynomial:
     """sqrt_pst.rs:14-20 -- 2^n evaluations viewed as 2^m_col rows of 2^m_row."""
 
@@ -106,6 +175,19 @@ class Polynomial:
             raise TpstError("evaluation count must be a power of two")
         h = C.c_void_p()
         ctx.check(ctx.lib.tpst_poly_from_evaluations(ctx.h, ptr(Z), n, C.byref(h)), "from_evaluations")
+        return cls(ctx, h, n)
+
+    @classmethod
+    def from_evaluations_cols(cls, ctx: Context, Z: np.ndarray, c0: int, c1: int) -> "Polynomial":
+        """This rank's column block [c0, c1) of the strided view only (one 2D
+        copy); serves commit_rows / commit_rows_partial for rows in [c0, c1)."""
+        Z = _u64(Z).reshape(-1, 4)
+        n = int(len(Z)).bit_length() - 1
+        if 1 << n != len(Z):
+            raise TpstError("evaluation count must be a power of two")
+        h = C.c_void_p()
+        ctx.check(ctx.lib.tpst_poly_from_evaluations_cols(ctx.h, ptr(Z), n, c0, c1, C.byref(h)),
+                  "from_evaluations_cols")
         return cls(ctx, h, n)
 
     @classmethod
