@@ -225,7 +225,8 @@ int tpst_g2_mul_generator(tpst_ctx* ctx, const uint64_t* scalars, size_t n, uint
 int tpst_g1_mul_generator_dev(tpst_ctx* ctx, const void* d_scalars, size_t n, void* d_out_mont);
 
 /* Field microbenchmark (measured peak for the roofline's compute column):
- * kind 0 = Fq Montgomery multiply, 1 = G1 XYZZ mixed add, 2 = Fq inverse, 16 + op = one wave
+ * kind 0 = Fq Montgomery multiply, 1 = G1 XYZZ mixed add, 2 = Fq inverse, 3 / 4 = Fq multiply
+ * variants (two interleaved accumulation chains / independent columns), 5 = G1 XYZZ doubling, 16 + op = one wave
  * running `iters` stages of wave-engine op `op` (csrc/wave_ops.inc).  Runs `threads`
  * threads x `iters` dependent ops each; returns kernel milliseconds. */
 int tpst_microbench(tpst_ctx* ctx, int kind, size_t threads, int iters, double* ms);

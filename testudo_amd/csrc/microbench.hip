@@ -20,6 +20,134 @@ __global__ void k_mb_fqmul(int iters, uint32_t* out) {
   store_f<Fq>(out + 12 * (size_t)t, a);
 }
 
+// ---- A/B variants of the device Montgomery product (latency experiments) --
+// ILP2: product scanning with the terms of every column split over two
+// independent (acc, hi) chains, merged when the column completes.
+__device__ __forceinline__ Fq mul_ilp2(const Fq& a, const Fq& b) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  return mul(a, b);
+#else
+  constexpr int N = 12;
+  uint32_t m[N], t[N];
+  uint64_t acc = 0;
+  uint32_t hi = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; k++) {
+    uint64_t a1 = 0;
+    uint32_t h1 = 0;
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < N) {
+        if (cnt++ & 1) mac_vv(a1, h1, a.v[i], b.v[j]);
+        else mac_vv(acc, hi, a.v[i], b.v[j]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      const int j = k - i;
+      if (i < k && j >= 1 && j < N) {
+        if (cnt++ & 1) mac_vs(a1, h1, m[i], FqCfg::p(j));
+        else mac_vs(acc, hi, m[i], FqCfg::p(j));
+      }
+    }
+    {  // merge the chains: (hi:acc) += (h1:a1)
+      const uint64_t s = acc + a1;
+      hi += h1 + (s < acc ? 1u : 0u);
+      acc = s;
+    }
+    if (k < N) {
+      const uint32_t lo = (uint32_t)acc;
+      m[k] = 0u - lo;
+      acc = ((acc >> 32) | ((uint64_t)hi << 32)) + (lo != 0u ? 1u : 0u);
+      hi = 0;
+      continue;
+    } else {
+      t[k - N] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+  t[N - 1] = (uint32_t)acc;
+  Fq r;
+#pragma unroll
+  for (int j = 0; j < N; j++) r.v[j] = t[j];
+  reduce_once(r);
+  return r;
+#endif
+}
+
+// COLS: the 23 columns of a*b accumulate independently (no chain between
+// columns), then a word-serial Montgomery reduction over the column sums.
+__device__ __forceinline__ Fq mul_cols(const Fq& a, const Fq& b) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  return mul(a, b);
+#else
+  constexpr int N = 12;
+  uint64_t c[2 * N];
+  uint32_t h[2 * N];
+#pragma unroll
+  for (int k = 0; k < 2 * N; k++) {
+    c[k] = 0;
+    h[k] = 0;
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++)
+#pragma unroll
+    for (int j = 0; j < N; j++) mac_vv(c[i + j], h[i + j], a.v[i], b.v[j]);
+  // REDC: word k exact once column k - 1's carry is in
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    const uint32_t lo = (uint32_t)c[k];
+    const uint32_t mk = 0u - lo;  // p0 = 1
+#pragma unroll
+    for (int j = 1; j < N; j++) mac_vs(c[k + j], h[k + j], mk, FqCfg::p(j));
+    // column k + mk*p0 = (c[k] - lo) + 2^32*(lo != 0): carry up
+    const uint64_t up = (c[k] >> 32) | ((uint64_t)h[k] << 32);
+    const uint64_t add = up + (lo != 0u ? 1u : 0u);
+    const uint64_t s = c[k + 1] + add;
+    h[k + 1] += (s < c[k + 1] ? 1u : 0u);
+    c[k + 1] = s;
+  }
+  Fq r;
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    const int k = N + j;
+    r.v[j] = (uint32_t)c[k];
+    const uint64_t up = (c[k] >> 32) | ((uint64_t)h[k] << 32);
+    if (k + 1 < 2 * N) {
+      const uint64_t s = c[k + 1] + up;
+      h[k + 1] += (s < c[k + 1] ? 1u : 0u);
+      c[k + 1] = s;
+    }
+  }
+  reduce_once(r);
+  return r;
+#endif
+}
+
+__global__ void k_mb_fqmul_v(int variant, int iters, uint32_t* out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  Fq a = Fq::one(), b = Fq::one();
+  a.v[0] ^= t;
+  b.v[1] ^= t * 7u + 1;
+  if (variant == 1)
+    for (int i = 0; i < iters; i++) a = mul_ilp2(a, b);
+  else
+    for (int i = 0; i < iters; i++) a = mul_cols(a, b);
+  store_f<Fq>(out + 12 * (size_t)t, a);
+}
+
+__global__ void k_mb_dbl(int iters, uint32_t* out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  G1A g = {Fq::from_limbs(params::G1_GEN_X), Fq::from_limbs(params::G1_GEN_Y)};
+  Xyzz<Fq> acc = dbl_affine(g);
+  acc.X.v[0] ^= (t & 1);
+  for (int i = 0; i < iters; i++) acc = dbl(acc);
+  store_f<Fq>(out + 12 * (size_t)t, acc.X);
+}
+
 __global__ void k_mb_madd(int iters, uint32_t* out) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   G1A g = {Fq::from_limbs(params::G1_GEN_X), Fq::from_limbs(params::G1_GEN_Y)};
@@ -162,6 +290,10 @@ extern "C" int tpst_microbench(tpst_ctx* ctx, int kind, size_t threads, int iter
     k_mb_madd<<<grid, bs, 0, ctx->stream>>>(iters, d);
   else if (kind == 2)
     k_mb_inv<<<grid, bs, 0, ctx->stream>>>(iters, d);
+  else if (kind == 3 || kind == 4)
+    k_mb_fqmul_v<<<grid, bs, 0, ctx->stream>>>(kind - 2, iters, d);
+  else if (kind == 5)
+    k_mb_dbl<<<grid, bs, 0, ctx->stream>>>(iters, d);
   else if (kind >= 16 && kind < 16 + wave::N_OPS) {
     const int op = kind - 16;
     const size_t lds = (((wave::OP_LEN[op] + 3) & ~3u) + (size_t)(wave::N_CONSTS + 64 + 4 * 48) * wave::SLOT) * 4;

@@ -42,6 +42,66 @@ void fr_out(const Fr& a, uint64_t* c) {
   memcpy(c, r.v, 32);
 }
 
+// 64-bit-limb host Montgomery product (CIOS, unsigned __int128) on the same
+// bits as Fq (6 x u64 = 12 x u32, R = 2^384 either way): the transcript's
+// Poseidon permutations run ~17 per MIPP round on the host, between device
+// phases, so their multiplications sit on the open's critical path.
+struct HostP64 {
+  uint64_t p[6];
+  uint64_t inv;  // -p^-1 mod 2^64
+  HostP64() {
+    for (int i = 0; i < 6; i++) p[i] = (uint64_t)params::FQ_P[2 * i] | ((uint64_t)params::FQ_P[2 * i + 1] << 32);
+    uint64_t x = 1;
+    for (int i = 0; i < 7; i++) x *= 2 - p[0] * x;  // Newton: x = p^-1 mod 2^64
+    inv = 0 - x;
+  }
+};
+const HostP64& hp64() {
+  static HostP64 h;
+  return h;
+}
+
+Fq hmul(const Fq& a, const Fq& b) {
+  typedef unsigned __int128 u128;
+  const HostP64& P = hp64();
+  uint64_t x[6], y[6], t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  memcpy(x, a.v, 48);
+  memcpy(y, b.v, 48);
+  for (int i = 0; i < 6; i++) {
+    u128 c = 0;
+    for (int j = 0; j < 6; j++) {
+      c += (u128)x[j] * y[i] + t[j];
+      t[j] = (uint64_t)c;
+      c >>= 64;
+    }
+    c += t[6];
+    t[6] = (uint64_t)c;
+    t[7] = (uint64_t)(c >> 64);
+    const uint64_t m = t[0] * P.inv;
+    c = ((u128)m * P.p[0] + t[0]) >> 64;
+    for (int j = 1; j < 6; j++) {
+      c += (u128)m * P.p[j] + t[j];
+      t[j - 1] = (uint64_t)c;
+      c >>= 64;
+    }
+    c += t[6];
+    t[5] = (uint64_t)c;
+    t[6] = t[7] + (uint64_t)(c >> 64);
+  }
+  // t < 2p: one conditional subtraction
+  uint64_t r[6];
+  u128 br = 0;
+  for (int j = 0; j < 6; j++) {
+    const u128 d = (u128)t[j] - P.p[j] - (uint64_t)br;
+    r[j] = (uint64_t)d;
+    br = (d >> 64) & 1;
+  }
+  const bool ge = t[6] || !br;
+  Fq out;
+  memcpy(out.v, ge ? r : t, 48);
+  return out;
+}
+
 // ------------------------------------------------------------ Poseidon ----
 struct PoseidonParams {
   Fq ark[39][3];
@@ -80,12 +140,12 @@ struct Sponge {
       for (int i = 0; i < 3; i++) st[i] = add(st[i], P.ark[r][i]);
       const bool full = r < 4 || r >= 35;
       for (int i = 0; i < (full ? 3 : 1); i++) {
-        const Fq x = st[i], x2 = sqr(x), x4 = sqr(x2), x8 = sqr(x4), x16 = sqr(x8);
-        st[i] = mul(x16, x);
+        const Fq x = st[i], x2 = hmul(x, x), x4 = hmul(x2, x2), x8 = hmul(x4, x4), x16 = hmul(x8, x8);
+        st[i] = hmul(x16, x);
       }
       Fq ns[3];
       for (int i = 0; i < 3; i++)
-        ns[i] = add(add(mul(P.mds[i][0], st[0]), mul(P.mds[i][1], st[1])), mul(P.mds[i][2], st[2]));
+        ns[i] = add(add(hmul(P.mds[i][0], st[0]), hmul(P.mds[i][1], st[1])), hmul(P.mds[i][2], st[2]));
       for (int i = 0; i < 3; i++) st[i] = ns[i];
     }
   }
