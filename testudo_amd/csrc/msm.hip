@@ -281,6 +281,67 @@ __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
   store_xyzz(buckets, key, acc);
 }
 
+// Short-chunk accumulation for the variable-base MSM (32-entry chunks over
+// ~64-entry buckets): no in-workgroup owner walk (it costs registers and a
+// barrier that the short chunks do not amortise); every piece of a bucket
+// that crosses a chunk boundary is parked -- the chunk's trailing piece in
+// part[2t + 1], its leading piece in part[2t] -- and k_bucket_fixup_short
+// sums them per bucket.
+template <class F>
+__global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
+    k_bucket_acc_short(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals, size_t m,
+                       uint32_t sent, const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend,
+                       const uint32_t* __restrict__ bases, const uint32_t* __restrict__ phib, uint32_t nbase,
+                       int lg, Xyzz<F>* __restrict__ buckets, Xyzz<F>* __restrict__ part) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t c0 = t << lg;
+  if (c0 >= m) return;
+  const size_t c1 = (c0 + ((size_t)1 << lg) < m) ? c0 + ((size_t)1 << lg) : m;
+  uint32_t key = keys[c0];
+  Affine<F> pt;
+  if (key < sent) pt = fetch_point<F>(bases, phib, nbase, vals[c0]);
+  Xyzz<F> acc = Xyzz<F>::inf();
+  for (size_t e = c0; e < c1; e++) {
+    uint32_t key_n = sent;
+    Affine<F> pt_n;
+    if (e + 1 < c1) {
+      key_n = keys[e + 1];
+      if (key_n < sent) pt_n = fetch_point<F>(bases, phib, nbase, vals[e + 1]);
+    }
+    if (key < sent) {
+      acc = add_affine(acc, pt);
+      if (key_n != key) {
+        const bool starts = bstart[key] >= c0;
+        const bool ends = bend[key] <= c1;
+        if (starts && ends)
+          store_xyzz(buckets, key, acc);
+        else
+          store_xyzz(part, 2 * t + (starts ? 1 : 0), acc);
+        acc = Xyzz<F>::inf();
+      }
+    }
+    key = key_n;
+    pt = pt_n;
+  }
+}
+
+// buckets crossing chunk boundaries: trailing piece of the first chunk plus
+// the leading pieces of the following ones
+template <class F>
+__global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
+    k_bucket_fixup_short(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend, size_t nbk, int lg,
+                         const Xyzz<F>* __restrict__ part, Xyzz<F>* __restrict__ buckets) {
+  const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nbk) return;
+  const uint32_t s = bstart[b], e = bend[b];
+  if (e <= s) return;
+  const size_t t0 = (size_t)s >> lg, t1 = (size_t)(e - 1) >> lg;
+  if (t0 == t1) return;
+  Xyzz<F> acc = load_xyzz(part, 2 * t0 + 1);
+  for (size_t t = t0 + 1; t <= t1; t++) acc = add(acc, load_xyzz(part, 2 * t));
+  store_xyzz(buckets, b, acc);
+}
+
 // segment t of group g: sum_{b in seg} (b+1) * S_b with b the bucket index
 // inside the group (bucket b holds digit value b+1)
 template <class F>
@@ -333,6 +394,55 @@ __global__ void __launch_bounds__(64, 1) k_window_combine(const Xyzz<F>* __restr
     acc = add(acc, load_xyzz(win, w));
   }
   store_xyzz(out, 0, acc);
+}
+
+// ---- cooperative XYZZ doubling (G1): lanes 0..2 of one wave each take one
+// Fq product of every level of dbl-2008-s-1 (4 product levels instead of 9
+// serial products; each product is broadcast from its lane with v_readlane).  The Horner
+// combination of the window sums is a chain of 16 (W - 1) doublings, so its
+// latency is the doubling's latency.
+__device__ __forceinline__ Fq shfl_fq(const Fq& v, int src) {  // lane src's value, wave-uniform (SGPRs)
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.v[i] = (uint32_t)__builtin_amdgcn_readlane((int)v.v[i], src);
+  return r;
+}
+
+__device__ __forceinline__ Xyzz<Fq> dbl_coop(const Xyzz<Fq>& p, int lane) {
+  if (is_zero(p.ZZ)) return p;  // uniform: every lane holds p
+  const Fq U = dbl(p.Y);
+  // level 1: V = U^2 (lane 0), XX = X^2 (lane 1)
+  Fq r = mul(lane == 0 ? U : p.X, lane == 0 ? U : p.X);
+  const Fq V = shfl_fq(r, 0), XX = shfl_fq(r, 1);
+  const Fq M = mul3(XX);
+  // level 2: W = U V (0), S = X V (1), ZZ' = V ZZ (2)
+  r = mul(lane == 0 ? U : lane == 1 ? p.X : p.ZZ, V);
+  const Fq W = shfl_fq(r, 0), S = shfl_fq(r, 1), ZZ3 = shfl_fq(r, 2);
+  // level 3: M^2 (0), W Y (1), ZZZ' = W ZZZ (2)
+  r = mul(lane == 0 ? M : W, lane == 0 ? M : lane == 1 ? p.Y : p.ZZZ);
+  const Fq MM = shfl_fq(r, 0), WY = shfl_fq(r, 1), ZZZ3 = shfl_fq(r, 2);
+  Xyzz<Fq> q;
+  q.X = sub(MM, dbl(S));
+  // level 4: M (S - X')
+  r = mul(M, sub(S, q.X));
+  q.Y = sub(shfl_fq(r, 0), WY);
+  q.ZZ = ZZ3;
+  q.ZZZ = ZZZ3;
+  return q;
+}
+
+// Horner over windows on one wave (lanes 0..63 run the same chain; lanes 0..2
+// carry its products): sum_w 2^(c w) G_w
+static __global__ void __launch_bounds__(64, 1) k_window_combine_coop(const Xyzz<Fq>* __restrict__ win, int W, int c,
+                                                               Xyzz<Fq>* __restrict__ out) {
+  if (blockIdx.x != 0) return;
+  const int lane = threadIdx.x;
+  Xyzz<Fq> acc = load_xyzz(win, W - 1);
+  for (int w = W - 2; w >= 0; w--) {
+    for (int i = 0; i < c; i++) acc = dbl_coop(acc, lane);
+    acc = add(acc, load_xyzz(win, w));
+  }
+  if (lane == 0) store_xyzz(out, 0, acc);
 }
 
 template <class F>
@@ -451,10 +561,11 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   TPST_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                               (uint32_t*)nullptr, (uint32_t*)nullptr, (int)m, 0, end_bit, s));
   const int lg = acc_chunk_lg(m);
+  const bool short_chunks = lg == 5;  // K2 at every size up to ~2^24 points
   const size_t nchunk = (m + ((size_t)1 << lg) - 1) >> lg;
   const size_t nblk = (nchunk + ACC_BLOCK - 1) / ACC_BLOCK;
   size_t need = Arena::need(m, 4) * 4 + Arena::need(nbk, 4) * 2 + Arena::need(nbk, sizeof(Xyzz<F>)) +
-                Arena::need(nchunk, sizeof(Xyzz<F>)) + Arena::need(nblk, sizeof(Xyzz<F>)) +
+                Arena::need(2 * nchunk, sizeof(Xyzz<F>)) + Arena::need(nblk, sizeof(Xyzz<F>)) +
                 reduce_scratch<F>(W, nb) +
                 Arena::need(W, sizeof(Xyzz<F>)) + Arena::need(glv ? n * 24 : 1, 4) + Arena::need(sort_bytes, 1) +
                 8192;
@@ -467,7 +578,7 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   uint32_t* bstart = ar.take<uint32_t>(nbk);
   uint32_t* bend = ar.take<uint32_t>(nbk);
   Xyzz<F>* buckets = ar.take<Xyzz<F>>(nbk);
-  Xyzz<F>* part = ar.take<Xyzz<F>>(nchunk);
+  Xyzz<F>* part = ar.take<Xyzz<F>>(2 * nchunk);
   Xyzz<F>* bpart = ar.take<Xyzz<F>>(nblk);
   Xyzz<F>* win = ar.take<Xyzz<F>>(W);
   uint32_t* phib = ar.take<uint32_t>(glv ? n * 24 : 1);
@@ -495,17 +606,28 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   TPST_TRY(hipGetLastError());
   pf->end(ST_BOUNDS, s);
   pf->begin(ST_BUCKET_ACC, s);
-  k_bucket_acc_chunk<F><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys2, vals2, m, sent, bstart, bend, d_bases, phib,
-                                                              (uint32_t)n, lg, buckets, part, bpart);
-  TPST_TRY(hipGetLastError());
-  k_bucket_fixup<F><<<grid_for(nblk, 64), 64, 0, s>>>(keys2, m, sent, bstart, bend, lg, nblk, part, bpart, buckets);
+  if (short_chunks) {
+    k_bucket_acc_short<F><<<grid_for(nchunk, 64), 64, 0, s>>>(keys2, vals2, m, sent, bstart, bend, d_bases, phib,
+                                                               (uint32_t)n, lg, buckets, part);
+    TPST_TRY(hipGetLastError());
+    k_bucket_fixup_short<F><<<grid_for(nbk, 64), 64, 0, s>>>(bstart, bend, nbk, lg, part, buckets);
+  } else {
+    k_bucket_acc_chunk<F><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys2, vals2, m, sent, bstart, bend, d_bases, phib,
+                                                                (uint32_t)n, lg, buckets, part, bpart);
+    TPST_TRY(hipGetLastError());
+    k_bucket_fixup<F><<<grid_for(nblk, 64), 64, 0, s>>>(keys2, m, sent, bstart, bend, lg, nblk, part, bpart,
+                                                        buckets);
+  }
   TPST_TRY(hipGetLastError());
   pf->end(ST_BUCKET_ACC, s);
   pf->begin(ST_REDUCE, s);
   TPST_TRY(reduce_buckets<F>(ar, s, buckets, W, nb, win));
   pf->end(ST_REDUCE, s);
   pf->begin(ST_COMBINE, s);
-  k_window_combine<F><<<1, 64, 0, s>>>(win, W, c, d_out);
+  if constexpr (sizeof(F) == sizeof(Fq))
+    k_window_combine_coop<<<1, 64, 0, s>>>(win, W, c, d_out);
+  else
+    k_window_combine<F><<<1, 64, 0, s>>>(win, W, c, d_out);
   TPST_TRY(hipGetLastError());
   pf->end(ST_COMBINE, s);
   return hipSuccess;
