@@ -20,7 +20,7 @@ and the Miller loops of their IPP pairs, one RCCL all-gather moves [row
 commitments | Miller partial], rank 0 runs the final exponentiation and the
 (transcript-sequential) open.
 
-roofline: the dominant kernel is bucket accumulation (k_bucket_acc_chunk +
+roofline: the dominant kernel is bucket accumulation (k_bucket_acc_short +
 its fixup); its duration is measured with HIP events on the library's own
 stream over the timed region (tpst_profile_*).  Algorithmic bytes per MSM =
 128 B per scalar-point pair (32 B Fr + 96 B affine G1).  The
@@ -51,7 +51,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
 VALU_PEAK_WAVE_INSTS = 256 * 4 * 0.5 * 2.4e9  # CUs x SIMDs x (1 wave-instr / 2 cycles) x 2.4 GHz
 BYTES_PER_PAIR = 128           # 32 B scalar + 96 B affine base
 SEED = 0x7E57D0
-PMC_FILE = os.path.join(ROOT, "profiles", "r02", "pmc_bucket_acc_chunk.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r02", "pmc_bucket_acc_short.json")
 
 
 def parse():
@@ -250,7 +250,7 @@ def main():
     windows = 8  # GLV: two 127-bit halves, 8 signed 16-bit windows each
     madds = 2 * n * windows
     achieved_fqmul = madds * fq_mults_per_madd() / (acc_avg_ms * 1e-3)
-    compute = {"bound": "valu-int32", "kernel": "k_bucket_acc_chunk<Fq>",
+    compute = {"bound": "valu-int32", "kernel": "k_bucket_acc_short<Fq>",
                "achieved_fq_mul_per_s": achieved_fqmul, "peak_fq_mul_per_s_measured": peak_fqmul,
                "frac": round(achieved_fqmul / peak_fqmul, 4),
                "fq_mul_per_madd": fq_mults_per_madd()}
@@ -282,7 +282,7 @@ def main():
         "roofline": {"bound": "valu-int32", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                      "traffic_source": (os.path.relpath(PMC_FILE, ROOT) if pmc else None),
-                     "kernel": "k_bucket_acc_chunk<Fq> (+ k_bucket_fixup)", "alg_bytes_per_launch": alg_bytes,
+                     "kernel": "k_bucket_acc_short<Fq> (+ k_bucket_fixup_short)", "alg_bytes_per_launch": alg_bytes,
                      "kernel_avg_ms": round(acc_avg_ms, 4),
                      "note": "HBM column secondary: the kernel is bound by 32-bit integer VALU issue"},
         "compute": compute,

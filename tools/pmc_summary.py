@@ -14,7 +14,7 @@ import sys
 from collections import defaultdict
 
 
-def load(d, counter, match="k_bucket_acc_chunk"):
+def load(d, counter, match="k_bucket_acc_short"):
     vals = defaultdict(list)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
@@ -32,7 +32,7 @@ def main():
     avg = lambda v: sum(v) / len(v)  # noqa: E731
     f_kb, w_kb = avg(fetch[grid]), avg(write.get(grid, [0.0]))
     res = {
-        "kernel": "k_bucket_acc_chunk<Fq> (bench: 2^20-point G1 MSM, GLV, c = 16)",
+        "kernel": "k_bucket_acc_short<Fq> (bench: 2^20-point G1 MSM, GLV, c = 16)",
         "grid": grid, "launches": {"fetch": len(fetch[grid]), "write": len(write.get(grid, [])),
                                    "valu": len(valu.get(grid, []))},
         "fetch_size_kb_per_launch": f_kb, "write_size_kb_per_launch": w_kb,
