@@ -55,6 +55,15 @@ extern "C" void tpst_destroy(tpst_ctx* ctx) {
   ctx->arena.release();
   ctx->io.release();
   ctx->arena2.release();
+  for (int i = 0; i < 3; i++) {
+    if (ctx->side[i]) {
+      (void)hipStreamSynchronize(ctx->side[i]);
+      (void)hipStreamDestroy(ctx->side[i]);
+    }
+    ctx->arena_side[i].release();
+  }
+  for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
+  if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   tpst_release_pst_state(ctx);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <mutex>
 #include <string>
+#include <vector>
 #include "msm.h"
 #include "pairing_kernels.h"
 
@@ -15,6 +16,13 @@ struct tpst_ctx {
   tpst::Arena io;      // staging for host-pointer entry points
   tpst::Arena arena2;  // scratch for nested primitives (open / MIPP)
   tpst::Profiler prof; // stage timing (tpst_profile_*)
+  // the opening runs four streams concurrently (pst_api.hip tpst_poly_open):
+  // `stream` + side[0..2], each with its own scratch arena; created on first use
+  hipStream_t side[3] = {nullptr, nullptr, nullptr};
+  tpst::Arena arena_side[3];
+  std::vector<hipEvent_t> events;  // timing-free event pool of the opening
+  void* pinned = nullptr;          // pinned host staging of the opening
+  size_t pinned_cap = 0;
 };
 
 void tpst_release_pst_state(tpst_ctx* ctx);

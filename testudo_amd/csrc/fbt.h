@@ -33,11 +33,14 @@ hipError_t fbt_build(Arena& ar, hipStream_t s, const uint32_t* d_bases, size_t n
 //            g < L / D, m < (n / L) D   -- MIPP folds (D = 1) and cross
 //            products (D = L / 2), a plain MSM is L = D = n;
 //   segments (d_seg != nullptr): k = seg[g] + m, m < seg[g+1] - seg[g].
+// sets > 1: the same groups again for each of `sets` scalar vectors (set q
+// reads S at d_scalars + 8 q set_stride), out[q groups + g].
 struct FbGroups {
   size_t groups = 1;
   size_t members = 0;  // per group (max over groups for segments)
   size_t L = 1, D = 1;
   const uint32_t* d_seg = nullptr;
+  size_t sets = 1, set_stride = 0;
 };
 
 template <class F>

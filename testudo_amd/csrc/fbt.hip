@@ -70,9 +70,11 @@ __global__ void __launch_bounds__(64) k_fbt_partial(const uint32_t* __restrict__
                                                     const uint32_t* __restrict__ scal, FbGroups gr,
                                                     Xyzz<F>* __restrict__ partial) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= gr.groups * gr.members * 8) return;
+  if (i >= gr.sets * gr.groups * gr.members * 8) return;
   const int ch = (int)(i & 7);
-  const size_t gm = i >> 3, g = gm / gr.members, m = gm % gr.members;
+  const size_t per_set = gr.groups * gr.members;
+  const size_t qgm = i >> 3, q = qgm / per_set, gm = qgm % per_set;
+  const size_t g = gm / gr.members, m = gm % gr.members;
   size_t k;
   bool valid = true;
   if (gr.d_seg) {
@@ -85,7 +87,7 @@ __global__ void __launch_bounds__(64) k_fbt_partial(const uint32_t* __restrict__
   Xyzz<F> acc = Xyzz<F>::inf();
   if (valid) {
     uint32_t s[8];
-    const uint4* sp = reinterpret_cast<const uint4*>(scal + 8 * k);
+    const uint4* sp = reinterpret_cast<const uint4*>(scal + 8 * (k + q * gr.set_stride));
     const uint4 a = sp[0], b = sp[1];
     s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w;
     s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
@@ -125,27 +127,28 @@ __global__ void __launch_bounds__(BS) k_seg_sum(const Xyzz<F>* __restrict__ in, 
 template <class F>
 hipError_t fbt_msm(Arena& ar, hipStream_t s, const uint32_t* d_table, const uint32_t* d_scalars, const FbGroups& g,
                    Xyzz<F>* d_out) {
-  if (!g.groups) return hipSuccess;
+  if (!g.groups || !g.sets) return hipSuccess;
   constexpr int BS = sizeof(F) > 48 ? 64 : 128;
   constexpr size_t R = 4;
+  const size_t G = g.groups * g.sets;
   size_t len = g.members * 8;
-  const size_t np = g.groups * (len ? len : 1);
+  const size_t np = G * (len ? len : 1);
   ar.reset();
   TPST_TRY(ar.reserve(2 * Arena::need(np, sizeof(Xyzz<F>))));
   Xyzz<F>* a = ar.take<Xyzz<F>>(np);
   Xyzz<F>* b = ar.take<Xyzz<F>>(np);
   if (!len) {
     len = 1;
-    TPST_TRY(hipMemsetAsync(a, 0, g.groups * sizeof(Xyzz<F>), s));
+    TPST_TRY(hipMemsetAsync(a, 0, G * sizeof(Xyzz<F>), s));
   } else {
-    k_fbt_partial<F><<<fbt_grid(g.groups * len, 64), 64, 0, s>>>(d_table, d_scalars, g, a);
+    k_fbt_partial<F><<<fbt_grid(G * len, 64), 64, 0, s>>>(d_table, d_scalars, g, a);
     TPST_TRY(hipGetLastError());
   }
   while (len > 1) {
     const size_t per = BS * R;
     const size_t parts = (len + per - 1) / per;
     Xyzz<F>* dst = parts == 1 ? d_out : b;
-    k_seg_sum<F, BS><<<(unsigned)(g.groups * parts), BS, 0, s>>>(a, len, per, parts, dst);
+    k_seg_sum<F, BS><<<(unsigned)(G * parts), BS, 0, s>>>(a, len, per, parts, dst);
     TPST_TRY(hipGetLastError());
     if (parts == 1) return hipSuccess;
     len = parts;
@@ -153,7 +156,7 @@ hipError_t fbt_msm(Arena& ar, hipStream_t s, const uint32_t* d_table, const uint
     a = b;
     b = t;
   }
-  return hipMemcpyAsync(d_out, a, g.groups * sizeof(Xyzz<F>), hipMemcpyDeviceToDevice, s);
+  return hipMemcpyAsync(d_out, a, G * sizeof(Xyzz<F>), hipMemcpyDeviceToDevice, s);
 }
 
 template hipError_t fbt_build<Fq>(Arena&, hipStream_t, const uint32_t*, size_t, uint32_t*);

@@ -20,6 +20,51 @@ __global__ void k_mb_fqmul(int iters, uint32_t* out) {
   store_f<Fq>(out + 12 * (size_t)t, a);
 }
 
+// ---- single-instruction issue rates: 8 independent chains per lane -------
+// kind 6: v_mad_u64_u32, 7: v_mad_u32_u24, 8: v_mul_lo_u32, 9: v_add_u32,
+// 10: v_fma_f64, 11: v_mul_hi_u32 (iters x 4 x 8 instructions per lane)
+template <int K>
+__global__ void k_mb_insn(int iters, uint32_t* out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t a64[8];
+  uint32_t a32[8];
+  double f[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    a64[j] = t * 13u + j;
+    a32[j] = t * 7u + j;
+    f[j] = (double)(t + j);
+  }
+  const uint32_t x = t | 1u, y = t * 3u + 5u;
+  const double fx = 1.0000001, fy = 1e-9;
+  for (int i = 0; i < iters; i++) {
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        if constexpr (K == 6) {
+          uint64_t c;
+          asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(a64[j]), "=&s"(c) : "v"(x), "v"(y));
+        } else if constexpr (K == 7) {
+          asm volatile("v_mad_u32_u24 %0, %1, %2, %0" : "+v"(a32[j]) : "v"(x), "v"(y));
+        } else if constexpr (K == 8) {
+          asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a32[j]) : "v"(x));
+        } else if constexpr (K == 9) {
+          asm volatile("v_add_u32 %0, %0, %1" : "+v"(a32[j]) : "v"(x));
+        } else if constexpr (K == 10) {
+          asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(f[j]) : "v"(fx), "v"(fy));
+        } else {
+          asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a32[j]) : "v"(x));
+        }
+      }
+    }
+  }
+  uint32_t r = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) r ^= (uint32_t)a64[j] ^ a32[j] ^ (uint32_t)f[j];
+  out[t] = r;
+}
+
 // ---- A/B variants of the device Montgomery product (latency experiments) --
 // ILP2: product scanning with the terms of every column split over two
 // independent (acc, hi) chains, merged when the column completes.
@@ -294,6 +339,18 @@ extern "C" int tpst_microbench(tpst_ctx* ctx, int kind, size_t threads, int iter
     k_mb_fqmul_v<<<grid, bs, 0, ctx->stream>>>(kind - 2, iters, d);
   else if (kind == 5)
     k_mb_dbl<<<grid, bs, 0, ctx->stream>>>(iters, d);
+  else if (kind == 6)
+    k_mb_insn<6><<<grid, bs, 0, ctx->stream>>>(iters, d);
+  else if (kind == 7)
+    k_mb_insn<7><<<grid, bs, 0, ctx->stream>>>(iters, d);
+  else if (kind == 8)
+    k_mb_insn<8><<<grid, bs, 0, ctx->stream>>>(iters, d);
+  else if (kind == 9)
+    k_mb_insn<9><<<grid, bs, 0, ctx->stream>>>(iters, d);
+  else if (kind == 10)
+    k_mb_insn<10><<<grid, bs, 0, ctx->stream>>>(iters, d);
+  else if (kind == 11)
+    k_mb_insn<11><<<grid, bs, 0, ctx->stream>>>(iters, d);
   else if (kind >= 16 && kind < 16 + wave::N_OPS) {
     const int op = kind - 16;
     const size_t lds = (((wave::OP_LEN[op] + 3) & ~3u) + (size_t)(wave::N_CONSTS + 64 + 4 * 48) * wave::SLOT) * 4;

@@ -92,10 +92,12 @@ constexpr int MW_PROG = MW_SET.words;
 constexpr size_t MW_LDS = (size_t)(MW_PROG + MW * MW_SLOTS * wave::SLOT) * 4;
 static_assert(MW_LDS <= 65536, "Miller kernel LDS");
 
+// map_s != 0: MIPP pair order (multi_pairing_prepared, pairing_kernels.h) -- pair
+// pi = g n + k of group g reads G1 / G2 / line column j(g, k); else j = pi
 __global__ void __launch_bounds__(64 * MW) k_miller_wave(const uint32_t* __restrict__ g1,
                                                          const uint32_t* __restrict__ g2,
                                                          const LineCoeff* __restrict__ coeffs, size_t np,
-                                                         Fq12* __restrict__ partial) {
+                                                         Fq12* __restrict__ partial, size_t n_per, size_t map_s) {
   extern __shared__ uint4 smem4[];
   wave::lds_t* prog = (wave::lds_t*)(smem4);
   wave::lds_t* vals = prog + MW_PROG;
@@ -104,8 +106,13 @@ __global__ void __launch_bounds__(64 * MW) k_miller_wave(const uint32_t* __restr
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const size_t pi = (size_t)blockIdx.x * MW + w;
   if (pi >= np) return;
-  const G1A p = load_affine<Fq>(g1, pi);
-  const G2A q = load_affine<Fq2>(g2, pi);
+  size_t j = pi;
+  if (map_s) {
+    const size_t g = pi / n_per, k = pi % n_per;
+    j = (k / map_s) * 2 * map_s + (g == 0 ? map_s : 0) + k % map_s;
+  }
+  const G1A p = load_affine<Fq>(g1, j);
+  const G2A q = load_affine<Fq2>(g2, j);
   if (is_inf(p) || is_inf(q)) {
     if (lane < 12) reinterpret_cast<Fq*>(partial + pi)[lane] = lane == 0 ? Fq::one() : Fq::zero();
     return;
@@ -121,14 +128,14 @@ __global__ void __launch_bounds__(64 * MW) k_miller_wave(const uint32_t* __restr
   // lanes 0..5: line idx, lanes 6..11: line idx + 1 (addition step)
   int idx = 0;
   Fq pre = Fq::zero();
-  if (lane < 12) pre = cf[((size_t)(idx + (lane >= 6)) * np + pi) * 6 + lane % 6];
+  if (lane < 12) pre = cf[((size_t)(idx + (lane >= 6)) * np + j) * 6 + lane % 6];
   for (int b = X_BITS - 2; b >= 0; b--) {
     const bool add = (params::BLS_X >> b) & 1;
     if (lane < 6 || (add && lane < 12)) wave::put_slot(vals, B + (lane < 6 ? lane : lane + 2), pre);
     const int nidx = idx + (add ? 2 : 1);
     if (b > 0 && lane < 12) {
       const bool nadd = (params::BLS_X >> (b - 1)) & 1;
-      if (lane < 6 || nadd) pre = cf[((size_t)(nidx + (lane >= 6)) * np + pi) * 6 + lane % 6];
+      if (lane < 6 || nadd) pre = cf[((size_t)(nidx + (lane >= 6)) * np + j) * 6 + lane % 6];
     }
     wave::wave_sync();
     if (add)
@@ -329,12 +336,13 @@ size_t multi_pairing_scratch(size_t groups, size_t n) {
 }
 
 hipError_t multi_pairing_prepared(Arena& ar, hipStream_t s, const uint32_t* d_g1, const uint32_t* d_g2,
-                                  const LineCoeff* d_coeffs, size_t groups, size_t n, Fq12* d_out, bool final_exp) {
+                                  const LineCoeff* d_coeffs, size_t groups, size_t n, Fq12* d_out, bool final_exp,
+                                  size_t map_s) {
   if (!groups) return hipSuccess;
   const size_t np = groups * n;
   Fq12* partial = ar.take<Fq12>(np ? np : 1);
   if (np) {
-    k_miller_wave<<<grid_for(np, MW), 64 * MW, MW_LDS, s>>>(d_g1, d_g2, d_coeffs, np, partial);
+    k_miller_wave<<<grid_for(np, MW), 64 * MW, MW_LDS, s>>>(d_g1, d_g2, d_coeffs, np, partial, n, map_s);
     TPST_TRY(hipGetLastError());
     TPST_TRY(tree_partials(ar, s, partial, groups, n));
   }

@@ -19,9 +19,14 @@ hipError_t g2_prepare_batch(hipStream_t s, const uint32_t* d_g2, size_t n, LineC
 // final_exp = false: the Miller-loop product of each group only (unreduced GT
 // partial of a row-sharded IPP, finished by gt_product_final).  Scratch from
 // `ar`: multi_pairing_scratch(groups, n) bytes.
+// map_s != 0 (MIPP cross pairings, groups = 2, n = H map_s with H in {1, 2}):
+// pair k of group g uses column j = (k / map_s) 2 map_s + (g ? 0 : map_s) +
+// k % map_s of d_g1 / d_g2 / d_coeffs (row length groups * n), i.e. group 0
+// pairs the upper half of every 2 map_s block of prepared G2 points, group 1
+// the lower half -- t_l / t_r of mipp.rs:87-94 against an unswapped h.
 hipError_t multi_pairing_prepared(Arena& ar, hipStream_t s, const uint32_t* d_g1, const uint32_t* d_g2,
                                   const LineCoeff* d_coeffs, size_t groups, size_t n, Fq12* d_out,
-                                  bool final_exp = true);
+                                  bool final_exp = true, size_t map_s = 0);
 size_t multi_pairing_scratch(size_t groups, size_t n);
 
 // groups x n Montgomery Fq12 partials -> groups final-exponentiated products

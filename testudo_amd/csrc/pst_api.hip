@@ -934,32 +934,84 @@ static int srs_fbt(tpst_ctx* ctx, SrsState* st, int odd) {
 // PST open of 2^k evals (Montgomery) at k Montgomery
 // scalars d_pt over the pair levels off..off+k-1: the k quotient scalar
 // vectors first (cheap Fr recurrence), then ONE grouped table MSM with a
-// group per level.  Writes k XYZZ points.
+// group per level.  Writes k XYZZ points.  Stream-ordered on `s` with the
+// caller's scratch (pst_open_scratch_words u32), so it can run beside the MIPP.
+static size_t pst_open_scratch_words(const SrsState* st, int k) {
+  return ((size_t)2 << k) * 8 + st->lvl_off[st->nv] * 8;
+}
+
 template <class F>
-static int pst_open_fbt(tpst_ctx* ctx, SrsState* st, const uint32_t* table, int off, const uint32_t* d_evals, int k,
-                        const uint32_t* d_pt, Xyzz<F>* d_out) {
-  hipStream_t s = ctx->stream;
-  DevBuf r0, r1, sc;
+static hipError_t pst_open_fbt_s(hipStream_t s, Arena& ar, const SrsState* st, const uint32_t* table, int off,
+                                 const uint32_t* d_evals, int k, const uint32_t* d_pt, Xyzz<F>* d_out,
+                                 uint32_t* scratch) {
   const size_t full = (size_t)1 << k;
-  TPST_HIP(ctx, r0.alloc(full * 32));
-  TPST_HIP(ctx, r1.alloc(full * 32));
-  TPST_HIP(ctx, sc.alloc(st->lvl_off[st->nv] * 32));
-  TPST_HIP(ctx, hipMemcpyAsync(r0.p, d_evals, full * 32, hipMemcpyDeviceToDevice, s));
-  uint32_t* cur = r0.u();
-  uint32_t* nxt = r1.u();
+  uint32_t* cur = scratch;
+  uint32_t* nxt = scratch + full * 8;
+  uint32_t* sc = scratch + 2 * full * 8;
+  hipError_t e = hipMemcpyAsync(cur, d_evals, full * 32, hipMemcpyDeviceToDevice, s);
+  if (e != hipSuccess) return e;
   for (int i = 0; i < k; i++) {
     const size_t half = (size_t)1 << (k - i - 1);
-    TPST_HIP(ctx, pst_step(s, cur, half, d_pt + 8 * i, sc.u() + 8 * st->lvl_off[off + i], nxt));
+    e = pst_step(s, cur, half, d_pt + 8 * i, sc + 8 * st->lvl_off[off + i], nxt);
+    if (e != hipSuccess) return e;
     std::swap(cur, nxt);
   }
   FbGroups g;
   g.groups = k;
   g.members = (size_t)1 << (k - 1);
   g.d_seg = st->seg.u() + off;
-  TPST_HIP(ctx, fbt_msm<F>(ctx->arena, s, table, sc.u(), g, d_out));
+  return fbt_msm<F>(ar, s, table, sc, g, d_out);
+}
+
+template <class F>
+static int pst_open_fbt(tpst_ctx* ctx, SrsState* st, const uint32_t* table, int off, const uint32_t* d_evals, int k,
+                        const uint32_t* d_pt, Xyzz<F>* d_out) {
+  DevBuf scratch;
+  TPST_HIP(ctx, scratch.alloc(pst_open_scratch_words(st, k) * 4));
+  TPST_HIP(ctx, pst_open_fbt_s<F>(ctx->stream, ctx->arena, st, table, off, d_evals, k, d_pt, d_out, scratch.u()));
   return TPST_OK;
 }
 
+// ---------------------------------------------------------------- open ----
+// Streams of the opening (created once per context) and a pool of events.
+static int open_streams(tpst_ctx* ctx, size_t n_events, size_t pinned_bytes) {
+  for (int i = 0; i < 3; i++)
+    if (!ctx->side[i]) TPST_HIP(ctx, hipStreamCreateWithFlags(&ctx->side[i], hipStreamNonBlocking));
+  while (ctx->events.size() < n_events) {
+    hipEvent_t e;
+    TPST_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ctx->events.push_back(e);
+  }
+  if (ctx->pinned_cap < pinned_bytes) {
+    if (ctx->pinned) TPST_HIP(ctx, hipHostFree(ctx->pinned));
+    ctx->pinned = nullptr;
+    ctx->pinned_cap = 0;
+    TPST_HIP(ctx, hipHostMalloc(&ctx->pinned, pinned_bytes, hipHostMallocDefault));
+    ctx->pinned_cap = pinned_bytes;
+  }
+  return TPST_OK;
+}
+
+// Polynomial::open (sqrt_pst.rs:168-230) with MippProof::prove (mipp.rs:31-153).
+//
+// Critical path = the transcript: each MIPP round's challenge needs that
+// round's comms_u and comms_t, and the next round's folds need the challenge.
+// Per round r (len = C >> r, s = len / 2) the work is spread over 4 streams:
+//   A (critical): a^(r) and c'a^(r) as ONE grouped table MSM over the original
+//     row commitments (two scalar sets W, c' W: a^(r)_i = sum_t W_t a_{i+t len},
+//     c' = the previous challenge inverse), then t_l, t_r against the PREVIOUS
+//     round's prepared h by bilinearity:
+//       e(a_i, h^(r)_k) = e(a_i, h^(r-1)_k) e(c' a_i, h^(r-1)_{k+len})
+//     -> Miller loops + the two final exponentiations; comms_t -> host.
+//   B: y fold (compress_field, mipp.rs:124-136) and the cross MSMs u_l, u_r
+//     (mipp.rs:66-75) -> canonical -> host.
+//   C: h^(r) = sum_t Wi_t h_{i + t len} (table MSM over powers_of_h) -> affine
+//     -> G2Prepared, consumed by round r+1 (so G2 preparation is off the
+//     critical path); in round 0 it builds the fold table over comm_list.
+//   D: U = MSM(comm_list, chi(b)) (sqrt_pst.rs:198) and the PST proof of q
+//     (sqrt_pst.rs:218-225), which needs nothing from the MIPP.
+// The host waits only for the round's comms (pinned staging), absorbs them
+// (mipp.rs:97-101) and squeezes the challenge; no stream is drained mid-open.
 extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, const uint64_t* comms,
                               const uint64_t* point, const uint64_t* T, tpst_open_proof* proof) {
   (void)T;  // the reference passes T but the prover does not use it (mipp.rs:38)
@@ -980,134 +1032,229 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     int rc = srs_fbt(ctx, st, p->odd);
     if (rc) return rc;
   }
-  hipStream_t s = ctx->stream;
   const int m = p->m_col;
+  const int k = p->m_row;
   const size_t C = (size_t)1 << m;
-  const size_t N = (size_t)1 << p->m_row;
   memset(proof, 0, sizeof *proof);
   proof->m_col = m;
-  proof->m_row = p->m_row;
+  proof->m_row = k;
   Sponge sp;
   sp.load(tr);
 
-  DevBuf A, Ar, Hr, H2, Y, Sc, dW, xa, xh, xy, gts, small, canon;
-  TPST_HIP(ctx, A.alloc(C * 96));
-  TPST_HIP(ctx, Ar.alloc(C * 96));
-  TPST_HIP(ctx, Hr.alloc(C * 192));
-  TPST_HIP(ctx, H2.alloc(C * 192));
-  TPST_HIP(ctx, Y.alloc(C * 32));
-  TPST_HIP(ctx, Sc.alloc(C * 32));
-  TPST_HIP(ctx, dW.alloc(C * 32));
-  TPST_HIP(ctx, xa.alloc(C * sizeof(Xyzz<Fq>)));
-  TPST_HIP(ctx, xh.alloc(C * sizeof(Xyzz<Fq2>)));
-  TPST_HIP(ctx, xy.alloc(4 * sizeof(Xyzz<Fq2>) + 64 * sizeof(Xyzz<Fq2>)));
-  TPST_HIP(ctx, gts.alloc(2 * sizeof(Fq12)));
-  TPST_HIP(ctx, small.alloc(256));
-  TPST_HIP(ctx, canon.alloc(4096));
-  // A = comms (Montgomery), tabulated for the folds; Y = chis
-  {
-    DevBuf up;
-    TPST_HIP(ctx, up.alloc(C * 96));
-    TPST_HIP(ctx, hipMemcpyAsync(up.p, comms, C * 96, hipMemcpyHostToDevice, s));
-    TPST_HIP(ctx, points_to_mont<Fq>(s, up.u(), A.u(), C));
-    if (st->t_A_n < C) {
-      TPST_HIP(ctx, st->t_A.alloc(fbt_words<Fq>(C) * 4));
-      st->t_A_n = C;
-    }
-    TPST_HIP(ctx, fbt_build<Fq>(ctx->arena, s, A.u(), C, st->t_A.u()));
-    TPST_HIP(ctx, hipStreamSynchronize(s));
+  // ---- host staging layout (bytes): per-round uploads, final upload, downloads
+  std::vector<size_t> up_off(m + 2);
+  size_t off = 0;
+  for (int r = 0; r < m; r++) {  // W | c'W | Wi | c' (Fr)
+    up_off[r] = off;
+    off += (3 * ((size_t)1 << r) + 1) * 32;
   }
-  TPST_HIP(ctx, hipMemcpyAsync(Y.p, p->chis.p, C * 32, hipMemcpyDeviceToDevice, s));
-  Xyzz<Fq>* x1 = (Xyzz<Fq>*)xy.p;
+  up_off[m] = off;  // final: W | Wi | evals | rs (Fr), a_rev (canonical Fr)
+  off += (3 * C + m + k) * 32;
+  const size_t up_bytes = off;
+  const size_t dn_U = up_bytes, dn_round = dn_U + 96, dn_final = dn_round + (size_t)m * (192 + 1152);
+  const size_t dn_bytes = 96 + (size_t)m * (192 + 1152) + 96 + 192 + (size_t)m * 96 + (size_t)k * 192;
+  const size_t n_ev = 8 + 4 * (size_t)m;
+  if (int rc = open_streams(ctx, n_ev, up_bytes + dn_bytes)) return rc;
+  uint8_t* pin = (uint8_t*)ctx->pinned;
+  hipStream_t sA = ctx->stream, sB = ctx->side[0], sC = ctx->side[1], sD = ctx->side[2];
+  Arena &arA = ctx->arena, &arB = ctx->arena_side[0], &arC = ctx->arena_side[1], &arD = ctx->arena_side[2];
+  hipEvent_t* ev = ctx->events.data();
+  enum { EV_PRE, EV_TABLE, EV_U, EV_FINAL_UP, EV_B_DONE, EV_C_DONE, EV_D_DONE, EV_A_DONE };
+  auto ev_up = [&](int r) { return ev[8 + 4 * r]; };
+  auto ev_a = [&](int r) { return ev[8 + 4 * r + 1]; };
+  auto ev_b = [&](int r) { return ev[8 + 4 * r + 2]; };
+  auto ev_c = [&](int r) { return ev[8 + 4 * r + 3]; };
+
+  // ---- device buffers (allocated before any stream runs: no hipFree mid-open)
+  const size_t Ch = C > 1 ? C / 2 : 1;
+  DevBuf up, A, P, Y, chiC, ScA, ScB, ScC, xa, xb, xd, xh, xp, Hb[2], Lb[2], gts, canA, canB, canC, canD, pstA, pstB;
+  TPST_HIP(ctx, up.alloc(up_bytes));
+  TPST_HIP(ctx, A.alloc(C * 96));
+  TPST_HIP(ctx, P.alloc(C * 96));
+  TPST_HIP(ctx, Y.alloc(C * 32));
+  TPST_HIP(ctx, chiC.alloc(C * 32));
+  TPST_HIP(ctx, ScA.alloc(2 * C * 32));
+  TPST_HIP(ctx, ScB.alloc(C * 32));
+  TPST_HIP(ctx, ScC.alloc(C * 32));
+  TPST_HIP(ctx, xa.alloc(C * sizeof(Xyzz<Fq>)));
+  TPST_HIP(ctx, xb.alloc(2 * sizeof(Xyzz<Fq>)));
+  TPST_HIP(ctx, xd.alloc((k + 1) * sizeof(Xyzz<Fq2>)));
+  TPST_HIP(ctx, xh.alloc(C * sizeof(Xyzz<Fq2>)));
+  TPST_HIP(ctx, xp.alloc(((size_t)m + 1) * sizeof(Xyzz<Fq>)));
+  for (int i = 0; i < 2; i++) {
+    TPST_HIP(ctx, Hb[i].alloc(Ch * 192));
+    TPST_HIP(ctx, Lb[i].alloc(Ch * N_LINE_COEFFS * sizeof(LineCoeff)));
+  }
+  TPST_HIP(ctx, gts.alloc(2 * sizeof(Fq12)));
+  TPST_HIP(ctx, canA.alloc(2 * 576));
+  TPST_HIP(ctx, canB.alloc(2 * 96));
+  TPST_HIP(ctx, canC.alloc((size_t)(m + 1) * 192));
+  TPST_HIP(ctx, canD.alloc(96 + (size_t)k * 192));
+  TPST_HIP(ctx, pstA.alloc(pst_open_scratch_words(st, m) * 4));
+  TPST_HIP(ctx, pstB.alloc(pst_open_scratch_words(st, k) * 4));
+  if (st->t_A_n < C) {
+    TPST_HIP(ctx, st->t_A.alloc(fbt_words<Fq>(C) * 4));
+    st->t_A_n = C;
+  }
   const uint32_t* H0 = st->ph[p->odd]->u();
+  const LineCoeff* L0 = (const LineCoeff*)st->hprep[p->odd].p;
   const uint32_t* tA = st->t_A.u();
   const uint32_t* tH = st->t_h[p->odd].u();
+  auto dup = [&](size_t byte_off) { return (uint32_t*)((uint8_t*)up.p + byte_off); };
 
-  // U = c_u = MSM(comm_list, chi(b)) over the caller's comm_list (sqrt_pst.rs:198),
-  // on the table just built from it; equals commit(q) for this polynomial's own
-  // comm_list (the :206 invariant, checked by the tests)
+  // ---- prologue (stream A): comm_list -> Montgomery, y = chi(b), canonical chi
   {
-    TPST_HIP(ctx, fr_from_mont(s, p->chis.u(), Sc.u(), C));
-    FbGroups g;
-    g.members = C;
-    g.L = g.D = C;
-    TPST_HIP(ctx, fbt_msm<Fq>(ctx->arena, s, tA, Sc.u(), g, x1));
+    uint8_t* a_stage = pin + up_off[m] + (3 * C + m) * 32;  // a_rev (canonical) -> D
+    for (int i = 0; i < k; i++) memcpy(a_stage + 32 * i, point + 4 * (k - 1 - i), 32);
   }
-  TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(s, x1, canon.u(), 1));
-  TPST_HIP(ctx, hipMemcpyAsync(proof->U, canon.p, 96, hipMemcpyDeviceToHost, s));
-  TPST_HIP(ctx, hipStreamSynchronize(s));
+  TPST_HIP(ctx, hipMemcpyAsync(A.p, comms, C * 96, hipMemcpyHostToDevice, sA));  // pageable: staged by HIP
+  TPST_HIP(ctx, points_to_mont<Fq>(sA, A.u(), A.u(), C));
+  TPST_HIP(ctx, hipMemcpyAsync(Y.p, p->chis.p, C * 32, hipMemcpyDeviceToDevice, sA));
+  TPST_HIP(ctx, fr_from_mont(sA, p->chis.u(), chiC.u(), C));
+  TPST_HIP(ctx, hipEventRecord(ev[EV_PRE], sA));
+  for (hipStream_t s2 : {sB, sC, sD}) TPST_HIP(ctx, hipStreamWaitEvent(s2, ev[EV_PRE], 0));
+
+  // ---- stream D: U, then the PST proof of q at a_rev
   {
-    uint8_t b[96];
-    g1_bytes(proof->U, b);
-    sp.absorb_bytes(b, 96);  // mipp.rs:56
+    arD.reset();
+    TPST_HIP(ctx, msm_var<Fq>(arD, sD, A.u(), chiC.u(), C, (Xyzz<Fq>*)xd.p));
+    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(sD, (Xyzz<Fq>*)xd.p, canD.u(), 1));
+    TPST_HIP(ctx, hipMemcpyAsync(pin + dn_U, canD.p, 96, hipMemcpyDeviceToHost, sD));
+    TPST_HIP(ctx, hipEventRecord(ev[EV_U], sD));
+    const size_t a_off = up_off[m] + (3 * C + m) * 32;
+    TPST_HIP(ctx, hipMemcpyAsync(dup(a_off), pin + a_off, (size_t)k * 32, hipMemcpyHostToDevice, sD));
+    TPST_HIP(ctx, fr_to_mont(sD, dup(a_off), dup(a_off), k));
+    Xyzz<Fq2>* x2 = (Xyzz<Fq2>*)xd.p + 1;
+    TPST_HIP(ctx, pst_open_fbt_s<Fq2>(sD, arD, st, st->t_php.u(), st->nv - k, p->q.u(), k, dup(a_off), x2, pstB.u()));
+    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq2>(sD, x2, canD.u() + 24, k));
+    TPST_HIP(ctx, hipMemcpyAsync(pin + dn_final + 96 + 192 + (size_t)m * 96, canD.u() + 24, (size_t)k * 192,
+                                 hipMemcpyDeviceToHost, sD));
+    TPST_HIP(ctx, hipEventRecord(ev[EV_D_DONE], sD));
   }
+  // ---- stream C (round 0): the fold table over comm_list
+  TPST_HIP(ctx, fbt_build<Fq>(arC, sC, A.u(), C, st->t_A.u()));
+  TPST_HIP(ctx, hipEventRecord(ev[EV_TABLE], sC));
+
   // W[t] / Wi[t]: products of the challenges (inverses) folded so far, so that
   // a^(r)_i = sum_t W[t] a_{i + t len}, h^(r)_i = sum_t Wi[t] h_{i + t len}
   std::vector<Fr> W(1, Fr::one()), Wi(1, Fr::one()), xs_inv;
-  auto upload = [&](const std::vector<Fr>& v) -> hipError_t {
-    return hipMemcpyAsync(dW.p, v.data(), v.size() * 32, hipMemcpyHostToDevice, s);
-  };
-  size_t len = C;
-  int round = 0;
-  while (len > 1) {  // mipp.rs:58-120
-    const size_t split = len / 2;
-    const uint32_t* Acur = A.u();
-    const uint32_t* Hcur = H0;
-    if (round > 0) {  // a^(r), h^(r) as table folds of the original vectors
+  Fr cprev = Fr::one();
+  bool have_U = false;
+  for (int r = 0; r < m; r++) {  // mipp.rs:58-120
+    const size_t len = C >> r, s = len / 2, nW = (size_t)1 << r;
+    // stage W | c'W | Wi | c' and upload once (stream A); B and C wait on it
+    uint8_t* stg = pin + up_off[r];
+    for (size_t t = 0; t < nW; t++) {
+      const Fr cw = mul(W[t], cprev);
+      memcpy(stg + 32 * t, W[t].v, 32);
+      memcpy(stg + 32 * (nW + t), cw.v, 32);
+      memcpy(stg + 32 * (2 * nW + t), Wi[t].v, 32);
+    }
+    memcpy(stg + 32 * 3 * nW, cprev.v, 32);
+    uint32_t* dW = dup(up_off[r]);
+    uint32_t* dcW = dW + 8 * nW;
+    uint32_t* dWi = dW + 16 * nW;
+    uint32_t* dcp = dW + 24 * nW;
+    TPST_HIP(ctx, hipMemcpyAsync(dW, stg, (3 * nW + 1) * 32, hipMemcpyHostToDevice, sA));
+    TPST_HIP(ctx, hipEventRecord(ev_up(r), sA));
+
+    // -- A: G1 side of t_l / t_r, Miller loops, final exponentiations
+    const uint32_t* g2 = H0;
+    const LineCoeff* lines = L0;
+    size_t H = 1;
+    if (r == 0) {
+      TPST_HIP(ctx, affine_rot(sA, A.u(), P.u(), C, 24));
+    } else {
+      TPST_HIP(ctx, hipStreamWaitEvent(sA, ev[EV_TABLE], 0));
+      TPST_HIP(ctx, mipp_scalars(sA, dW, nullptr, len, 0, C, ScA.u()));
+      TPST_HIP(ctx, mipp_scalars(sA, dcW, nullptr, len, 0, C, ScA.u() + 8 * C));
       FbGroups g;
       g.groups = len;
       g.members = C / len;
       g.L = len;
       g.D = 1;
-      TPST_HIP(ctx, upload(Wi));
-      TPST_HIP(ctx, mipp_scalars(s, dW.u(), nullptr, len, 0, C, Sc.u()));
-      TPST_HIP(ctx, fbt_msm<Fq2>(ctx->arena, s, tH, Sc.u(), g, (Xyzz<Fq2>*)xh.p));
-      TPST_HIP(ctx, xyzz_to_affine_mont<Fq2>(s, (Xyzz<Fq2>*)xh.p, Hr.u(), len));
-      TPST_HIP(ctx, upload(W));
-      TPST_HIP(ctx, mipp_scalars(s, dW.u(), nullptr, len, 0, C, Sc.u()));
-      TPST_HIP(ctx, fbt_msm<Fq>(ctx->arena, s, tA, Sc.u(), g, (Xyzz<Fq>*)xa.p));
-      TPST_HIP(ctx, xyzz_to_affine_mont<Fq>(s, (Xyzz<Fq>*)xa.p, Ar.u(), len));
-      Acur = Ar.u();
-      Hcur = Hr.u();
-    } else {
-      TPST_HIP(ctx, upload(W));
+      g.sets = 2;
+      g.set_stride = C;
+      TPST_HIP(ctx, fbt_msm<Fq>(arA, sA, tA, ScA.u(), g, (Xyzz<Fq>*)xa.p));
+      TPST_HIP(ctx, xyzz_to_affine_rot<Fq>(sA, (Xyzz<Fq>*)xa.p, P.u(), 2 * len, len));
+      H = 2;
+      if (r >= 2) {  // h^(r-1), prepared by stream C during round r-1
+        TPST_HIP(ctx, hipStreamWaitEvent(sA, ev_c(r - 1), 0));
+        g2 = Hb[(r - 1) & 1].u();
+        lines = (const LineCoeff*)Lb[(r - 1) & 1].p;
+      }
     }
-    // u_l = a[:s] ^ y[s:], u_r = a[s:] ^ y[:s]  (mipp.rs:66-75): cross-term groups
-    {
+    arA.reset();
+    TPST_HIP(ctx, arA.reserve(multi_pairing_scratch(2, H * s)));
+    TPST_HIP(ctx, multi_pairing_prepared(arA, sA, P.u(), g2, lines, 2, H * s, (Fq12*)gts.p, true, s));
+    TPST_HIP(ctx, fq12_from_mont(sA, (Fq12*)gts.p, canA.u(), 2));
+    uint8_t* dn_r = pin + dn_round + (size_t)r * (192 + 1152);
+    TPST_HIP(ctx, hipMemcpyAsync(dn_r + 192, canA.p, 1152, hipMemcpyDeviceToHost, sA));
+    TPST_HIP(ctx, hipEventRecord(ev_a(r), sA));
+
+    // -- B: y fold by the previous challenge, cross MSMs u_l / u_r
+    TPST_HIP(ctx, hipStreamWaitEvent(sB, ev_up(r), 0));
+    if (r == 0) {
+      arB.reset();
+      TPST_HIP(ctx, msm_var<Fq>(arB, sB, A.u(), chiC.u() + 8 * s, s, (Xyzz<Fq>*)xb.p));          // a[:s]^y[s:]
+      arB.reset();
+      TPST_HIP(ctx, msm_var<Fq>(arB, sB, A.u() + 24 * s, chiC.u(), s, (Xyzz<Fq>*)xb.p + 1));     // a[s:]^y[:s]
+    } else {
+      TPST_HIP(ctx, compress_fr(sB, Y.u(), len, dcp));  // y_l + c' y_r (mipp.rs:124-136)
+      TPST_HIP(ctx, hipStreamWaitEvent(sB, ev[EV_TABLE], 0));
+      TPST_HIP(ctx, mipp_scalars(sB, dW, Y.u(), len, s, C, ScB.u()));
       FbGroups g;
       g.groups = 2;
-      g.members = C / len * split;
+      g.members = C / len * s;
       g.L = len;
-      g.D = split;
-      TPST_HIP(ctx, mipp_scalars(s, dW.u(), Y.u(), len, split, C, Sc.u()));
-      TPST_HIP(ctx, fbt_msm<Fq>(ctx->arena, s, tA, Sc.u(), g, x1));
+      g.D = s;
+      TPST_HIP(ctx, fbt_msm<Fq>(arB, sB, tA, ScB.u(), g, (Xyzz<Fq>*)xb.p));
     }
-    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(s, x1, canon.u(), 2));
-    // t_l = e(a[:s], h[s:]), t_r = e(a[s:], h[:s]) as one batched launch of
-    // two groups: G2 side is h with its halves swapped
-    TPST_HIP(ctx, hipMemcpyAsync(H2.p, Hcur + 48 * split, split * 192, hipMemcpyDeviceToDevice, s));
-    TPST_HIP(ctx, hipMemcpyAsync(H2.u() + 48 * split, Hcur, split * 192, hipMemcpyDeviceToDevice, s));
-    TPST_HIP(ctx, multi_pairing(ctx->arena, s, Acur, H2.u(), 2, split, (Fq12*)gts.p));
-    TPST_HIP(ctx, fq12_from_mont(s, (Fq12*)gts.p, canon.u() + 48, 2));
-    TPST_HIP(ctx, hipMemcpyAsync(proof->comms_u[round][0], canon.p, 96, hipMemcpyDeviceToHost, s));
-    TPST_HIP(ctx, hipMemcpyAsync(proof->comms_u[round][1], canon.u() + 24, 96, hipMemcpyDeviceToHost, s));
-    TPST_HIP(ctx, hipMemcpyAsync(proof->comms_t[round][0], canon.u() + 48, 576, hipMemcpyDeviceToHost, s));
-    TPST_HIP(ctx, hipMemcpyAsync(proof->comms_t[round][1], canon.u() + 48 + 144, 576, hipMemcpyDeviceToHost, s));
-    TPST_HIP(ctx, hipStreamSynchronize(s));
+    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(sB, (Xyzz<Fq>*)xb.p, canB.u(), 2));
+    TPST_HIP(ctx, hipMemcpyAsync(dn_r, canB.p, 192, hipMemcpyDeviceToHost, sB));
+    TPST_HIP(ctx, hipEventRecord(ev_b(r), sB));
+
+    // -- C: h^(r) for round r+1 (r >= 1; round 1 pairs against h^(0) itself)
+    if (r >= 1 && r + 1 < m) {
+      TPST_HIP(ctx, hipStreamWaitEvent(sC, ev_up(r), 0));
+      TPST_HIP(ctx, mipp_scalars(sC, dWi, nullptr, len, 0, C, ScC.u()));
+      FbGroups g;
+      g.groups = len;
+      g.members = C / len;
+      g.L = len;
+      g.D = 1;
+      TPST_HIP(ctx, fbt_msm<Fq2>(arC, sC, tH, ScC.u(), g, (Xyzz<Fq2>*)xh.p));
+      TPST_HIP(ctx, xyzz_to_affine_mont<Fq2>(sC, (Xyzz<Fq2>*)xh.p, Hb[r & 1].u(), len));
+      TPST_HIP(ctx, g2_prepare_batch(sC, Hb[r & 1].u(), len, (LineCoeff*)Lb[r & 1].p));
+      TPST_HIP(ctx, hipEventRecord(ev_c(r), sC));
+    }
+
+    // -- host: transcript (mipp.rs:56, 97-101) and the challenge
+    if (!have_U) {
+      TPST_HIP(ctx, hipEventSynchronize(ev[EV_U]));
+      memcpy(proof->U, pin + dn_U, 96);
+      uint8_t b[96];
+      g1_bytes(proof->U, b);
+      sp.absorb_bytes(b, 96);
+      have_U = true;
+    }
+    TPST_HIP(ctx, hipEventSynchronize(ev_b(r)));
+    TPST_HIP(ctx, hipEventSynchronize(ev_a(r)));
+    memcpy(proof->comms_u[r][0], dn_r, 96);
+    memcpy(proof->comms_u[r][1], dn_r + 96, 96);
+    memcpy(proof->comms_t[r][0], dn_r + 192, 576);
+    memcpy(proof->comms_t[r][1], dn_r + 192 + 576, 576);
     uint8_t b[96];
-    g1_bytes(proof->comms_u[round][0], b);
+    g1_bytes(proof->comms_u[r][0], b);
     sp.absorb_bytes(b, 96);
-    g1_bytes(proof->comms_u[round][1], b);
+    g1_bytes(proof->comms_u[r][1], b);
     sp.absorb_bytes(b, 96);
-    sp.absorb_bytes((const uint8_t*)proof->comms_t[round][0], 576);
-    sp.absorb_bytes((const uint8_t*)proof->comms_t[round][1], 576);
+    sp.absorb_bytes((const uint8_t*)proof->comms_t[r][0], 576);
+    sp.absorb_bytes((const uint8_t*)proof->comms_t[r][1], 576);
     uint64_t ci_c[4];
     sp.challenge(ci_c);  // mipp.rs:101
     const Fr c_inv = fr_canon(ci_c);
     const Fr c = fr_inv(c_inv);  // mipp.rs:106
-    // y_l + c_inv y_r (mipp.rs:124-136); a and h folds are implicit in W / Wi
-    TPST_HIP(ctx, hipMemcpyAsync(small.p, c_inv.v, 32, hipMemcpyHostToDevice, s));
-    TPST_HIP(ctx, compress_fr(s, Y.u(), split, small.u()));
     std::vector<Fr> W2(2 * W.size()), Wi2(2 * Wi.size());
     for (size_t t = 0; t < W2.size(); t++) {
       W2[t] = (t & 1) ? mul(W[t >> 1], c) : W[t >> 1];
@@ -1115,71 +1262,72 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     }
     W.swap(W2);
     Wi.swap(Wi2);
-    TPST_HIP(ctx, hipStreamSynchronize(s));  // small.p is rewritten next round
     xs_inv.push_back(c_inv);
-    len = split;
-    round++;
+    cprev = c_inv;
   }
-  // final_a = a^(m+1)_0, final_h = h^(m+1)_0 (one group over all C bases)
+  if (!have_U) {
+    TPST_HIP(ctx, hipEventSynchronize(ev[EV_U]));
+    memcpy(proof->U, pin + dn_U, 96);
+    uint8_t b[96];
+    g1_bytes(proof->U, b);
+    sp.absorb_bytes(b, 96);
+  }
+
+  // ---- epilogue: final_a (A), final_h (C), pst_proof_h (B); rs need only the
+  // transcript state after the last round (mipp.rs:138-141)
   {
+    uint8_t* stg = pin + up_off[m];
+    for (size_t t = 0; t < C; t++) {
+      memcpy(stg + 32 * t, W[t].v, 32);
+      memcpy(stg + 32 * (C + t), Wi[t].v, 32);
+      Fr v = Fr::one();  // p_h evaluations from the challenges (mipp.rs:159-180)
+      for (int j = 0; j < m; j++)
+        if ((t >> j) & 1) v = mul(v, xs_inv[m - j - 1]);
+      memcpy(stg + 32 * (2 * C + t), v.v, 32);
+    }
+    for (int i = 0; i < m; i++) {
+      uint64_t cc[4];
+      sp.challenge(cc);
+      const Fr rr = fr_canon(cc);
+      memcpy(stg + 32 * (3 * C + i), rr.v, 32);
+    }
+  }
+  uint32_t* dWf = dup(up_off[m]);
+  TPST_HIP(ctx, hipMemcpyAsync(dWf, pin + up_off[m], (3 * C + m) * 32, hipMemcpyHostToDevice, sA));
+  TPST_HIP(ctx, hipEventRecord(ev[EV_FINAL_UP], sA));
+  TPST_HIP(ctx, hipStreamWaitEvent(sA, ev[EV_TABLE], 0));
+  {  // final_a = a^(m)_0 (one group over all C bases)
     FbGroups g;
     g.members = C;
-    TPST_HIP(ctx, upload(W));
-    TPST_HIP(ctx, mipp_scalars(s, dW.u(), nullptr, 1, 0, C, Sc.u()));
-    TPST_HIP(ctx, fbt_msm<Fq>(ctx->arena, s, tA, Sc.u(), g, x1));
-    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(s, x1, canon.u(), 1));
-    TPST_HIP(ctx, hipMemcpyAsync(proof->final_a, canon.p, 96, hipMemcpyDeviceToHost, s));
-    TPST_HIP(ctx, hipStreamSynchronize(s));
-    TPST_HIP(ctx, upload(Wi));
-    TPST_HIP(ctx, mipp_scalars(s, dW.u(), nullptr, 1, 0, C, Sc.u()));
-    TPST_HIP(ctx, fbt_msm<Fq2>(ctx->arena, s, tH, Sc.u(), g, (Xyzz<Fq2>*)xh.p));
-    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq2>(s, (Xyzz<Fq2>*)xh.p, canon.u() + 24, 1));
-    TPST_HIP(ctx, hipMemcpyAsync(proof->final_h, canon.u() + 24, 192, hipMemcpyDeviceToHost, s));
-    TPST_HIP(ctx, hipStreamSynchronize(s));
+    TPST_HIP(ctx, mipp_scalars(sA, dWf, nullptr, 1, 0, C, ScA.u()));
+    TPST_HIP(ctx, fbt_msm<Fq>(arA, sA, tA, ScA.u(), g, (Xyzz<Fq>*)xa.p));
+    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(sA, (Xyzz<Fq>*)xa.p, canA.u(), 1));
+    TPST_HIP(ctx, hipMemcpyAsync(pin + dn_final, canA.p, 96, hipMemcpyDeviceToHost, sA));
   }
-  // p_h evaluations from the challenges (mipp.rs:159-180), then rs and open_g1
-  if (m > 0) {
-    std::vector<uint32_t> evals(C * 8);
-    for (size_t i = 0; i < C; i++) {
-      Fr v = Fr::one();
-      for (int j = 0; j < m; j++)
-        if ((i >> j) & 1) v = mul(v, xs_inv[m - j - 1]);
-      memcpy(&evals[8 * i], v.v, 32);
-    }
-    std::vector<uint32_t> rs(8 * m);
-    for (int i = 0; i < m; i++) {  // mipp.rs:138-141
-      uint64_t c[4];
-      sp.challenge(c);
-      const Fr r = fr_canon(c);
-      memcpy(&rs[8 * i], r.v, 32);
-    }
-    DevBuf de, dr;
-    TPST_HIP(ctx, de.alloc(C * 32));
-    TPST_HIP(ctx, dr.alloc(m * 32));
-    TPST_HIP(ctx, hipMemcpyAsync(de.p, evals.data(), C * 32, hipMemcpyHostToDevice, s));
-    TPST_HIP(ctx, hipMemcpyAsync(dr.p, rs.data(), m * 32, hipMemcpyHostToDevice, s));
-    int rc = pst_open_fbt<Fq>(ctx, st, st->t_pgp.u(), st->nv - m, de.u(), m, dr.u(), x1 + 4);
-    if (rc) return rc;
-    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(s, x1 + 4, canon.u(), m));
-    TPST_HIP(ctx, hipMemcpyAsync(proof->pst_proof_h, canon.p, (size_t)m * 96, hipMemcpyDeviceToHost, s));
-    TPST_HIP(ctx, hipStreamSynchronize(s));
+  TPST_HIP(ctx, hipStreamWaitEvent(sC, ev[EV_FINAL_UP], 0));
+  {  // final_h = h^(m)_0
+    FbGroups g;
+    g.members = C;
+    TPST_HIP(ctx, mipp_scalars(sC, dWf + 8 * C, nullptr, 1, 0, C, ScC.u()));
+    TPST_HIP(ctx, fbt_msm<Fq2>(arC, sC, tH, ScC.u(), g, (Xyzz<Fq2>*)xh.p));
+    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq2>(sC, (Xyzz<Fq2>*)xh.p, canC.u(), 1));
+    TPST_HIP(ctx, hipMemcpyAsync(pin + dn_final + 96, canC.p, 192, hipMemcpyDeviceToHost, sC));
+    TPST_HIP(ctx, hipEventRecord(ev[EV_C_DONE], sC));
   }
-  // PST open of q at a_rev (sqrt_pst.rs:218-225)
-  {
-    const int k = p->m_row;
-    std::vector<uint64_t> arev(4 * k);
-    for (int i = 0; i < k; i++) memcpy(&arev[4 * i], point + 4 * (k - 1 - i), 32);
-    DevBuf da;
-    TPST_HIP(ctx, da.alloc(k * 32));
-    TPST_HIP(ctx, hipMemcpyAsync(da.p, arev.data(), k * 32, hipMemcpyHostToDevice, s));
-    TPST_HIP(ctx, fr_to_mont(s, da.u(), da.u(), k));
-    Xyzz<Fq2>* x2 = (Xyzz<Fq2>*)xy.p + 4;
-    int rc = pst_open_fbt<Fq2>(ctx, st, st->t_php.u(), st->nv - k, p->q.u(), k, da.u(), x2);
-    if (rc) return rc;
-    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq2>(s, x2, canon.u(), k));
-    TPST_HIP(ctx, hipMemcpyAsync(proof->pst_proof, canon.p, (size_t)k * 192, hipMemcpyDeviceToHost, s));
-    TPST_HIP(ctx, hipStreamSynchronize(s));
+  if (m > 0) {  // pst_proof_h = open_g1(p_h, rs) (mipp.rs:144)
+    TPST_HIP(ctx, hipStreamWaitEvent(sB, ev[EV_FINAL_UP], 0));
+    TPST_HIP(ctx, pst_open_fbt_s<Fq>(sB, arB, st, st->t_pgp.u(), st->nv - m, dWf + 16 * C, m, dWf + 24 * C,
+                                     (Xyzz<Fq>*)xp.p, pstA.u()));
+    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(sB, (Xyzz<Fq>*)xp.p, canC.u() + 48, m));
+    TPST_HIP(ctx, hipMemcpyAsync(pin + dn_final + 96 + 192, canC.u() + 48, (size_t)m * 96, hipMemcpyDeviceToHost,
+                                 sB));
   }
+  TPST_HIP(ctx, hipEventRecord(ev[EV_B_DONE], sB));
+  for (hipStream_t s2 : {sA, sB, sC, sD}) TPST_HIP(ctx, hipStreamSynchronize(s2));
+  memcpy(proof->final_a, pin + dn_final, 96);
+  memcpy(proof->final_h, pin + dn_final + 96, 192);
+  if (m > 0) memcpy(proof->pst_proof_h, pin + dn_final + 96 + 192, (size_t)m * 96);
+  memcpy(proof->pst_proof, pin + dn_final + 96 + 192 + (size_t)m * 96, (size_t)k * 192);
   sp.store(tr);
   return TPST_OK;
 }
