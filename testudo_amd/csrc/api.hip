@@ -40,7 +40,12 @@ extern "C" int tpst_create(int device, tpst_ctx** out) {
   tpst_ctx* c = new tpst_ctx();
   c->device = device;
   c->arena.prof = &c->prof;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  // the library stream carries every critical path (the opening's transcript
+  // chain in particular); the opening's side streams (pst_api.hip) are
+  // created at the lowest priority so the dispatcher favours this one
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
+  if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, greatest) != hipSuccess) {
     delete c;
     return TPST_E_HIP;
   }

@@ -1,4 +1,5 @@
 // Fixed-base lookup tables + grouped fixed-base MSM (see fbt.h).
+#include "coop.h"
 #include "fbt.h"
 
 namespace tpst {
@@ -29,6 +30,68 @@ __global__ void __launch_bounds__(64) k_fbt_pow(const uint32_t* __restrict__ bas
   }
 }
 
+// the same chain on a quad of lanes per base (coop.h): 3 product latencies
+// per doubling instead of 9
+template <class F>
+__global__ void __launch_bounds__(64) k_fbt_pow_quad(const uint32_t* __restrict__ bases, size_t n,
+                                                     Xyzz<F>* __restrict__ tmp) {
+  const size_t k = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+  const int qi = threadIdx.x & 3;
+  if (k >= n) return;  // quad-uniform
+  Xyzz<F> p = to_xyzz(load_affine<F>(bases, k));
+  for (int w = 0; w < FBT_W; w++) {
+    if (qi == 0) store_xyzz(tmp, k * FBT_W + w, p);
+    if (w + 1 < FBT_W) {
+      p = dbl_quad(p, qi);
+      p = dbl_quad(p, qi);
+      p = dbl_quad(p, qi);
+      p = dbl_quad(p, qi);
+    }
+  }
+}
+
+// entries (k, w, 0..7) = (1..8) * tmp[k, w] from one thread: the multiples by
+// repeated addition, normalised to affine with ONE inversion (Montgomery's
+// batch trick over d_m = ZZ_m ZZZ_m; the multiples are recomputed for the
+// output pass instead of being held in registers)
+template <class F>
+__global__ void __launch_bounds__(64) k_fbt_mult8(const Xyzz<F>* __restrict__ tmp, size_t n,
+                                                  uint32_t* __restrict__ table) {
+  // d_m and the prefix products live in LDS (a lane's column), not in
+  // dynamically indexed registers
+  __shared__ F sd[FBT_M][64], spre[FBT_M][64];
+  const int l = threadIdx.x;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + l;
+  if (i >= n * FBT_W) return;
+  const Xyzz<F> P = load_xyzz(tmp, i);
+  Xyzz<F> q = P;
+  F pre = F::one();
+  for (int j = 0; j < FBT_M; j++) {
+    const F d = is_zero(q.ZZ) ? F::one() : mul(q.ZZ, q.ZZZ);
+    pre = j ? mul(pre, d) : d;
+    sd[j][l] = d;
+    spre[j][l] = pre;
+    if (j + 1 < FBT_M) q = add(q, P);
+  }
+  F acc = inv(pre);  // 1 / (d_0 ... d_7)
+  for (int j = FBT_M - 1; j >= 0; j--) {
+    const F t = j ? mul(acc, spre[j - 1][l]) : acc;  // 1 / d_j
+    if (j) acc = mul(acc, sd[j][l]);
+    spre[j][l] = t;
+  }
+  q = P;
+  for (int j = 0; j < FBT_M; j++) {
+    Affine<F> a = Affine<F>::inf();
+    if (!is_zero(q.ZZ)) {
+      const F t = spre[j][l];
+      const F izz = mul(t, q.ZZZ), izzz = mul(t, q.ZZ);
+      a = {mul(q.X, izz), mul(q.Y, izzz)};
+    }
+    store_affine<F>(table, i * FBT_M + j, a);
+    if (j + 1 < FBT_M) q = add(q, P);
+  }
+}
+
 // entry (k, w, m) = (m+1) * tmp[k, w], normalised to affine
 template <class F>
 __global__ void __launch_bounds__(64) k_fbt_mult(const Xyzz<F>* __restrict__ tmp, size_t n,
@@ -51,9 +114,15 @@ hipError_t fbt_build(Arena& ar, hipStream_t s, const uint32_t* d_bases, size_t n
   ar.reset();
   TPST_TRY(ar.reserve(Arena::need(n * FBT_W, sizeof(Xyzz<F>))));
   Xyzz<F>* tmp = ar.take<Xyzz<F>>(n * FBT_W);
-  k_fbt_pow<F><<<fbt_grid(n, 64), 64, 0, s>>>(d_bases, n, tmp);
-  TPST_TRY(hipGetLastError());
-  k_fbt_mult<F><<<fbt_grid(fbt_entries<F>(n), 64), 64, 0, s>>>(tmp, n, d_table);
+  if constexpr (sizeof(F) == sizeof(Fq)) {  // G1 (timed: the opening's comm_list table)
+    k_fbt_pow_quad<F><<<fbt_grid(4 * n, 64), 64, 0, s>>>(d_bases, n, tmp);
+    TPST_TRY(hipGetLastError());
+    k_fbt_mult8<F><<<fbt_grid(n * FBT_W, 64), 64, 0, s>>>(tmp, n, d_table);
+  } else {  // G2 tables are built once per SRS
+    k_fbt_pow<F><<<fbt_grid(n, 64), 64, 0, s>>>(d_bases, n, tmp);
+    TPST_TRY(hipGetLastError());
+    k_fbt_mult<F><<<fbt_grid(fbt_entries<F>(n), 64), 64, 0, s>>>(tmp, n, d_table);
+  }
   return hipGetLastError();
 }
 
@@ -64,13 +133,15 @@ __device__ __forceinline__ int fbt_digit(const uint32_t* s, int w, int& carry) {
   return carry ? d - 16 : d;
 }
 
-// thread (g, m, chunk): sum of the 8 lookups of windows [8 chunk, 8 chunk + 8)
+// quad of lanes (coop.h) per (group, member, chunk): sum of the 8 lookups of
+// windows [8 chunk, 8 chunk + 8)
 template <class F>
-__global__ void __launch_bounds__(64) k_fbt_partial(const uint32_t* __restrict__ table,
-                                                    const uint32_t* __restrict__ scal, FbGroups gr,
-                                                    Xyzz<F>* __restrict__ partial) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= gr.sets * gr.groups * gr.members * 8) return;
+__global__ void __launch_bounds__(64) k_fbt_partial_quad(const uint32_t* __restrict__ table,
+                                                         const uint32_t* __restrict__ scal, FbGroups gr,
+                                                         Xyzz<F>* __restrict__ partial) {
+  const size_t i = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+  const int qi = threadIdx.x & 3;
+  if (i >= gr.sets * gr.groups * gr.members * 8) return;  // quad-uniform
   const int ch = (int)(i & 7);
   const size_t per_set = gr.groups * gr.members;
   const size_t qgm = i >> 3, q = qgm / per_set, gm = qgm % per_set;
@@ -99,26 +170,32 @@ __global__ void __launch_bounds__(64) k_fbt_partial(const uint32_t* __restrict__
       if (d) {
         Affine<F> t = load_affine<F>(table, (k * FBT_W + w) * FBT_M + (d < 0 ? -d : d) - 1);
         if (d < 0) t = neg(t);
-        acc = add_affine(acc, t);
+        acc = add_affine_quad(acc, t, qi);
       }
     }
   }
-  store_xyzz(partial, i, acc);
+  if (qi == 0) store_xyzz(partial, i, acc);
 }
 
-// out[seg * out_len + part] = sum of in[seg * seg_len + part * per .. + per)
+// out[seg * parts + part] = sum of in[seg * seg_len + part * per .. + per),
+// BS / 4 quads per block
 template <class F, int BS>
-__global__ void __launch_bounds__(BS) k_seg_sum(const Xyzz<F>* __restrict__ in, size_t seg_len, size_t per,
-                                                size_t parts, Xyzz<F>* __restrict__ out) {
-  __shared__ Xyzz<F> sh[BS];
+__global__ void __launch_bounds__(BS) k_seg_sum_quad(const Xyzz<F>* __restrict__ in, size_t seg_len, size_t per,
+                                                     size_t parts, Xyzz<F>* __restrict__ out) {
+  constexpr int Q = BS / 4;
+  __shared__ Xyzz<F> sh[Q];
+  const int quad = threadIdx.x >> 2, qi = threadIdx.x & 3;
   const size_t seg = blockIdx.x / parts, part = blockIdx.x % parts;
   const size_t lo = part * per, hi = lo + per < seg_len ? lo + per : seg_len;
   Xyzz<F> acc = Xyzz<F>::inf();
-  for (size_t j = lo + threadIdx.x; j < hi; j += BS) acc = add(acc, load_xyzz(in, seg * seg_len + j));
-  sh[threadIdx.x] = acc;
+  for (size_t j = lo + quad; j < hi; j += Q) acc = add_quad(acc, load_xyzz(in, seg * seg_len + j), qi);
+  if (qi == 0) sh[quad] = acc;
   __syncthreads();
-  for (int h = BS / 2; h > 0; h >>= 1) {
-    if ((int)threadIdx.x < h) sh[threadIdx.x] = add(sh[threadIdx.x], sh[threadIdx.x + h]);
+  for (int h = Q / 2; h > 0; h >>= 1) {
+    if (quad < h) {
+      const Xyzz<F> v = add_quad(sh[quad], sh[quad + h], qi);
+      if (qi == 0) sh[quad] = v;
+    }
     __syncthreads();
   }
   if (threadIdx.x == 0) store_xyzz(out, blockIdx.x, sh[0]);
@@ -128,8 +205,8 @@ template <class F>
 hipError_t fbt_msm(Arena& ar, hipStream_t s, const uint32_t* d_table, const uint32_t* d_scalars, const FbGroups& g,
                    Xyzz<F>* d_out) {
   if (!g.groups || !g.sets) return hipSuccess;
-  constexpr int BS = sizeof(F) > 48 ? 64 : 128;
-  constexpr size_t R = 4;
+  constexpr int BS = 128;  // 32 quads per partial sum
+  constexpr size_t R = 4;  // serial additions per quad before the tree
   const size_t G = g.groups * g.sets;
   size_t len = g.members * 8;
   const size_t np = G * (len ? len : 1);
@@ -141,14 +218,14 @@ hipError_t fbt_msm(Arena& ar, hipStream_t s, const uint32_t* d_table, const uint
     len = 1;
     TPST_TRY(hipMemsetAsync(a, 0, G * sizeof(Xyzz<F>), s));
   } else {
-    k_fbt_partial<F><<<fbt_grid(G * len, 64), 64, 0, s>>>(d_table, d_scalars, g, a);
+    k_fbt_partial_quad<F><<<fbt_grid(4 * G * len, 64), 64, 0, s>>>(d_table, d_scalars, g, a);
     TPST_TRY(hipGetLastError());
   }
   while (len > 1) {
-    const size_t per = BS * R;
+    const size_t per = BS / 4 * R;
     const size_t parts = (len + per - 1) / per;
     Xyzz<F>* dst = parts == 1 ? d_out : b;
-    k_seg_sum<F, BS><<<(unsigned)(G * parts), BS, 0, s>>>(a, len, per, parts, dst);
+    k_seg_sum_quad<F, BS><<<(unsigned)(G * parts), BS, 0, s>>>(a, len, per, parts, dst);
     TPST_TRY(hipGetLastError());
     if (parts == 1) return hipSuccess;
     len = parts;

@@ -2,6 +2,7 @@
 #include <cstdlib>
 #include <hipcub/hipcub.hpp>
 #include "device_util.h"
+#include "coop.h"
 #include "msm.h"
 
 namespace tpst {
@@ -343,103 +344,62 @@ __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
 }
 
 // segment t of group g: sum_{b in seg} (b+1) * S_b with b the bucket index
-// inside the group (bucket b holds digit value b+1)
+// inside the group (bucket b holds digit value b+1): running sums over the L
+// buckets plus (segment offset) * (segment sum).  One quad of lanes per
+// segment (coop.h): 4 / 3 product latencies per addition / doubling.
 template <class F>
-__global__ void __launch_bounds__(64, 1) k_seg_reduce(const Xyzz<F>* __restrict__ buckets, uint32_t nb, uint32_t L, size_t nseg,
-                             Xyzz<F>* __restrict__ seg_out) {
-  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nseg) return;
+__global__ void __launch_bounds__(64) k_seg_reduce_quad(const Xyzz<F>* __restrict__ buckets, uint32_t nb, uint32_t L,
+                                                        size_t nseg, Xyzz<F>* __restrict__ seg_out) {
+  const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+  const int qi = threadIdx.x & 3;
+  if (t >= nseg) return;  // quad-uniform
   const uint32_t S = nb / L;
   const size_t g = t / S;
   const uint32_t k = (uint32_t)(t % S);
   const size_t base = g * nb + (size_t)k * L;
   Xyzz<F> acc = Xyzz<F>::inf(), sum = Xyzz<F>::inf();
   for (int b = (int)L - 1; b >= 0; b--) {
-    acc = add(acc, load_xyzz(buckets, base + b));
-    sum = add(sum, acc);
+    acc = add_quad(acc, load_xyzz(buckets, base + b), qi);
+    sum = add_quad(sum, acc, qi);
   }
   const uint32_t s0 = k * L;
-  if (s0 != 0 && !is_inf(acc)) {
-    uint32_t sc[1] = {s0};
-    int nbits = 32 - __builtin_clz(s0);
-    sum = add(sum, scalar_mul_xyzz(acc, sc, nbits));
-  }
-  store_xyzz(seg_out, t, sum);
+  if (s0 != 0 && !is_inf(acc)) sum = add_quad(sum, scalar_mul_quad(acc, s0, 32 - __builtin_clz(s0), qi), qi);
+  if (qi == 0) store_xyzz(seg_out, t, sum);
 }
 
-// one workgroup per group: sum its S partial points
+// one workgroup of BS / 4 quads per group: sum its S partial points
 template <class F, int BS>
-__global__ void __launch_bounds__(BS) k_group_reduce(const Xyzz<F>* __restrict__ seg, uint32_t S,
-                                                     Xyzz<F>* __restrict__ out) {
-  __shared__ Xyzz<F> sh[BS];
+__global__ void __launch_bounds__(BS) k_group_reduce_quad(const Xyzz<F>* __restrict__ seg, uint32_t S,
+                                                          Xyzz<F>* __restrict__ out) {
+  constexpr int Q = BS / 4;
+  __shared__ Xyzz<F> sh[Q];
   const size_t g = blockIdx.x;
+  const int quad = threadIdx.x >> 2, qi = threadIdx.x & 3;
   Xyzz<F> acc = Xyzz<F>::inf();
-  for (uint32_t k = threadIdx.x; k < S; k += BS) acc = add(acc, load_xyzz(seg, g * S + k));
-  sh[threadIdx.x] = acc;
+  for (uint32_t k = quad; k < S; k += Q) acc = add_quad(acc, load_xyzz(seg, g * S + k), qi);
+  if (qi == 0) sh[quad] = acc;
   __syncthreads();
-  for (int h = BS / 2; h > 0; h >>= 1) {
-    if ((int)threadIdx.x < h) sh[threadIdx.x] = add(sh[threadIdx.x], sh[threadIdx.x + h]);
+  for (int h = Q / 2; h > 0; h >>= 1) {
+    if (quad < h) {  // a quad reads its two operands before its lane 0 writes (one wave, in order)
+      const Xyzz<F> v = add_quad(sh[quad], sh[quad + h], qi);
+      if (qi == 0) sh[quad] = v;
+    }
     __syncthreads();
   }
   if (threadIdx.x == 0) store_xyzz(out, g, sh[0]);
 }
 
-// Horner over windows: sum_w 2^(c w) G_w
+// Horner over windows on one wave, sum_w 2^(c w) G_w: every quad runs the
+// same chain, its doublings quad-cooperative (coop.h, 3 product latencies
+// per doubling)
 template <class F>
-__global__ void __launch_bounds__(64, 1) k_window_combine(const Xyzz<F>* __restrict__ win, int W, int c, Xyzz<F>* __restrict__ out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  Xyzz<F> acc = load_xyzz(win, W - 1);
-  for (int w = W - 2; w >= 0; w--) {
-    for (int i = 0; i < c; i++) acc = dbl(acc);
-    acc = add(acc, load_xyzz(win, w));
-  }
-  store_xyzz(out, 0, acc);
-}
-
-// ---- cooperative XYZZ doubling (G1): lanes 0..2 of one wave each take one
-// Fq product of every level of dbl-2008-s-1 (4 product levels instead of 9
-// serial products; each product is broadcast from its lane with v_readlane).  The Horner
-// combination of the window sums is a chain of 16 (W - 1) doublings, so its
-// latency is the doubling's latency.
-__device__ __forceinline__ Fq shfl_fq(const Fq& v, int src) {  // lane src's value, wave-uniform (SGPRs)
-  Fq r;
-#pragma unroll
-  for (int i = 0; i < 12; i++) r.v[i] = (uint32_t)__builtin_amdgcn_readlane((int)v.v[i], src);
-  return r;
-}
-
-__device__ __forceinline__ Xyzz<Fq> dbl_coop(const Xyzz<Fq>& p, int lane) {
-  if (is_zero(p.ZZ)) return p;  // uniform: every lane holds p
-  const Fq U = dbl(p.Y);
-  // level 1: V = U^2 (lane 0), XX = X^2 (lane 1)
-  Fq r = mul(lane == 0 ? U : p.X, lane == 0 ? U : p.X);
-  const Fq V = shfl_fq(r, 0), XX = shfl_fq(r, 1);
-  const Fq M = mul3(XX);
-  // level 2: W = U V (0), S = X V (1), ZZ' = V ZZ (2)
-  r = mul(lane == 0 ? U : lane == 1 ? p.X : p.ZZ, V);
-  const Fq W = shfl_fq(r, 0), S = shfl_fq(r, 1), ZZ3 = shfl_fq(r, 2);
-  // level 3: M^2 (0), W Y (1), ZZZ' = W ZZZ (2)
-  r = mul(lane == 0 ? M : W, lane == 0 ? M : lane == 1 ? p.Y : p.ZZZ);
-  const Fq MM = shfl_fq(r, 0), WY = shfl_fq(r, 1), ZZZ3 = shfl_fq(r, 2);
-  Xyzz<Fq> q;
-  q.X = sub(MM, dbl(S));
-  // level 4: M (S - X')
-  r = mul(M, sub(S, q.X));
-  q.Y = sub(shfl_fq(r, 0), WY);
-  q.ZZ = ZZ3;
-  q.ZZZ = ZZZ3;
-  return q;
-}
-
-// Horner over windows on one wave (lanes 0..63 run the same chain; lanes 0..2
-// carry its products): sum_w 2^(c w) G_w
-static __global__ void __launch_bounds__(64, 1) k_window_combine_coop(const Xyzz<Fq>* __restrict__ win, int W, int c,
-                                                               Xyzz<Fq>* __restrict__ out) {
+static __global__ void __launch_bounds__(64, 1) k_window_combine_coop(const Xyzz<F>* __restrict__ win, int W, int c,
+                                                               Xyzz<F>* __restrict__ out) {
   if (blockIdx.x != 0) return;
   const int lane = threadIdx.x;
-  Xyzz<Fq> acc = load_xyzz(win, W - 1);
+  Xyzz<F> acc = load_xyzz(win, W - 1);
   for (int w = W - 2; w >= 0; w--) {
-    for (int i = 0; i < c; i++) acc = dbl_coop(acc, lane);
+    for (int i = 0; i < c; i++) acc = dbl_quad(acc, lane & 3);
     acc = add(acc, load_xyzz(win, w));
   }
   if (lane == 0) store_xyzz(out, 0, acc);
@@ -526,15 +486,15 @@ static hipError_t reduce_buckets(Arena& ar, hipStream_t s, const Xyzz<F>* d_buck
   const uint32_t S = nb / L;
   const size_t nseg = groups * S;
   Xyzz<F>* seg = ar.take<Xyzz<F>>(nseg);
-  k_seg_reduce<F><<<grid_for(nseg, 64), 64, 0, s>>>(d_buckets, nb, L, nseg, seg);
+  k_seg_reduce_quad<F><<<grid_for(4 * nseg, 64), 64, 0, s>>>(d_buckets, nb, L, nseg, seg);
   TPST_TRY(hipGetLastError());
   if (S >= 256 && S % 64 == 0) {  // two-pass tree: 64 -> 1, then per group
     Xyzz<F>* mid = ar.take<Xyzz<F>>(nseg / 64);
-    k_group_reduce<F, 64><<<(unsigned)(nseg / 64), 64, 0, s>>>(seg, 64, mid);
+    k_group_reduce_quad<F, 256><<<(unsigned)(nseg / 64), 256, 0, s>>>(seg, 64, mid);
     TPST_TRY(hipGetLastError());
-    k_group_reduce<F, 64><<<(unsigned)groups, 64, 0, s>>>(mid, S / 64, d_group_out);
+    k_group_reduce_quad<F, 256><<<(unsigned)groups, 256, 0, s>>>(mid, S / 64, d_group_out);
   } else {
-    k_group_reduce<F, 64><<<(unsigned)groups, 64, 0, s>>>(seg, S, d_group_out);
+    k_group_reduce_quad<F, 256><<<(unsigned)groups, 256, 0, s>>>(seg, S, d_group_out);
   }
   return hipGetLastError();
 }
@@ -624,10 +584,7 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   TPST_TRY(reduce_buckets<F>(ar, s, buckets, W, nb, win));
   pf->end(ST_REDUCE, s);
   pf->begin(ST_COMBINE, s);
-  if constexpr (sizeof(F) == sizeof(Fq))
-    k_window_combine_coop<<<1, 64, 0, s>>>(win, W, c, d_out);
-  else
-    k_window_combine<F><<<1, 64, 0, s>>>(win, W, c, d_out);
+  k_window_combine_coop<F><<<1, 64, 0, s>>>(win, W, c, d_out);
   TPST_TRY(hipGetLastError());
   pf->end(ST_COMBINE, s);
   return hipSuccess;

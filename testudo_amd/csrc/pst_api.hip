@@ -975,8 +975,10 @@ static int pst_open_fbt(tpst_ctx* ctx, SrsState* st, const uint32_t* table, int 
 // ---------------------------------------------------------------- open ----
 // Streams of the opening (created once per context) and a pool of events.
 static int open_streams(tpst_ctx* ctx, size_t n_events, size_t pinned_bytes) {
-  for (int i = 0; i < 3; i++)
-    if (!ctx->side[i]) TPST_HIP(ctx, hipStreamCreateWithFlags(&ctx->side[i], hipStreamNonBlocking));
+  int least = 0, greatest = 0;
+  TPST_HIP(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
+  for (int i = 0; i < 2; i++)
+    if (!ctx->side[i]) TPST_HIP(ctx, hipStreamCreateWithPriority(&ctx->side[i], hipStreamNonBlocking, least));
   while (ctx->events.size() < n_events) {
     hipEvent_t e;
     TPST_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -996,7 +998,8 @@ static int open_streams(tpst_ctx* ctx, size_t n_events, size_t pinned_bytes) {
 //
 // Critical path = the transcript: each MIPP round's challenge needs that
 // round's comms_u and comms_t, and the next round's folds need the challenge.
-// Per round r (len = C >> r, s = len / 2) the work is spread over 4 streams:
+// Per round r (len = C >> r, s = len / 2) the work is spread over 3 streams
+// (one hardware queue each; A at the highest priority):
 //   A (critical): a^(r) and c'a^(r) as ONE grouped table MSM over the original
 //     row commitments (two scalar sets W, c' W: a^(r)_i = sum_t W_t a_{i+t len},
 //     c' = the previous challenge inverse), then t_l, t_r against the PREVIOUS
@@ -1004,12 +1007,12 @@ static int open_streams(tpst_ctx* ctx, size_t n_events, size_t pinned_bytes) {
 //       e(a_i, h^(r)_k) = e(a_i, h^(r-1)_k) e(c' a_i, h^(r-1)_{k+len})
 //     -> Miller loops + the two final exponentiations; comms_t -> host.
 //   B: y fold (compress_field, mipp.rs:124-136) and the cross MSMs u_l, u_r
-//     (mipp.rs:66-75) -> canonical -> host.
-//   C: h^(r) = sum_t Wi_t h_{i + t len} (table MSM over powers_of_h) -> affine
-//     -> G2Prepared, consumed by round r+1 (so G2 preparation is off the
-//     critical path); in round 0 it builds the fold table over comm_list.
-//   D: U = MSM(comm_list, chi(b)) (sqrt_pst.rs:198) and the PST proof of q
-//     (sqrt_pst.rs:218-225), which needs nothing from the MIPP.
+//     (mipp.rs:66-75) -> canonical -> host; in round 0 first U =
+//     MSM(comm_list, chi(b)) (sqrt_pst.rs:198) and after it the PST proof of
+//     q (sqrt_pst.rs:218-225), which needs nothing from the MIPP.
+//   C: in round 0 the fold table over comm_list (fbt.h); then h^(r) =
+//     sum_t Wi_t h_{i + t len} (table MSM over powers_of_h) -> affine ->
+//     G2Prepared, consumed by round r+1 (G2 preparation off the critical path).
 // The host waits only for the round's comms (pinned staging), absorbs them
 // (mipp.rs:97-101) and squeezes the challenge; no stream is drained mid-open.
 extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, const uint64_t* comms,
@@ -1056,8 +1059,8 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   const size_t n_ev = 8 + 4 * (size_t)m;
   if (int rc = open_streams(ctx, n_ev, up_bytes + dn_bytes)) return rc;
   uint8_t* pin = (uint8_t*)ctx->pinned;
-  hipStream_t sA = ctx->stream, sB = ctx->side[0], sC = ctx->side[1], sD = ctx->side[2];
-  Arena &arA = ctx->arena, &arB = ctx->arena_side[0], &arC = ctx->arena_side[1], &arD = ctx->arena_side[2];
+  hipStream_t sA = ctx->stream, sB = ctx->side[0], sC = ctx->side[1];
+  Arena &arA = ctx->arena, &arB = ctx->arena_side[0], &arC = ctx->arena_side[1];
   hipEvent_t* ev = ctx->events.data();
   enum { EV_PRE, EV_TABLE, EV_U, EV_FINAL_UP, EV_B_DONE, EV_C_DONE, EV_D_DONE, EV_A_DONE };
   auto ev_up = [&](int r) { return ev[8 + 4 * r]; };
@@ -1112,28 +1115,36 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   TPST_HIP(ctx, hipMemcpyAsync(Y.p, p->chis.p, C * 32, hipMemcpyDeviceToDevice, sA));
   TPST_HIP(ctx, fr_from_mont(sA, p->chis.u(), chiC.u(), C));
   TPST_HIP(ctx, hipEventRecord(ev[EV_PRE], sA));
-  for (hipStream_t s2 : {sB, sC, sD}) TPST_HIP(ctx, hipStreamWaitEvent(s2, ev[EV_PRE], 0));
+  for (hipStream_t s2 : {sB, sC}) TPST_HIP(ctx, hipStreamWaitEvent(s2, ev[EV_PRE], 0));
 
-  // ---- stream D: U, then the PST proof of q at a_rev
-  {
-    arD.reset();
-    TPST_HIP(ctx, msm_var<Fq>(arD, sD, A.u(), chiC.u(), C, (Xyzz<Fq>*)xd.p));
-    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(sD, (Xyzz<Fq>*)xd.p, canD.u(), 1));
-    TPST_HIP(ctx, hipMemcpyAsync(pin + dn_U, canD.p, 96, hipMemcpyDeviceToHost, sD));
-    TPST_HIP(ctx, hipEventRecord(ev[EV_U], sD));
-    const size_t a_off = up_off[m] + (3 * C + m) * 32;
-    TPST_HIP(ctx, hipMemcpyAsync(dup(a_off), pin + a_off, (size_t)k * 32, hipMemcpyHostToDevice, sD));
-    TPST_HIP(ctx, fr_to_mont(sD, dup(a_off), dup(a_off), k));
-    Xyzz<Fq2>* x2 = (Xyzz<Fq2>*)xd.p + 1;
-    TPST_HIP(ctx, pst_open_fbt_s<Fq2>(sD, arD, st, st->t_php.u(), st->nv - k, p->q.u(), k, dup(a_off), x2, pstB.u()));
-    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq2>(sD, x2, canD.u() + 24, k));
-    TPST_HIP(ctx, hipMemcpyAsync(pin + dn_final + 96 + 192 + (size_t)m * 96, canD.u() + 24, (size_t)k * 192,
-                                 hipMemcpyDeviceToHost, sD));
-    TPST_HIP(ctx, hipEventRecord(ev[EV_D_DONE], sD));
-  }
   // ---- stream C (round 0): the fold table over comm_list
   TPST_HIP(ctx, fbt_build<Fq>(arC, sC, A.u(), C, st->t_A.u()));
   TPST_HIP(ctx, hipEventRecord(ev[EV_TABLE], sC));
+  // ---- stream B: U = MSM(comm_list, chi(b)) on that table
+  TPST_HIP(ctx, hipStreamWaitEvent(sB, ev[EV_TABLE], 0));
+  {
+    FbGroups g;
+    g.members = C;
+    g.L = g.D = C;
+    TPST_HIP(ctx, fbt_msm<Fq>(arB, sB, tA, chiC.u(), g, (Xyzz<Fq>*)xd.p));
+    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(sB, (Xyzz<Fq>*)xd.p, canD.u(), 1));
+    TPST_HIP(ctx, hipMemcpyAsync(pin + dn_U, canD.p, 96, hipMemcpyDeviceToHost, sB));
+    TPST_HIP(ctx, hipEventRecord(ev[EV_U], sB));
+  }
+  // PST proof of q at a_rev (stream B, after round 0's cross terms)
+  auto pst_q = [&]() -> int {
+    const size_t a_off = up_off[m] + (3 * C + m) * 32;
+    TPST_HIP(ctx, hipMemcpyAsync(dup(a_off), pin + a_off, (size_t)k * 32, hipMemcpyHostToDevice, sB));
+    TPST_HIP(ctx, fr_to_mont(sB, dup(a_off), dup(a_off), k));
+    Xyzz<Fq2>* x2 = (Xyzz<Fq2>*)xd.p + 1;
+    TPST_HIP(ctx, pst_open_fbt_s<Fq2>(sB, arB, st, st->t_php.u(), st->nv - k, p->q.u(), k, dup(a_off), x2, pstB.u()));
+    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq2>(sB, x2, canD.u() + 24, k));
+    TPST_HIP(ctx, hipMemcpyAsync(pin + dn_final + 96 + 192 + (size_t)m * 96, canD.u() + 24, (size_t)k * 192,
+                                 hipMemcpyDeviceToHost, sB));
+    return TPST_OK;
+  };
+  if (m == 0)
+    if (int rc = pst_q()) return rc;
 
   // W[t] / Wi[t]: products of the challenges (inverses) folded so far, so that
   // a^(r)_i = sum_t W[t] a_{i + t len}, h^(r)_i = sum_t Wi[t] h_{i + t len}
@@ -1193,15 +1204,10 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     TPST_HIP(ctx, hipEventRecord(ev_a(r), sA));
 
     // -- B: y fold by the previous challenge, cross MSMs u_l / u_r
+    // (u_l = a[:s]^y[s:], u_r = a[s:]^y[:s], on the comm_list table)
     TPST_HIP(ctx, hipStreamWaitEvent(sB, ev_up(r), 0));
-    if (r == 0) {
-      arB.reset();
-      TPST_HIP(ctx, msm_var<Fq>(arB, sB, A.u(), chiC.u() + 8 * s, s, (Xyzz<Fq>*)xb.p));          // a[:s]^y[s:]
-      arB.reset();
-      TPST_HIP(ctx, msm_var<Fq>(arB, sB, A.u() + 24 * s, chiC.u(), s, (Xyzz<Fq>*)xb.p + 1));     // a[s:]^y[:s]
-    } else {
-      TPST_HIP(ctx, compress_fr(sB, Y.u(), len, dcp));  // y_l + c' y_r (mipp.rs:124-136)
-      TPST_HIP(ctx, hipStreamWaitEvent(sB, ev[EV_TABLE], 0));
+    if (r > 0) TPST_HIP(ctx, compress_fr(sB, Y.u(), len, dcp));  // y_l + c' y_r (mipp.rs:124-136)
+    {
       TPST_HIP(ctx, mipp_scalars(sB, dW, Y.u(), len, s, C, ScB.u()));
       FbGroups g;
       g.groups = 2;
@@ -1213,6 +1219,8 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(sB, (Xyzz<Fq>*)xb.p, canB.u(), 2));
     TPST_HIP(ctx, hipMemcpyAsync(dn_r, canB.p, 192, hipMemcpyDeviceToHost, sB));
     TPST_HIP(ctx, hipEventRecord(ev_b(r), sB));
+    if (r == 0)
+      if (int rc = pst_q()) return rc;
 
     // -- C: h^(r) for round r+1 (r >= 1; round 1 pairs against h^(0) itself)
     if (r >= 1 && r + 1 < m) {
@@ -1323,7 +1331,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
                                  sB));
   }
   TPST_HIP(ctx, hipEventRecord(ev[EV_B_DONE], sB));
-  for (hipStream_t s2 : {sA, sB, sC, sD}) TPST_HIP(ctx, hipStreamSynchronize(s2));
+  for (hipStream_t s2 : {sA, sB, sC}) TPST_HIP(ctx, hipStreamSynchronize(s2));
   memcpy(proof->final_a, pin + dn_final, 96);
   memcpy(proof->final_h, pin + dn_final + 96, 192);
   if (m > 0) memcpy(proof->pst_proof_h, pin + dn_final + 96 + 192, (size_t)m * 96);
