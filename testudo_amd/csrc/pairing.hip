@@ -1,10 +1,9 @@
 // K4: optimal-ate multi-pairing on gfx950.
 //
 // Layout: prepared line coefficients are coefficient-major (all pairs' step
-// idx coefficients contiguous) so the Miller kernel's per-step loads are
-// coalesced across threads.  A thread owns `k` pairs of one group and keeps
-// one running f (Fq12), so f^2 is paid once per step for k pairs
-// (arkworks does the same with chunks of 4, bls12/mod.rs multi_miller_loop).
+// idx coefficients contiguous) so the line evaluation's loads are coalesced
+// across threads.  The Miller loop itself is restructured as a product of
+// per-bit line products (see "multi-pairing by line products" below).
 #include "device_util.h"
 #include "pairing_kernels.h"
 #include "wave_tower.h"
@@ -79,95 +78,20 @@ hipError_t g2_prepare_batch(hipStream_t s, const uint32_t* d_g2, size_t n, LineC
   return hipGetLastError();
 }
 
-// ---- wave-cooperative Miller loop (wave_tower.h) -------------------------
-// One wave per pair: per bit one SQR_LP stage (f^2 and the line products
-// c0*py, c1*px of this bit's 1-2 lines, 58-62 lanes) and one MUL034 stage
-// per line (39 lanes).  The line coefficients of bit k+1 are fetched while
-// bit k's stages run.
-constexpr int MW = 4;                          // waves per workgroup
-constexpr int MW_SLOTS = 64 + 12 + 12 + 14 + 12;  // PROD, F, F2, B (lines + P), D (prepared lines)
-constexpr int MW_OPS[] = {wave::OP_SQR_LP1, wave::OP_SQR_LP2, wave::OP_MUL034};
-constexpr wave::OpSet<3> MW_SET(MW_OPS);
-constexpr int MW_PROG = MW_SET.words;
-constexpr size_t MW_LDS = (size_t)(MW_PROG + MW * MW_SLOTS * wave::SLOT) * 4;
-static_assert(MW_LDS <= 65536, "Miller kernel LDS");
-
-// map_s != 0: MIPP pair order (multi_pairing_prepared, pairing_kernels.h) -- pair
-// pi = g n + k of group g reads G1 / G2 / line column j(g, k); else j = pi
-__global__ void __launch_bounds__(64 * MW) k_miller_wave(const uint32_t* __restrict__ g1,
-                                                         const uint32_t* __restrict__ g2,
-                                                         const LineCoeff* __restrict__ coeffs, size_t np,
-                                                         Fq12* __restrict__ partial, size_t n_per, size_t map_s) {
-  extern __shared__ uint4 smem4[];
-  wave::lds_t* prog = (wave::lds_t*)(smem4);
-  wave::lds_t* vals = prog + MW_PROG;
-  wave::load_set(prog, MW_SET);
-  __syncthreads();
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const size_t pi = (size_t)blockIdx.x * MW + w;
-  if (pi >= np) return;
-  size_t j = pi;
-  if (map_s) {
-    const size_t g = pi / n_per, k = pi % n_per;
-    j = (k / map_s) * 2 * map_s + (g == 0 ? map_s : 0) + k % map_s;
-  }
-  const G1A p = load_affine<Fq>(g1, j);
-  const G2A q = load_affine<Fq2>(g2, j);
-  if (is_inf(p) || is_inf(q)) {
-    if (lane < 12) reinterpret_cast<Fq*>(partial + pi)[lane] = lane == 0 ? Fq::one() : Fq::zero();
-    return;
-  }
-  const int base = w * MW_SLOTS;
-  const wave::Eng e{vals, base, 0};
-  int F = base + 64, F2 = base + 76;
-  const int B = base + 88, D = base + 102;
-  if (lane == 0) wave::put_slot(vals, B + 6, p.x);
-  if (lane == 1) wave::put_slot(vals, B + 7, p.y);
-  wave::set_one(vals, F);
-  const Fq* cf = reinterpret_cast<const Fq*>(coeffs);  // LineCoeff = 6 Fq
-  // lanes 0..5: line idx, lanes 6..11: line idx + 1 (addition step)
-  int idx = 0;
-  Fq pre = Fq::zero();
-  if (lane < 12) pre = cf[((size_t)(idx + (lane >= 6)) * np + j) * 6 + lane % 6];
-  for (int b = X_BITS - 2; b >= 0; b--) {
-    const bool add = (params::BLS_X >> b) & 1;
-    if (lane < 6 || (add && lane < 12)) wave::put_slot(vals, B + (lane < 6 ? lane : lane + 2), pre);
-    const int nidx = idx + (add ? 2 : 1);
-    if (b > 0 && lane < 12) {
-      const bool nadd = (params::BLS_X >> (b - 1)) & 1;
-      if (lane < 6 || nadd) pre = cf[((size_t)(nidx + (lane >= 6)) * np + j) * 6 + lane % 6];
-    }
-    wave::wave_sync();
-    if (add)
-      wave::run(e, prog + MW_SET.off[1], F, B, F2, D);
-    else
-      wave::run(e, prog + MW_SET.off[0], F, B, F2, D);
-    wave::run(e, prog + MW_SET.off[2], F2, D, F);
-    if (add) {
-      wave::run(e, prog + MW_SET.off[2], F, D + 6, F2);
-      const int t = F;
-      F = F2;
-      F2 = t;
-    }
-    idx = nidx;
-  }
-  wave::store_f12(vals, F, partial + pi);
-}
-
 // ---- product of a group's partials + final exponentiation ----------------
-constexpr int FW = 4;  // waves per workgroup
+constexpr int FW = 2;  // waves per workgroup
 constexpr int FW_SLOTS = 64 + 36;          // PROD, ACC, IN, TMP per wave
 constexpr int FE_SLOTS = 10 * 12 + 24;     // wave 0: 10 registers + inversion temporaries
 constexpr int FE_OPS[] = {wave::OP_F12_MUL, wave::OP_CYC_SQR, wave::OP_FROB1, wave::OP_FROB2, wave::OP_CONJ,
                           wave::OP_INV1,    wave::OP_INV2,    wave::OP_INV3,  wave::OP_INV4,  wave::OP_INV5,
-                          wave::OP_INV6,    wave::OP_INV7};
+                          wave::OP_INV6,    wave::OP_INV7,    wave::OP_F12_SQR};
 constexpr int N_FE_OPS = sizeof(FE_OPS) / sizeof(FE_OPS[0]);
 constexpr wave::OpSet<N_FE_OPS> FE_SET(FE_OPS);
 constexpr int FW_PROG = FE_SET.words;
 constexpr size_t FW_LDS = (size_t)(FW_PROG + (wave::N_CONSTS + FW * FW_SLOTS + FE_SLOTS) * wave::SLOT) * 4;
 static_assert(FW_LDS <= 65536, "final-exponentiation kernel LDS");
 
-enum { FE_MUL, FE_CYC, FE_FROB1, FE_FROB2, FE_CONJ, FE_INV1 };
+enum { FE_MUL, FE_CYC, FE_FROB1, FE_FROB2, FE_CONJ, FE_INV1, FE_SQR12 = 12 };
 
 __device__ int fe_exp_by_x(const wave::Eng& e, const wave::lds_t* prog, int src, int r1, int r2) {
   int cur = src;
@@ -286,7 +210,7 @@ constexpr size_t RW_CHUNK = 8;
 static_assert(RW_LDS <= 65536, "tree-product kernel LDS");
 
 __global__ void __launch_bounds__(64 * RW) k_f12_chunk_prod(const Fq12* __restrict__ in, size_t groups, size_t n,
-                                                            size_t nout, Fq12* __restrict__ out) {
+                                                            size_t nout, Fq12* __restrict__ out, size_t chunk) {
   extern __shared__ uint4 smem4[];
   wave::lds_t* prog = (wave::lds_t*)(smem4);
   wave::lds_t* vals = prog + RW_PROG;
@@ -297,7 +221,7 @@ __global__ void __launch_bounds__(64 * RW) k_f12_chunk_prod(const Fq12* __restri
   const size_t o = (size_t)blockIdx.x * RW + w;
   if (o >= groups * nout) return;
   const size_t g = o / nout, j = o % nout;
-  const size_t k0 = j * RW_CHUNK, k1 = (k0 + RW_CHUNK < n) ? k0 + RW_CHUNK : n;
+  const size_t k0 = j * chunk, k1 = (k0 + chunk < n) ? k0 + chunk : n;
   const int base = wave::N_CONSTS + w * RW_SLOTS;
   const wave::Eng e{vals, base, 0};
   int acc = base + 64, in_r = base + 76, tmp = base + 88;
@@ -318,7 +242,7 @@ static hipError_t tree_partials(Arena& ar, hipStream_t s, Fq12*& partial, size_t
   while (n > 2 * FW) {
     const size_t nout = (n + RW_CHUNK - 1) / RW_CHUNK;
     Fq12* nxt = ar.take<Fq12>(groups * nout);
-    k_f12_chunk_prod<<<grid_for(groups * nout, RW), 64 * RW, RW_LDS, s>>>(partial, groups, n, nout, nxt);
+    k_f12_chunk_prod<<<grid_for(groups * nout, RW), 64 * RW, RW_LDS, s>>>(partial, groups, n, nout, nxt, RW_CHUNK);
     TPST_TRY(hipGetLastError());
     partial = nxt;
     n = nout;
@@ -326,27 +250,205 @@ static hipError_t tree_partials(Arena& ar, hipStream_t s, Fq12*& partial, size_t
   return hipSuccess;
 }
 
-size_t multi_pairing_scratch(size_t groups, size_t n) {
-  size_t tot = Arena::need(groups * (n ? n : 1), sizeof(Fq12));
-  while (n > 2 * FW) {
-    n = (n + RW_CHUNK - 1) / RW_CHUNK;
-    tot += Arena::need(groups * n, sizeof(Fq12));
+// ---- multi-pairing by line products ---------------------------------------
+// With m_{p,b} the line value(s) of pair p at bit b (b = 62..0), the Miller
+// product of a group is
+//     prod_p f_p = prod_b M_b^(2^b),   M_b = prod_p m_{p,b}.
+// The M_b do not depend on f, so they are a parallel tree over the pairs
+// (k_line_eval, then k_f12_chunk_prod levels); the only serial chain left is
+// Horner over the bits: per block of LB bits a block multiplier
+// MB_j = prod_{b in block} M_b^(2^(b - lo_j)) (k_miller_blocks, all blocks in
+// parallel), then F = MB_top, F = F^(2^LB) MB_j for the lower blocks, and the
+// final exponentiation in the same wave (k_chain_final): 56 squarings + 7
+// products instead of 63 x (square + line product) per pair.
+// G1 operands may be XYZZ: the line of column j is scaled by
+// lambda = ZZ ZZZ in Fq (c0 Y ZZ, c1 X ZZZ, c2 ZZ ZZZ), a factor the final
+// exponentiation removes, so no inversion is needed before pairing.
+constexpr int LB = 8;                                     // bits per block
+constexpr int N_BITS = X_BITS - 1;                        // 63 Miller bits
+constexpr int NBLK = (N_BITS + LB - 1) / LB;              // 8 blocks
+constexpr int TREE_CHUNK = 4;
+
+__device__ __forceinline__ size_t pair_column(size_t g, size_t k, size_t n, size_t map_s) {
+  return map_s ? (k / map_s) * 2 * map_s + (g == 0 ? map_s : 0) + k % map_s : g * n + k;
+}
+
+__global__ void k_set_one(Fq12* __restrict__ v, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) v[i] = Fq12::one();
+}
+
+// out[(g * 69 + idx) * n + k] = line idx of pair (g, k) at its G1 point (dense Fq12)
+__global__ void __launch_bounds__(64) k_line_eval(const LineCoeff* __restrict__ coeffs, const uint32_t* __restrict__ g1,
+                                                  size_t rot_L, const uint32_t* __restrict__ g2, size_t groups,
+                                                  size_t n, size_t map_s, Fq12* __restrict__ out) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= groups * N_LINE_COEFFS * n) return;
+  const size_t k = t % n, gi = t / n, idx = gi % N_LINE_COEFFS, g = gi / N_LINE_COEFFS;
+  const size_t ncol = groups * n;
+  const size_t j = pair_column(g, k, n, map_s);
+  Fq12 r = Fq12::one();
+  if (!is_inf(load_affine<Fq2>(g2, j))) {
+    Fq px, py, lam;
+    bool inf, scaled = rot_L != 0;
+    if (scaled) {
+      const size_t src = (j / rot_L) * rot_L + ((j % rot_L) + rot_L / 2) % rot_L;
+      const Xyzz<Fq> P = load_xyzz(reinterpret_cast<const Xyzz<Fq>*>(g1), src);
+      inf = is_inf(P);
+      px = mul(P.X, P.ZZZ);
+      py = mul(P.Y, P.ZZ);
+      lam = mul(P.ZZ, P.ZZZ);
+    } else {
+      const G1A P = load_affine<Fq>(g1, j);
+      inf = is_inf(P);
+      px = P.x;
+      py = P.y;
+    }
+    if (!inf) {
+      const LineCoeff c = coeffs[idx * ncol + j];
+      r = Fq12{{mul_fq(c.c0, py), Fq2::zero(), Fq2::zero()},
+               {mul_fq(c.c1, px), scaled ? mul_fq(c.c2, lam) : c.c2, Fq2::zero()}};
+    }
   }
-  return tot + 1024;
+  out[t] = r;
+}
+
+// line index of the doubling at bit b (62..0); its addition line follows it
+__device__ __forceinline__ int dbl_idx(int b) {
+  int idx = 0;
+  for (int c = X_BITS - 2; c > b; c--) idx += 1 + (int)((params::BLS_X >> c) & 1);
+  return idx;
+}
+
+// one wave per (group, block): MB = prod_{b in block} M_b^(2^(b - lo))
+constexpr int BW = 4;
+constexpr int BW_SLOTS = 64 + 36;
+constexpr int BW_OPS[] = {wave::OP_F12_MUL, wave::OP_F12_SQR};
+constexpr wave::OpSet<2> BW_SET(BW_OPS);
+constexpr int BW_PROG = BW_SET.words;
+constexpr size_t BW_LDS = (size_t)(BW_PROG + (wave::N_CONSTS + BW * BW_SLOTS) * wave::SLOT) * 4;
+static_assert(BW_LDS <= 65536, "block-multiplier kernel LDS");
+
+__global__ void __launch_bounds__(64 * BW) k_miller_blocks(const Fq12* __restrict__ M, size_t groups,
+                                                           Fq12* __restrict__ MB) {
+  extern __shared__ uint4 smem4[];
+  wave::lds_t* prog = (wave::lds_t*)(smem4);
+  wave::lds_t* vals = prog + BW_PROG;
+  wave::load_set(prog, BW_SET);
+  wave::load_consts(vals, 0);
+  __syncthreads();
+  const int w = threadIdx.x >> 6;
+  const size_t o = (size_t)blockIdx.x * BW + w;
+  if (o >= groups * NBLK) return;
+  const size_t g = o / NBLK;
+  const int blk = (int)(o % NBLK);
+  const int lo = blk * LB, hi = (lo + LB < N_BITS ? lo + LB : N_BITS) - 1;
+  const int base = wave::N_CONSTS + w * BW_SLOTS;
+  const wave::Eng e{vals, base, 0};
+  int acc = base + 64, in_r = base + 76, tmp = base + 88;
+  const Fq12* Mg = M + g * N_LINE_COEFFS;
+  for (int b = hi; b >= lo; b--) {
+    const int idx = dbl_idx(b);
+    const bool add = (params::BLS_X >> b) & 1;
+    if (b == hi) {
+      wave::load_f12(vals, acc, Mg + idx);
+    } else {
+      wave::run(e, prog + BW_SET.off[1], acc, 0, tmp);  // acc^2
+      wave::load_f12(vals, in_r, Mg + idx);
+      wave::run(e, prog + BW_SET.off[0], tmp, in_r, acc);
+    }
+    if (add) {
+      wave::load_f12(vals, in_r, Mg + idx + 1);
+      wave::run(e, prog + BW_SET.off[0], acc, in_r, tmp);
+      const int t = acc;
+      acc = tmp;
+      tmp = t;
+    }
+  }
+  wave::store_f12(vals, acc, MB + o);
+}
+
+// one wave per group: F = MB_top, F = F^(2^LB) MB_j, then (optionally) the
+// final exponentiation
+constexpr size_t CH_LDS = (size_t)(FW_PROG + (wave::N_CONSTS + FW_SLOTS + FE_SLOTS) * wave::SLOT) * 4;
+static_assert(CH_LDS <= 65536, "chain kernel LDS");
+
+__global__ void __launch_bounds__(64) k_chain_final(const Fq12* __restrict__ MB, Fq12* __restrict__ out, int do_final) {
+  extern __shared__ uint4 smem4[];
+  wave::lds_t* prog = (wave::lds_t*)(smem4);
+  wave::lds_t* vals = prog + FW_PROG;
+  wave::load_set(prog, FE_SET);
+  wave::load_consts(vals, 0);
+  __syncthreads();
+  const size_t g = blockIdx.x;
+  const int base = wave::N_CONSTS;
+  const wave::Eng e{vals, base, 0};
+  int acc = base + 64, in_r = base + 76, tmp = base + 88;
+  const Fq12* MBg = MB + g * NBLK;
+  wave::load_f12(vals, acc, MBg + NBLK - 1);
+  for (int blk = NBLK - 2; blk >= 0; blk--) {
+    for (int i = 0; i < LB; i++) {
+      wave::run(e, prog + FE_SET.off[FE_SQR12], acc, 0, tmp);
+      const int t = acc;
+      acc = tmp;
+      tmp = t;
+    }
+    wave::load_f12(vals, in_r, MBg + blk);
+    wave::run(e, prog + FE_SET.off[FE_MUL], acc, in_r, tmp);
+    const int t = acc;
+    acc = tmp;
+    tmp = t;
+  }
+  if (!do_final) {
+    wave::store_f12(vals, acc, out + g);
+    return;
+  }
+  const int fe = wave::N_CONSTS + FW_SLOTS;
+  const int r = fe_final_exp(e, prog, acc, fe, fe + 120);
+  wave::store_f12(vals, r, out + g);
+}
+
+static size_t line_tree_len(size_t n) {  // tree levels over n pairs, chunk TREE_CHUNK
+  size_t tot = 0;
+  while (n > 1) {
+    n = (n + TREE_CHUNK - 1) / TREE_CHUNK;
+    tot += n;
+  }
+  return tot;
+}
+
+size_t multi_pairing_scratch(size_t groups, size_t n) {
+  const size_t G = groups * N_LINE_COEFFS;
+  return Arena::need(G * (n ? n : 1), sizeof(Fq12)) + Arena::need(G * (line_tree_len(n) + 1), sizeof(Fq12)) +
+         Arena::need(groups * NBLK, sizeof(Fq12)) + 4096 + 256 * 16;
 }
 
 hipError_t multi_pairing_prepared(Arena& ar, hipStream_t s, const uint32_t* d_g1, const uint32_t* d_g2,
                                   const LineCoeff* d_coeffs, size_t groups, size_t n, Fq12* d_out, bool final_exp,
-                                  size_t map_s) {
+                                  size_t map_s, size_t rot_L) {
   if (!groups) return hipSuccess;
-  const size_t np = groups * n;
-  Fq12* partial = ar.take<Fq12>(np ? np : 1);
-  if (np) {
-    k_miller_wave<<<grid_for(np, MW), 64 * MW, MW_LDS, s>>>(d_g1, d_g2, d_coeffs, np, partial, n, map_s);
+  const size_t G = groups * N_LINE_COEFFS;
+  Fq12* lines = ar.take<Fq12>(G * (n ? n : 1));
+  if (n) {
+    k_line_eval<<<grid_for(G * n, 64), 64, 0, s>>>(d_coeffs, d_g1, rot_L, d_g2, groups, n, map_s, lines);
     TPST_TRY(hipGetLastError());
-    TPST_TRY(tree_partials(ar, s, partial, groups, n));
+  } else {
+    k_set_one<<<grid_for(G, 64), 64, 0, s>>>(lines, G);
+    TPST_TRY(hipGetLastError());
+    n = 1;
   }
-  k_final_wave<<<(unsigned)groups, 64 * FW, FW_LDS, s>>>(partial, n, d_out, final_exp ? 1 : 0);
+  while (n > 1) {
+    const size_t nout = (n + TREE_CHUNK - 1) / TREE_CHUNK;
+    Fq12* nxt = ar.take<Fq12>(G * nout);
+    k_f12_chunk_prod<<<grid_for(G * nout, RW), 64 * RW, RW_LDS, s>>>(lines, G, n, nout, nxt, TREE_CHUNK);
+    TPST_TRY(hipGetLastError());
+    lines = nxt;
+    n = nout;
+  }
+  Fq12* MB = ar.take<Fq12>(groups * NBLK);
+  k_miller_blocks<<<grid_for(groups * NBLK, BW), 64 * BW, BW_LDS, s>>>(lines, groups, MB);
+  TPST_TRY(hipGetLastError());
+  k_chain_final<<<(unsigned)groups, 64, CH_LDS, s>>>(MB, d_out, final_exp ? 1 : 0);
   return hipGetLastError();
 }
 

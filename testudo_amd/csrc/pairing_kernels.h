@@ -24,9 +24,14 @@ hipError_t g2_prepare_batch(hipStream_t s, const uint32_t* d_g2, size_t n, LineC
 // k % map_s of d_g1 / d_g2 / d_coeffs (row length groups * n), i.e. group 0
 // pairs the upper half of every 2 map_s block of prepared G2 points, group 1
 // the lower half -- t_l / t_r of mipp.rs:87-94 against an unswapped h.
+// rot_L != 0: d_g1 is XYZZ (Montgomery) and column j's G1 point is
+// d_g1[(j / rot_L) rot_L + ((j % rot_L) + rot_L / 2) % rot_L] (the MIPP
+// rotation); the pairing is computed without normalising it (its lines are
+// scaled by an Fq factor that the final exponentiation removes, so with
+// final_exp = false the partial differs from the affine one by such a factor).
 hipError_t multi_pairing_prepared(Arena& ar, hipStream_t s, const uint32_t* d_g1, const uint32_t* d_g2,
                                   const LineCoeff* d_coeffs, size_t groups, size_t n, Fq12* d_out,
-                                  bool final_exp = true, size_t map_s = 0);
+                                  bool final_exp = true, size_t map_s = 0, size_t rot_L = 0);
 size_t multi_pairing_scratch(size_t groups, size_t n);
 
 // groups x n Montgomery Fq12 partials -> groups final-exponentiated products

@@ -188,26 +188,6 @@ hipError_t xyzz_to_affine_mont(hipStream_t s, const Xyzz<F>* d_in, uint32_t* d_o
   return hipGetLastError();
 }
 
-// MIPP pairing G1 side (pst_api.hip, tpst_poly_open): out[j] = affine of
-// in[(j / L) L + ((j % L) + L / 2) % L] -- each block of L points rotated by
-// half a block, so that column j of the (unswapped) prepared h lines meets
-// its t_l / t_r partner (mipp.rs:87-94)
-template <class F>
-__global__ void __launch_bounds__(64, 1) k_xyzz_to_affine_rot(const Xyzz<F>* __restrict__ in, uint32_t* __restrict__ out,
-                                                              size_t n, size_t L) {
-  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
-  const size_t src = (j / L) * L + ((j % L) + L / 2) % L;
-  store_affine(out, j, to_affine(load_xyzz(in, src)));
-}
-
-template <class F>
-hipError_t xyzz_to_affine_rot(hipStream_t s, const Xyzz<F>* d_in, uint32_t* d_out, size_t n, size_t L) {
-  if (!n) return hipSuccess;
-  k_xyzz_to_affine_rot<F><<<grid_for(n, 64), 64, 0, s>>>(d_in, d_out, n, L);
-  return hipGetLastError();
-}
-
 __global__ void k_affine_rot(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, size_t n, size_t words) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n * words) return;
@@ -267,6 +247,5 @@ template hipError_t pair_sum<Fq>(hipStream_t, const uint32_t*, size_t, uint32_t*
 template hipError_t pair_sum<Fq2>(hipStream_t, const uint32_t*, size_t, uint32_t*);
 template hipError_t xyzz_to_affine_mont<Fq>(hipStream_t, const Xyzz<Fq>*, uint32_t*, size_t);
 template hipError_t xyzz_to_affine_mont<Fq2>(hipStream_t, const Xyzz<Fq2>*, uint32_t*, size_t);
-template hipError_t xyzz_to_affine_rot<Fq>(hipStream_t, const Xyzz<Fq>*, uint32_t*, size_t, size_t);
 
 }  // namespace tpst

@@ -1187,7 +1187,6 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
       g.sets = 2;
       g.set_stride = C;
       TPST_HIP(ctx, fbt_msm<Fq>(arA, sA, tA, ScA.u(), g, (Xyzz<Fq>*)xa.p));
-      TPST_HIP(ctx, xyzz_to_affine_rot<Fq>(sA, (Xyzz<Fq>*)xa.p, P.u(), 2 * len, len));
       H = 2;
       if (r >= 2) {  // h^(r-1), prepared by stream C during round r-1
         TPST_HIP(ctx, hipStreamWaitEvent(sA, ev_c(r - 1), 0));
@@ -1195,9 +1194,12 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
         lines = (const LineCoeff*)Lb[(r - 1) & 1].p;
       }
     }
+    // G1 side: round 0 the rotated comm_list (affine); later rounds the XYZZ
+    // folds, rotated and line-scaled inside the pairing (no inversion)
     arA.reset();
     TPST_HIP(ctx, arA.reserve(multi_pairing_scratch(2, H * s)));
-    TPST_HIP(ctx, multi_pairing_prepared(arA, sA, P.u(), g2, lines, 2, H * s, (Fq12*)gts.p, true, s));
+    TPST_HIP(ctx, multi_pairing_prepared(arA, sA, r == 0 ? P.u() : xa.u(), g2, lines, 2, H * s, (Fq12*)gts.p, true,
+                                         s, r == 0 ? 0 : len));
     TPST_HIP(ctx, fq12_from_mont(sA, (Fq12*)gts.p, canA.u(), 2));
     uint8_t* dn_r = pin + dn_round + (size_t)r * (192 + 1152);
     TPST_HIP(ctx, hipMemcpyAsync(dn_r + 192, canA.p, 1152, hipMemcpyDeviceToHost, sA));

@@ -49,9 +49,6 @@ hipError_t pair_sum(hipStream_t s, const uint32_t* d_in, size_t half, uint32_t* 
 template <class F>
 hipError_t xyzz_to_affine_mont(hipStream_t s, const Xyzz<F>* d_in, uint32_t* d_out, size_t n);
 
-// MIPP pairing inputs: out[j] = affine(in[(j / L) L + ((j % L) + L/2) % L])
-template <class F>
-hipError_t xyzz_to_affine_rot(hipStream_t s, const Xyzz<F>* d_in, uint32_t* d_out, size_t n, size_t L);
 // affine rotation by half: out[j] = in[(j + n/2) % n], `words` u32 per point
 hipError_t affine_rot(hipStream_t s, const uint32_t* d_in, uint32_t* d_out, size_t n, size_t words);
 
