@@ -20,9 +20,11 @@ and the Miller loops of their IPP pairs, one RCCL all-gather moves [row
 commitments | Miller partial], rank 0 runs the final exponentiation and the
 (transcript-sequential) open.
 
-roofline: the dominant kernel is bucket accumulation (k_bucket_acc_short +
-its fixup); its duration is measured with HIP events on the library's own
-stream over the timed region (tpst_profile_*).  Algorithmic bytes per MSM =
+roofline: the dominant kernel is bucket accumulation (k_bucket_acc_short, one
+launch per window group, msm.hip msm_groups); its duration per MSM (all group
+launches, back to back on the library's own stream, with the earlier groups'
+reductions running beside them on aux streams) is measured with HIP events on
+that stream over the timed region (tpst_profile_*).  Algorithmic bytes per MSM =
 128 B per scalar-point pair (32 B Fr + 96 B affine G1).  The
 kernel is integer-VALU bound ("bound": "valu-int32"), so the HBM fraction is
 small by construction; `traffic` is the rocprofv3 PMC HBM bytes per launch of
@@ -282,7 +284,7 @@ def main():
         "roofline": {"bound": "valu-int32", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                      "traffic_source": (os.path.relpath(PMC_FILE, ROOT) if pmc else None),
-                     "kernel": "k_bucket_acc_short<Fq> (+ k_bucket_fixup_short)", "alg_bytes_per_launch": alg_bytes,
+                     "kernel": "k_bucket_acc_short<Fq> (3 window-group launches per MSM)", "alg_bytes_per_launch": alg_bytes,
                      "kernel_avg_ms": round(acc_avg_ms, 4),
                      "note": "HBM column secondary: the kernel is bound by 32-bit integer VALU issue"},
         "compute": compute,

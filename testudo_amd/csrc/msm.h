@@ -45,6 +45,15 @@ struct Arena {
   char* base = nullptr;
   size_t cap = 0;
   size_t off = 0;
+  // auxiliary streams + events of the window-grouped MSM (msm_var): the
+  // latency-bound reduction / doubling chain of one window group runs on an
+  // aux stream while the next group's bucket accumulation fills the chip.
+  // Created on first use on the current device, destroyed by release().
+  static constexpr int N_AUX = 2, N_AUX_EV = 16;
+  hipStream_t aux[N_AUX] = {};
+  hipEvent_t aux_ev[N_AUX_EV] = {};
+  bool aux_ready = false;
+  hipError_t aux_init();
   hipError_t reserve(size_t bytes);
   void reset() { off = 0; }
   template <class T>

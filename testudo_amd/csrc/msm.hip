@@ -1,5 +1,6 @@
 // Pippenger MSM kernels for gfx950 (see msm.h for the pipeline).
 #include <cstdlib>
+#include <string>
 #include <hipcub/hipcub.hpp>
 #include "device_util.h"
 #include "coop.h"
@@ -287,17 +288,23 @@ __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
 // barrier that the short chunks do not amortise); every piece of a bucket
 // that crosses a chunk boundary is parked -- the chunk's trailing piece in
 // part[2t + 1], its leading piece in part[2t] -- and k_bucket_fixup_short
-// sums them per bucket.
+// sums them per bucket.  One launch covers the entries of windows [wlo, whi)
+// (range[w] = first sorted entry of window w, device-side): chunk indices stay
+// global (t = entry >> lg) so a chunk straddling two window groups is split
+// between their launches without sharing a part[] slot.
 template <class F>
 __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
-    k_bucket_acc_short(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals, size_t m,
-                       uint32_t sent, const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend,
+    k_bucket_acc_short(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                       const uint32_t* __restrict__ range, int wlo, int whi, uint32_t sent,
+                       const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend,
                        const uint32_t* __restrict__ bases, const uint32_t* __restrict__ phib, uint32_t nbase,
                        int lg, Xyzz<F>* __restrict__ buckets, Xyzz<F>* __restrict__ part) {
-  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t c0 = t << lg;
-  if (c0 >= m) return;
-  const size_t c1 = (c0 + ((size_t)1 << lg) < m) ? c0 + ((size_t)1 << lg) : m;
+  const size_t e_lo = range[wlo], e_hi = range[whi];
+  const size_t t = (e_lo >> lg) + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t c0 = t << lg;
+  if (c0 >= e_hi) return;
+  const size_t c1 = (c0 + ((size_t)1 << lg) < e_hi) ? c0 + ((size_t)1 << lg) : e_hi;
+  if (c0 < e_lo) c0 = e_lo;
   uint32_t key = keys[c0];
   Affine<F> pt;
   if (key < sent) pt = fetch_point<F>(bases, phib, nbase, vals[c0]);
@@ -330,10 +337,10 @@ __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
 // the leading pieces of the following ones
 template <class F>
 __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
-    k_bucket_fixup_short(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend, size_t nbk, int lg,
-                         const Xyzz<F>* __restrict__ part, Xyzz<F>* __restrict__ buckets) {
-  const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nbk) return;
+    k_bucket_fixup_short(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend, size_t b0,
+                         size_t b1, int lg, const Xyzz<F>* __restrict__ part, Xyzz<F>* __restrict__ buckets) {
+  const size_t b = b0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= b1) return;
   const uint32_t s = bstart[b], e = bend[b];
   if (e <= s) return;
   const size_t t0 = (size_t)s >> lg, t1 = (size_t)(e - 1) >> lg;
@@ -389,20 +396,43 @@ __global__ void __launch_bounds__(BS) k_group_reduce_quad(const Xyzz<F>* __restr
   if (threadIdx.x == 0) store_xyzz(out, g, sh[0]);
 }
 
-// Horner over windows on one wave, sum_w 2^(c w) G_w: every quad runs the
-// same chain, its doublings quad-cooperative (coop.h, 3 product latencies
-// per doubling)
+// Contribution of the window group [wlo, whi) on one wave:
+// 2^(c wlo) sum_{wlo <= w < whi} 2^(c (w - wlo)) G_w (Horner, then c wlo more
+// doublings), plus the `nextra` finished contributions of the other groups.
+// Every quad runs the same chain, its doublings and additions
+// quad-cooperative (coop.h: 3 / 4 product latencies).
 template <class F>
-static __global__ void __launch_bounds__(64, 1) k_window_combine_coop(const Xyzz<F>* __restrict__ win, int W, int c,
-                                                               Xyzz<F>* __restrict__ out) {
+static __global__ void __launch_bounds__(64, 1) k_window_chain(const Xyzz<F>* __restrict__ win, int wlo, int whi,
+                                                              int c, const Xyzz<F>* __restrict__ extra, int nextra,
+                                                              Xyzz<F>* __restrict__ out) {
   if (blockIdx.x != 0) return;
-  const int lane = threadIdx.x;
-  Xyzz<F> acc = load_xyzz(win, W - 1);
-  for (int w = W - 2; w >= 0; w--) {
-    for (int i = 0; i < c; i++) acc = dbl_quad(acc, lane & 3);
-    acc = add(acc, load_xyzz(win, w));
+  const int qi = threadIdx.x & 3;
+  Xyzz<F> acc = load_xyzz(win, whi - 1);
+  for (int w = whi - 2; w >= wlo; w--) {
+    for (int i = 0; i < c; i++) acc = dbl_quad(acc, qi);
+    acc = add_quad(acc, load_xyzz(win, w), qi);
   }
-  if (lane == 0) store_xyzz(out, 0, acc);
+  for (int i = 0; i < c * wlo; i++) acc = dbl_quad(acc, qi);
+  for (int k = 0; k < nextra; k++) acc = add_quad(acc, load_xyzz(extra, k), qi);
+  if (threadIdx.x == 0) store_xyzz(out, 0, acc);
+}
+
+// range[w] = first sorted entry of window w (keys = w nb + digit; range[W] =
+// number of non-zero digits, the sentinels sort last)
+static __global__ void k_window_range(const uint32_t* __restrict__ keys, size_t m, uint32_t nb, int W,
+                                      uint32_t* __restrict__ range) {
+  const int w = threadIdx.x;
+  if (w > W) return;
+  const uint32_t target = (uint32_t)w * nb;
+  size_t lo = 0, hi = m;
+  while (lo < hi) {
+    const size_t mid = (lo + hi) >> 1;
+    if (keys[mid] < target)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  range[w] = (uint32_t)lo;
 }
 
 template <class F>
@@ -499,6 +529,139 @@ static hipError_t reduce_buckets(Arena& ar, hipStream_t s, const Xyzz<F>* d_buck
   return hipGetLastError();
 }
 
+// Two-level weighted reduction without per-segment scalar multiplications
+// (work ~1/3 of reduce_buckets at the K2 shape, for the window groups whose
+// reduction runs under other groups' accumulation -- throughput, not latency).
+// Level 1: segments of L1 buckets -> S_k = sum_{b in seg} (b - k L1 + 1) X_b and
+// T_k = sum_{b in seg} X_b; then sum_b (b+1) X_b = sum_k S_k + L1 sum_k k T_k,
+// the second sum being the same weighted reduction over Tn_{k-1} = T_k.
+template <class F>
+__global__ void __launch_bounds__(64) k_seg_run_quad(const Xyzz<F>* __restrict__ buckets, uint32_t nb, uint32_t L,
+                                                     size_t nseg, Xyzz<F>* __restrict__ S_out,
+                                                     Xyzz<F>* __restrict__ Tn) {
+  const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+  const int qi = threadIdx.x & 3;
+  if (t >= nseg) return;  // quad-uniform
+  const uint32_t S = nb / L;
+  const size_t g = t / S;
+  const uint32_t k = (uint32_t)(t % S);
+  const size_t base = g * nb + (size_t)k * L;
+  Xyzz<F> acc = Xyzz<F>::inf(), sum = Xyzz<F>::inf();
+  for (int b = (int)L - 1; b >= 0; b--) {
+    acc = add_quad(acc, load_xyzz(buckets, base + b), qi);
+    sum = add_quad(sum, acc, qi);
+  }
+  if (qi == 0) {
+    store_xyzz(S_out, t, sum);
+    store_xyzz(Tn, g * S + (k ? k - 1 : S - 1), k ? acc : Xyzz<F>::inf());
+  }
+}
+
+// out[g] = a[g] + 2^lg b[g], one quad per group
+template <class F>
+__global__ void __launch_bounds__(64) k_lift_add_quad(const Xyzz<F>* __restrict__ a, const Xyzz<F>* __restrict__ b,
+                                                      int lg, size_t groups, Xyzz<F>* __restrict__ out) {
+  const size_t g = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+  const int qi = threadIdx.x & 3;
+  if (g >= groups) return;
+  Xyzz<F> r = load_xyzz(b, g);
+  for (int i = 0; i < lg; i++) r = dbl_quad(r, qi);
+  r = add_quad(r, load_xyzz(a, g), qi);
+  if (qi == 0) store_xyzz(out, g, r);
+}
+
+// sum of S points per group (tree passes of k_group_reduce_quad)
+template <class F>
+static hipError_t sum_groups(Arena& ar, hipStream_t s, const Xyzz<F>* in, size_t groups, uint32_t S, Xyzz<F>* out) {
+  if (S >= 256 && S % 64 == 0) {
+    Xyzz<F>* mid = ar.take<Xyzz<F>>(groups * S / 64);
+    k_group_reduce_quad<F, 256><<<(unsigned)(groups * S / 64), 256, 0, s>>>(in, 64, mid);
+    TPST_TRY(hipGetLastError());
+    k_group_reduce_quad<F, 256><<<(unsigned)groups, 256, 0, s>>>(mid, S / 64, out);
+  } else {
+    k_group_reduce_quad<F, 256><<<(unsigned)groups, 256, 0, s>>>(in, S, out);
+  }
+  return hipGetLastError();
+}
+
+constexpr int RED2_LG = 4;  // level-1 segment length 16
+
+static bool red2_ok(uint32_t nb) { return nb >= (16u << RED2_LG); }
+
+template <class F>
+static size_t reduce2_scratch(size_t groups, uint32_t nb) {
+  const uint32_t S1 = nb >> RED2_LG;
+  return 2 * Arena::need(groups * S1, sizeof(Xyzz<F>)) + reduce_scratch<F>(groups, S1) +
+         Arena::need(groups * S1 / 64 + 1, sizeof(Xyzz<F>)) + 2 * Arena::need(groups, sizeof(Xyzz<F>));
+}
+
+template <class F>
+static hipError_t reduce_buckets2(Arena& ar, hipStream_t s, const Xyzz<F>* d_buckets, size_t groups, uint32_t nb,
+                                  Xyzz<F>* d_group_out) {
+  const uint32_t L1 = 1u << RED2_LG, S1 = nb / L1;
+  const size_t nseg = groups * S1;
+  Xyzz<F>* Sk = ar.take<Xyzz<F>>(nseg);
+  Xyzz<F>* Tn = ar.take<Xyzz<F>>(nseg);
+  Xyzz<F>* R = ar.take<Xyzz<F>>(groups);
+  Xyzz<F>* SS = ar.take<Xyzz<F>>(groups);
+  k_seg_run_quad<F><<<grid_for(4 * nseg, 64), 64, 0, s>>>(d_buckets, nb, L1, nseg, Sk, Tn);
+  TPST_TRY(hipGetLastError());
+  TPST_TRY(reduce_buckets<F>(ar, s, Tn, groups, S1, R));
+  TPST_TRY(sum_groups<F>(ar, s, Sk, groups, S1, SS));
+  k_lift_add_quad<F><<<grid_for(4 * groups, 64), 64, 0, s>>>(SS, R, RED2_LG, groups, d_group_out);
+  return hipGetLastError();
+}
+
+// TPST_MSM_RED2: 0 = weighted-segment reduction everywhere, 1 (default) = the
+// two-level reduction for the aux-stream window groups, 2 = everywhere
+static int red2_mode() {
+  static const int v = [] {
+    const char* e = getenv("TPST_MSM_RED2");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+// window groups of the variable-base MSM (TPST_MSM_GROUPS, default 3): with
+// more than one, the groups' bucket accumulations run top group first on the
+// main stream; each finished group's reduction and doubling chain run on an aux
+// stream under the next group's accumulation, so only the last group's
+// reduction and its c-doubling Horner remain after the accumulation
+static int msm_groups(size_t n, int W) {
+  static const int env = [] {
+    const char* e = getenv("TPST_MSM_GROUPS");
+    return e ? atoi(e) : 0;
+  }();
+  if (n < ((size_t)1 << 17) || W < 4) return 1;
+  int g = env > 0 ? env : 3;
+  if (g > (Arena::N_AUX_EV - 1) / 2) g = (Arena::N_AUX_EV - 1) / 2;
+  return g > W ? W : g;
+}
+
+// window boundaries wb[0..NG] of the groups: TPST_MSM_SPLIT = window counts
+// from the bottom group up ("2,3,3"), else an even split
+static void msm_group_bounds(int W, int NG, int* wb) {
+  static const std::string env = [] {
+    const char* e = getenv("TPST_MSM_SPLIT");
+    return std::string(e ? e : "");
+  }();
+  for (int g = 0; g <= NG; g++) wb[g] = g * W / NG;
+  if (env.empty()) return;
+  int cnt[16], k = 0, tot = 0;
+  for (size_t i = 0; i < env.size() && k < 16;) {
+    const int v = atoi(env.c_str() + i);
+    if (v <= 0) return;
+    cnt[k++] = v;
+    tot += v;
+    const size_t j = env.find(',', i);
+    if (j == std::string::npos) break;
+    i = j + 1;
+  }
+  if (k != NG || tot != W) return;
+  wb[0] = 0;
+  for (int g = 0; g < NG; g++) wb[g + 1] = wb[g] + cnt[g];
+}
+
 template <class F>
 hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint32_t* d_scalars, size_t n,
                    Xyzz<F>* d_out) {
@@ -512,7 +675,8 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   const int c = msm_window_bits(glv ? 2 * n : n);
   const int W = glv ? num_windows_bits(c, 128) : num_windows(c);
   const uint32_t nb = 1u << (c - 1);
-  const size_t m = (size_t)(glv ? 2 : 1) * W * n;
+  const size_t per_win = (size_t)(glv ? 2 : 1) * n;  // entries of one window (zero digits included)
+  const size_t m = per_win * W;
   if (m >= ((size_t)1 << 31)) return hipErrorInvalidValue;
   const size_t nbk = (size_t)W * nb;
   const uint32_t sent = (uint32_t)nbk;  // zero digits; sorts after every bucket key
@@ -520,15 +684,34 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   size_t sort_bytes = 0;
   TPST_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                               (uint32_t*)nullptr, (uint32_t*)nullptr, (int)m, 0, end_bit, s));
-  const int lg = acc_chunk_lg(m);
-  const bool short_chunks = lg == 5;  // K2 at every size up to ~2^24 points
+  const int NG = msm_groups(n, W);
+  int wb[Arena::N_AUX_EV / 2 + 1];
+  msm_group_bounds(W, NG, wb);
+  if (NG > 1) TPST_TRY(ar.aux_init());
+  int lg;
+  if (NG > 1) {  // per-group launches: keep >= 4 waves per SIMD in each
+    static const int env_lg = [] {
+      const char* e = getenv("TPST_MSM_LG");
+      return e ? atoi(e) : 0;
+    }();
+    lg = 4;
+    while (lg < 8 && ((m / NG) >> (lg + 1)) >= (size_t)4 * 64 * 1024) lg++;
+    if (env_lg >= 3 && env_lg <= 8) lg = env_lg;
+  } else {
+    lg = acc_chunk_lg(m);
+  }
+  const bool short_chunks = NG > 1 || lg == 5;  // K2 at every size up to ~2^24 points
   const size_t nchunk = (m + ((size_t)1 << lg) - 1) >> lg;
   const size_t nblk = (nchunk + ACC_BLOCK - 1) / ACC_BLOCK;
+  size_t red_need = 0;
+  for (int g = 0; g < NG; g++) {
+    const size_t gw = (size_t)(wb[g + 1] - wb[g]);
+    red_need += reduce_scratch<F>(gw, nb) + (red2_ok(nb) ? reduce2_scratch<F>(gw, nb) : 0);
+  }
   size_t need = Arena::need(m, 4) * 4 + Arena::need(nbk, 4) * 2 + Arena::need(nbk, sizeof(Xyzz<F>)) +
-                Arena::need(2 * nchunk, sizeof(Xyzz<F>)) + Arena::need(nblk, sizeof(Xyzz<F>)) +
-                reduce_scratch<F>(W, nb) +
-                Arena::need(W, sizeof(Xyzz<F>)) + Arena::need(glv ? n * 24 : 1, 4) + Arena::need(sort_bytes, 1) +
-                8192;
+                Arena::need(2 * nchunk, sizeof(Xyzz<F>)) + Arena::need(nblk, sizeof(Xyzz<F>)) + red_need +
+                Arena::need(W, sizeof(Xyzz<F>)) + Arena::need(NG, sizeof(Xyzz<F>)) + Arena::need(W + 1, 4) +
+                Arena::need(glv ? n * 24 : 1, 4) + Arena::need(sort_bytes, 1) + 8192;
   ar.reset();
   TPST_TRY(ar.reserve(need));
   uint32_t* keys = ar.take<uint32_t>(m);
@@ -541,6 +724,8 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   Xyzz<F>* part = ar.take<Xyzz<F>>(2 * nchunk);
   Xyzz<F>* bpart = ar.take<Xyzz<F>>(nblk);
   Xyzz<F>* win = ar.take<Xyzz<F>>(W);
+  Xyzz<F>* contrib = ar.take<Xyzz<F>>(NG);
+  uint32_t* range = ar.take<uint32_t>(W + 1);
   uint32_t* phib = ar.take<uint32_t>(glv ? n * 24 : 1);
   void* tmp = ar.take<char>(sort_bytes);
 
@@ -564,27 +749,67 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   TPST_TRY(hipMemsetAsync(buckets, 0, nbk * sizeof(Xyzz<F>), s));  // ZZ = 0 == infinity
   k_bucket_bounds<<<grid_for(m, 256), 256, 0, s>>>(keys2, m, sent, bstart, bend);
   TPST_TRY(hipGetLastError());
+  k_window_range<<<1, 64 * ((W + 64) / 64), 0, s>>>(keys2, m, nb, W, range);
+  TPST_TRY(hipGetLastError());
   pf->end(ST_BOUNDS, s);
-  pf->begin(ST_BUCKET_ACC, s);
-  if (short_chunks) {
-    k_bucket_acc_short<F><<<grid_for(nchunk, 64), 64, 0, s>>>(keys2, vals2, m, sent, bstart, bend, d_bases, phib,
-                                                               (uint32_t)n, lg, buckets, part);
-    TPST_TRY(hipGetLastError());
-    k_bucket_fixup_short<F><<<grid_for(nbk, 64), 64, 0, s>>>(bstart, bend, nbk, lg, part, buckets);
-  } else {
+  if (!short_chunks) {  // one launch, long chunks (more than ~2^21 points)
+    pf->begin(ST_BUCKET_ACC, s);
     k_bucket_acc_chunk<F><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys2, vals2, m, sent, bstart, bend, d_bases, phib,
                                                                 (uint32_t)n, lg, buckets, part, bpart);
     TPST_TRY(hipGetLastError());
     k_bucket_fixup<F><<<grid_for(nblk, 64), 64, 0, s>>>(keys2, m, sent, bstart, bend, lg, nblk, part, bpart,
                                                         buckets);
+    TPST_TRY(hipGetLastError());
+    pf->end(ST_BUCKET_ACC, s);
+    pf->begin(ST_REDUCE, s);
+    TPST_TRY(reduce_buckets<F>(ar, s, buckets, W, nb, win));
+    pf->end(ST_REDUCE, s);
+    pf->begin(ST_COMBINE, s);
+    k_window_chain<F><<<1, 64, 0, s>>>(win, 0, W, c, nullptr, 0, d_out);
+    TPST_TRY(hipGetLastError());
+    pf->end(ST_COMBINE, s);
+    return hipSuccess;
   }
-  TPST_TRY(hipGetLastError());
-  pf->end(ST_BUCKET_ACC, s);
+  // groups accumulate on the context stream; the fixup / reduction / chain of
+  // group g > 0 run on an aux stream (a separate low-priority accumulation
+  // stream measured slower: 4+ streams share the hardware queues)
+  hipStream_t bulk = s;
+  pf->begin(ST_BUCKET_ACC, bulk);
+  for (int g = NG - 1; g >= 0; g--) {  // top windows first: their chains are the longest
+    const int wlo = wb[g], whi = wb[g + 1];
+    const size_t gchunks = ((per_win * (size_t)(whi - wlo)) >> lg) + 2;
+    k_bucket_acc_short<F><<<grid_for(gchunks, 64), 64, 0, bulk>>>(keys2, vals2, range, wlo, whi, sent, bstart,
+                                                                   bend, d_bases, phib, (uint32_t)n, lg, buckets,
+                                                                   part);
+    TPST_TRY(hipGetLastError());
+    if (g == 0) pf->end(ST_BUCKET_ACC, bulk);
+    const size_t b0 = (size_t)wlo * nb, b1 = (size_t)whi * nb;
+    hipStream_t a = g ? ar.aux[g % Arena::N_AUX] : s;
+    if (NG > 1) {
+      TPST_TRY(hipEventRecord(ar.aux_ev[2 * g], bulk));
+      TPST_TRY(hipStreamWaitEvent(a, ar.aux_ev[2 * g], 0));
+    }
+    k_bucket_fixup_short<F><<<grid_for(b1 - b0, 64), 64, 0, a>>>(bstart, bend, b0, b1, lg, part, buckets);
+    TPST_TRY(hipGetLastError());
+    if (g == 0) break;
+    if (red2_mode() >= 1 && red2_ok(nb))
+      TPST_TRY(reduce_buckets2<F>(ar, a, buckets + b0, (size_t)(whi - wlo), nb, win + wlo));
+    else
+      TPST_TRY(reduce_buckets<F>(ar, a, buckets + b0, (size_t)(whi - wlo), nb, win + wlo));
+    k_window_chain<F><<<1, 64, 0, a>>>(win, wlo, whi, c, nullptr, 0, contrib + g);
+    TPST_TRY(hipGetLastError());
+    TPST_TRY(hipEventRecord(ar.aux_ev[2 * g + 1], a));
+  }
+  const int w1 = wb[1];  // group 0 = windows [0, w1)
   pf->begin(ST_REDUCE, s);
-  TPST_TRY(reduce_buckets<F>(ar, s, buckets, W, nb, win));
+  if (red2_mode() >= 2 && red2_ok(nb))
+    TPST_TRY(reduce_buckets2<F>(ar, s, buckets, (size_t)w1, nb, win));
+  else
+    TPST_TRY(reduce_buckets<F>(ar, s, buckets, (size_t)w1, nb, win));
   pf->end(ST_REDUCE, s);
   pf->begin(ST_COMBINE, s);
-  k_window_combine_coop<F><<<1, 64, 0, s>>>(win, W, c, d_out);
+  for (int g = 1; g < NG; g++) TPST_TRY(hipStreamWaitEvent(s, ar.aux_ev[2 * g + 1], 0));
+  k_window_chain<F><<<1, 64, 0, s>>>(win, 0, w1, c, contrib + 1, NG - 1, d_out);
   TPST_TRY(hipGetLastError());
   pf->end(ST_COMBINE, s);
   return hipSuccess;
@@ -653,6 +878,28 @@ void Arena::release() {
   if (base) (void)hipFree(base);
   base = nullptr;
   cap = off = 0;
+  if (aux_ready) {
+    for (auto& st : aux) {
+      (void)hipStreamSynchronize(st);
+      (void)hipStreamDestroy(st);
+      st = nullptr;
+    }
+    for (auto& e : aux_ev) {
+      (void)hipEventDestroy(e);
+      e = nullptr;
+    }
+    aux_ready = false;
+  }
+}
+
+hipError_t Arena::aux_init() {
+  if (aux_ready) return hipSuccess;
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
+  for (auto& st : aux) TPST_TRY(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, greatest));
+  for (auto& e : aux_ev) TPST_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  aux_ready = true;
+  return hipSuccess;
 }
 
 int msm_window_bits(size_t n) {

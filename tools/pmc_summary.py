@@ -1,6 +1,7 @@
 """Summarise rocprofv3 --pmc passes of the bench into the roofline's traffic
-and VALU figures for the dominant kernel (k_bucket_acc_chunk) at the bench's
-grid size.  gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE
+and VALU figures for the dominant kernel (k_bucket_acc_short): the MSM runs
+one launch per window group (msm.hip msm_groups), so the figures are per MSM
+= the sum over one call's launches (launch count of the rarest grid = MSMs).  gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE
 reports half of the bytes of wide coalesced reads -> x2; WRITE_SIZE as is.
 FETCH/WRITE_SIZE are in KB (rocprofv3 derived metrics, 1024 B).
 
@@ -28,18 +29,19 @@ def main():
     fetch = load(dfetch, "FETCH_SIZE")
     write = load(dwrite, "WRITE_SIZE")
     valu = load(dvalu, "SQ_INSTS_VALU")
-    grid = max(fetch, key=lambda g: len(fetch[g]))  # the bench's launches dominate the count
     avg = lambda v: sum(v) / len(v)  # noqa: E731
-    f_kb, w_kb = avg(fetch[grid]), avg(write.get(grid, [0.0]))
+    n_msm = min(len(v) for v in fetch.values())
+    per_msm = lambda d: sum(sum(v) for v in d.values()) / n_msm if d else None  # noqa: E731
+    f_kb, w_kb = per_msm(fetch), per_msm(write) or 0.0
     res = {
-        "kernel": "k_bucket_acc_short<Fq> (bench: 2^20-point G1 MSM, GLV, c = 16)",
-        "grid": grid, "launches": {"fetch": len(fetch[grid]), "write": len(write.get(grid, [])),
-                                   "valu": len(valu.get(grid, []))},
-        "fetch_size_kb_per_launch": f_kb, "write_size_kb_per_launch": w_kb,
+        "kernel": "k_bucket_acc_short<Fq> (bench: 2^20-point G1 MSM, GLV, c = 16, one launch per window group)",
+        "grids": {str(g): len(v) for g, v in fetch.items()}, "msm_calls": n_msm,
+        "fetch_size_kb_per_msm": f_kb, "write_size_kb_per_msm": w_kb,
         "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE as reported; KB = 1024 B",
         "hbm_bytes_per_launch": (2 * f_kb + w_kb) * 1024.0,
-        "valu_insts_per_launch": avg(valu[grid]) if valu.get(grid) else None,
-        "other_grids": {str(g): len(v) for g, v in fetch.items() if g != grid},
+        "hbm_bytes_note": "per MSM (all window-group launches of one call), the unit of kernel_avg_ms",
+        "valu_insts_per_launch": per_msm(valu),
+        "per_grid_avg_fetch_kb": {str(g): avg(v) for g, v in fetch.items()},
         "note": "FETCH counts fabric requests incl. Infinity-Cache hits: bases gathered once per window entry",
     }
     os.makedirs(os.path.dirname(out), exist_ok=True)
