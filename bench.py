@@ -341,7 +341,8 @@ def pst_leg(ctx, log_n, reps=5):
     t = time.perf_counter()
     ok = S.verify(ctx, S.PoseidonTranscript(), U, pt, v, pst_proof, mipp, T)
     verify_s = time.perf_counter() - t
-    return {"log_n": log_n, "commit_s": round(warm[0], 4), "open_s": round(warm[1], 4),
+    sizes = _wire_sizes(ctx, nv, pst_proof, mipp)
+    return {"log_n": log_n, "commit_s": round(warm[0], 4), "open_s": round(warm[1], 4), **sizes,
             "commit_plus_open_s": round(warm[0] + warm[1], 4), "reps": reps,
             "h2d_s": round(warm[2], 4), "commit_open_incl_h2d_s": round(warm[0] + warm[1] + warm[2], 4),
             "first_call": {"commit_s": round(cold[0], 4), "open_s": round(cold[1], 4)},
@@ -349,6 +350,14 @@ def pst_leg(ctx, log_n, reps=5):
             "note": "Z resident in HBM for commit_s/open_s (benches/pst.rs:48-62: the polynomial is built before "
                     "the timers); h2d_s = from_evaluations from pageable host memory; eval before the open timer; "
                     "SRS tables built in srs_setup"}
+
+
+def _wire_sizes(ctx, nv, pst_proof, mipp):
+    """benches/pst.rs:43-46,64-74: compressed CanonicalSerialize lengths."""
+    from testudo_amd import serialize as W
+    from testudo_amd import sqrt_pst as S
+    return {"proof_size": W.proof_size(pst_proof, mipp),
+            "commiter_key_size": len(W.ser_committer_key(nv, S.srs_export(ctx, nv)))}
 
 
 def sharded_leg(ctx, log_n, dist, dev):
@@ -409,6 +418,7 @@ def sharded_leg(ctx, log_n, dist, dev):
     ok = S.verify(ctx, S.PoseidonTranscript(), U, pt, v, pst_proof, mipp, T)
     c, o = min(commits[1:]), min(opens[1:])
     return {"log_n": log_n, "commit_s": round(c, 4), "open_s": round(o, 4), "commit_plus_open_s": round(c + o, 4),
+            **_wire_sizes(ctx, nv, pst_proof, mipp),
             "first_call": {"commit_s": round(commits[0], 4), "open_s": round(opens[0], 4)},
             "ranks": world, "rows_per_rank": r1 - r0, "verified": ok,
             "h2d_s_rank0_full": round(h2d_full_s, 4), "h2d_s_rank0_shard": round(h2d_s, 4),

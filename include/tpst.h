@@ -217,6 +217,31 @@ int tpst_mlpc_check(tpst_ctx* ctx, int nv, const uint64_t* comm, const uint64_t*
 int tpst_mlpc_check_2(tpst_ctx* ctx, int nv, const uint64_t* comm_h, const uint64_t* point, const uint64_t* value,
                       const uint64_t* proofs);
 
+/* ---- arkworks wire format (csrc/serialize.hip; host only, no context) ------
+ * CanonicalSerialize with Compress::Yes (ark-serialize 0.4): G1 48 B, G2 96 B
+ * (x with SWFlags in the top bits of the last byte: 0x80 y negative, 0x40
+ * infinity), GT 576 B, usize / Vec length as u64 LE.  The byte strings of
+ * benches/pst.rs:43-46,64-74 (commiter_key_size, proof_size = |Proof| +
+ * |MippProof|).  Writers: out == NULL only reports the length in *len;
+ * TPST_E_ARG if cap is too small or an element is not canonical.  Readers
+ * validate like Validate::Yes (canonical, on curve, prime-order subgroup). */
+int tpst_ser_g1(const uint64_t* p, uint8_t* out48);
+int tpst_ser_g2(const uint64_t* p, uint8_t* out96);
+int tpst_de_g1(const uint8_t* in48, uint64_t* p);
+int tpst_de_g2(const uint8_t* in96, uint64_t* p);
+/* Commitment { nv, g_product } (sqrt_pst.rs:201 U, :121-125 comm_list entries) */
+int tpst_ser_commitment(int nv, const uint64_t* g1, uint8_t* out, size_t cap, size_t* len);
+/* Proof { proofs: Vec<G2> } -- the pst_proof of Polynomial::open (sqrt_pst.rs:225) */
+int tpst_ser_pst_proof(const tpst_open_proof* p, uint8_t* out, size_t cap, size_t* len);
+/* MippProof (mipp.rs:21-28) */
+int tpst_ser_mipp_proof(const tpst_open_proof* p, uint8_t* out, size_t cap, size_t* len);
+/* both back into a tpst_open_proof (U left zero) */
+int tpst_de_open_proof(const uint8_t* pst, size_t pst_len, const uint8_t* mipp, size_t mipp_len,
+                       tpst_open_proof* out);
+/* CommitterKey { nv, powers_of_g, powers_of_h, g, h } from the flat SRS of
+ * tpst_srs_export (benches/pst.rs:43-46) */
+int tpst_ser_committer_key(int nv, const uint64_t* srs_flat, uint8_t* out, size_t cap, size_t* len);
+
 /* ---- utilities ----------------------------------------------------------- */
 /* out[i] = scalars[i] * G1 generator (affine, canonical); synthetic bases */
 int tpst_g1_mul_generator(tpst_ctx* ctx, const uint64_t* scalars, size_t n, uint64_t* out);

@@ -71,6 +71,14 @@ def _check_fullsize(ctx, n):
     assert np.array_equal(mipp.final_h, _arr(d["final_h"], (24,)))
     assert np.array_equal(mipp.pst_proof_h, _arr(d["pst_proof_h"], (m_col, 12)))
     assert S.verify(ctx, S.PoseidonTranscript(), U, pt, v, pst_proof, mipp, T)
+    # wire format (benches/pst.rs:64-74): sizes, and verify on the decoded proof
+    from testudo_amd import serialize as W
+    b_pst, b_mipp = W.ser_pst_proof(pst_proof, mipp), W.ser_mipp_proof(pst_proof, mipp)
+    assert len(b_pst) + len(b_mipp) == 8 + 96 * m_row + 24 + 1296 * m_col + 144
+    if n == 20:
+        assert len(b_pst) + len(b_mipp) == 14096
+    pst2, mipp2 = W.de_open_proof(b_pst, b_mipp)
+    assert S.verify(ctx, S.PoseidonTranscript(), U, pt, v, pst2, mipp2, T)
     bad = fr_array([(limbs_to_int(v) + 1) % R])[0]
     assert not S.verify(ctx, S.PoseidonTranscript(), U, pt, bad, pst_proof, mipp, T)
 

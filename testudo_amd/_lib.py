@@ -71,6 +71,15 @@ PROTOTYPES = [
     ("tpst_mlpc_open_g1", C.c_int, [_vp, _u64p, C.c_int, _u64p, _u64p]),
     ("tpst_mlpc_check", C.c_int, [_vp, C.c_int, _u64p, _u64p, _u64p, _u64p]),
     ("tpst_mlpc_check_2", C.c_int, [_vp, C.c_int, _u64p, _u64p, _u64p, _u64p]),
+    ("tpst_ser_g1", C.c_int, [_u64p, C.c_char_p]),
+    ("tpst_ser_g2", C.c_int, [_u64p, C.c_char_p]),
+    ("tpst_de_g1", C.c_int, [C.c_char_p, _u64p]),
+    ("tpst_de_g2", C.c_int, [C.c_char_p, _u64p]),
+    ("tpst_ser_commitment", C.c_int, [C.c_int, _u64p, C.c_char_p, _sz, C.POINTER(_sz)]),
+    ("tpst_ser_pst_proof", C.c_int, [_vp, C.c_char_p, _sz, C.POINTER(_sz)]),
+    ("tpst_ser_mipp_proof", C.c_int, [_vp, C.c_char_p, _sz, C.POINTER(_sz)]),
+    ("tpst_de_open_proof", C.c_int, [C.c_char_p, _sz, C.c_char_p, _sz, _vp]),
+    ("tpst_ser_committer_key", C.c_int, [C.c_int, _u64p, C.c_char_p, _sz, C.POINTER(_sz)]),
     ("tpst_profile_enable", C.c_int, [_vp, C.c_int]),
     ("tpst_profile_reset", C.c_int, [_vp]),
     ("tpst_profile_read", C.c_int, [_vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
