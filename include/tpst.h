@@ -217,6 +217,54 @@ int tpst_mlpc_check(tpst_ctx* ctx, int nv, const uint64_t* comm, const uint64_t*
 int tpst_mlpc_check_2(tpst_ctx* ctx, int nv, const uint64_t* comm_h, const uint64_t* point, const uint64_t* value,
                       const uint64_t* proofs);
 
+/* Transcript calls of the R1CS prover (poseidon_transcript.rs:55-60, 83-85):
+ * append_scalar -- an Fr absorbed as one Fq element of the same value;
+ * new_from_state2 -- a fresh sponge that absorbs the 32-byte uncompressed Fr. */
+int tpst_transcript_append_fr(tpst_transcript* t, const uint64_t* fr);
+int tpst_transcript_reset_fr(tpst_transcript* t, const uint64_t* fr);
+
+/* ---- Spartan R1CS sum-checks (csrc/r1cs.hip) ------
+ * R1CSInstance (r1csinstance.rs): num_cons x (2 num_vars) sparse A, B, C;
+ * z = vars || 1 || inputs || 0.  Matrices as (row u32, col u32, canonical Fr)
+ * triples, any order; kept on the device as CSR (multiply_vec) + CSC
+ * (compute_eval_table_sparse). */
+typedef struct tpst_r1cs tpst_r1cs;
+int tpst_r1cs_load(tpst_ctx* ctx, size_t num_cons, size_t num_vars, size_t num_inputs, const size_t* nnz /*[3]*/,
+                   const uint32_t* const* rows /*[3]*/, const uint32_t* const* cols /*[3]*/,
+                   const uint64_t* const* vals /*[3]*/, tpst_r1cs** out);
+/* produce_synthetic_r1cs (r1csinstance.rs:166-242) over the SplitMix64 Fr
+ * stream of `seed` (the reference draws thread_rng): also returns the
+ * satisfying vars (num_vars Fr) and inputs (num_inputs Fr) */
+int tpst_r1cs_synthetic(tpst_ctx* ctx, size_t num_cons, size_t num_vars, size_t num_inputs, uint64_t seed,
+                        tpst_r1cs** out, uint64_t* vars, uint64_t* inputs);
+void tpst_r1cs_free(tpst_r1cs* r);
+
+#define TPST_R1CS_MAX_ROUNDS 48
+/* R1CSProof (r1csproof.rs:24-38) without the Groth16 part; canonical Fr.
+ * sc1: cubic round polynomials (4 coefficients, constant first), sc2: quad
+ * (3); claims_phase2 = (Az, Bz, Cz, Az Bz)(rx); claims_phase2_z_abc = the
+ * phase-two finals (z(ry), ABC(ry)); open = (comm U, proof_eval_vars_at_ry,
+ * mipp_proof) of the witness polynomial at ry[1..]. */
+typedef struct {
+  int32_t rounds_x, rounds_y, num_vars_log, pad;
+  uint64_t T[72];
+  uint64_t initial_state[4];
+  uint64_t sc1[TPST_R1CS_MAX_ROUNDS][4][4];
+  uint64_t claims_phase2[4][4];
+  uint64_t claims_phase2_z_abc[2][4];
+  uint64_t r_abc[3][4];
+  uint64_t sc2[TPST_R1CS_MAX_ROUNDS][3][4];
+  uint64_t rx[TPST_R1CS_MAX_ROUNDS][4];
+  uint64_t ry[TPST_R1CS_MAX_ROUNDS][4];
+  uint64_t transcript_sat_state[4];
+  uint64_t eval_vars_at_ry[4];
+  tpst_open_proof open;
+} tpst_r1cs_proof;
+/* R1CSProof::prove (r1csproof.rs:237-370) minus prove_verifier: needs the SRS
+ * loaded for ceil(log2(num_vars) / 2) variables; `tr` is updated in place. */
+int tpst_r1cs_prove(tpst_ctx* ctx, tpst_r1cs* r1cs, const uint64_t* vars, const uint64_t* inputs,
+                    tpst_transcript* tr, tpst_r1cs_proof* out);
+
 /* ---- arkworks wire format (csrc/serialize.hip; host only, no context) ------
  * CanonicalSerialize with Compress::Yes (ark-serialize 0.4): G1 48 B, G2 96 B
  * (x with SWFlags in the top bits of the last byte: 0x80 y negative, 0x40

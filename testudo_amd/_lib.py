@@ -71,6 +71,13 @@ PROTOTYPES = [
     ("tpst_mlpc_open_g1", C.c_int, [_vp, _u64p, C.c_int, _u64p, _u64p]),
     ("tpst_mlpc_check", C.c_int, [_vp, C.c_int, _u64p, _u64p, _u64p, _u64p]),
     ("tpst_mlpc_check_2", C.c_int, [_vp, C.c_int, _u64p, _u64p, _u64p, _u64p]),
+    ("tpst_transcript_append_fr", C.c_int, [_vp, _u64p]),
+    ("tpst_transcript_reset_fr", C.c_int, [_vp, _u64p]),
+    ("tpst_r1cs_load", C.c_int, [_vp, _sz, _sz, _sz, C.POINTER(_sz), C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp),
+                                 C.POINTER(_vp)]),
+    ("tpst_r1cs_synthetic", C.c_int, [_vp, _sz, _sz, _sz, C.c_uint64, C.POINTER(_vp), _u64p, _u64p]),
+    ("tpst_r1cs_free", None, [_vp]),
+    ("tpst_r1cs_prove", C.c_int, [_vp, _vp, _u64p, _u64p, _vp, _vp]),
     ("tpst_ser_g1", C.c_int, [_u64p, C.c_char_p]),
     ("tpst_ser_g2", C.c_int, [_u64p, C.c_char_p]),
     ("tpst_de_g1", C.c_int, [C.c_char_p, _u64p]),
@@ -105,6 +112,28 @@ class OpenProof(C.Structure):
         ("final_h", C.c_uint64 * 24),
         ("pst_proof_h", (C.c_uint64 * 12) * MAX_VARS),
     ]
+
+R1CS_MAX_ROUNDS = 48
+
+
+class R1CSProof(C.Structure):
+    """tpst_r1cs_proof: R1CSProof (r1csproof.rs:24-38) without the Groth16 part."""
+    _fields_ = [
+        ("rounds_x", C.c_int32), ("rounds_y", C.c_int32), ("num_vars_log", C.c_int32), ("pad", C.c_int32),
+        ("T", C.c_uint64 * 72),
+        ("initial_state", C.c_uint64 * 4),
+        ("sc1", ((C.c_uint64 * 4) * 4) * R1CS_MAX_ROUNDS),
+        ("claims_phase2", (C.c_uint64 * 4) * 4),
+        ("claims_phase2_z_abc", (C.c_uint64 * 4) * 2),
+        ("r_abc", (C.c_uint64 * 4) * 3),
+        ("sc2", ((C.c_uint64 * 4) * 3) * R1CS_MAX_ROUNDS),
+        ("rx", (C.c_uint64 * 4) * R1CS_MAX_ROUNDS),
+        ("ry", (C.c_uint64 * 4) * R1CS_MAX_ROUNDS),
+        ("transcript_sat_state", C.c_uint64 * 4),
+        ("eval_vars_at_ry", C.c_uint64 * 4),
+        ("open", OpenProof),
+    ]
+
 
 _lib = None
 

@@ -571,6 +571,30 @@ extern "C" int tpst_transcript_append_gt(tpst_transcript* t, const uint64_t* gt)
   return TPST_OK;
 }
 
+// append_scalar (poseidon_transcript.rs:83-85): Absorb of an Fr into the Fq
+// sponge = one Fq element with the same integer value (r < p)
+extern "C" int tpst_transcript_append_fr(tpst_transcript* t, const uint64_t* fr) {
+  if (!t || !fr || !fr_ok(fr)) return TPST_E_ARG;
+  Sponge sp;
+  sp.load(t);
+  const uint64_t l[6] = {fr[0], fr[1], fr[2], fr[3], 0, 0};
+  sp.absorb(std::vector<Fq>{fq_canon(l)});
+  sp.store(t);
+  return TPST_OK;
+}
+
+// new_from_state2 (poseidon_transcript.rs:55-60): a fresh sponge, then
+// append(Fr) = absorb of its 32-byte uncompressed serialisation
+extern "C" int tpst_transcript_reset_fr(tpst_transcript* t, const uint64_t* fr) {
+  if (!t || !fr || !fr_ok(fr)) return TPST_E_ARG;
+  memset(t, 0, sizeof *t);
+  Sponge sp;
+  sp.load(t);
+  sp.absorb_bytes((const uint8_t*)fr, 32);
+  sp.store(t);
+  return TPST_OK;
+}
+
 extern "C" int tpst_transcript_challenge(tpst_transcript* t, uint64_t* out) {
   if (!t || !out) return TPST_E_ARG;
   Sponge sp;
