@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--pst-log-n", type=int, default=20)
     ap.add_argument("--no-sharded", action="store_true", help="skip the 2^24 (row-sharded) commit+open leg")
     ap.add_argument("--sharded-log-n", type=int, default=24)
+    ap.add_argument("--no-r1cs", action="store_true", help="skip the R1CSProof::prove leg")
+    ap.add_argument("--r1cs-log-cons", type=int, default=20)
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the launcher / rendezvous / timing plumbing only (gloo)")
     return ap.parse_args()
@@ -298,6 +300,11 @@ def main():
             result["pst_2p24"] = sharded_leg(ctx, args.sharded_log_n, None, dev)
         except Exception as e:  # never lose the bench line to the secondary leg
             result["pst_2p24"] = {"error": repr(e)}
+    if not args.no_r1cs and world == 1:
+        try:
+            result["r1cs"] = r1cs_leg(ctx, args.r1cs_log_cons)
+        except Exception as e:  # never lose the bench line to the secondary leg
+            result["r1cs"] = {"error": repr(e)}
     if not args.no_cpu and world == 1:
         result["cpu_baseline"] = cpu_leg(ctx, bk, sc, out, result)
     print(json.dumps(result), flush=True)
@@ -350,6 +357,33 @@ def pst_leg(ctx, log_n, reps=5):
             "note": "Z resident in HBM for commit_s/open_s (benches/pst.rs:48-62: the polynomial is built before "
                     "the timers); h2d_s = from_evaluations from pageable host memory; eval before the open timer; "
                     "SRS tables built in srs_setup"}
+
+
+def r1cs_leg(ctx, log_cons, reps=3):
+    """R1CSProof::prove (r1csproof.rs:237-370, Groth16 step excluded) on a
+    synthetic 2^log_cons-constraint instance with as many variables: the live
+    equivalent of BASELINE configs[4] (testudo_snark::prove is absent from the
+    reference snapshot).  Witness commit + both sum-checks +
+    the PST opening, instance and SRS built before the timer."""
+    from testudo_amd import r1cs as D
+    from testudo_amd import sqrt_pst as S
+    n_cons = n_vars = 1 << log_cons
+    S.srs_setup(ctx, (log_cons + 1) // 2, SEED + 1)
+    inst, vars_, inputs = D.R1CSInstance.produce_synthetic_r1cs(ctx, n_cons, n_vars, 10, SEED + 7)
+    times = []
+    for _ in range(reps + 1):
+        ctx.synchronize()
+        t = time.perf_counter()
+        proof, rx, ry = D.R1CSProof.prove(inst, vars_, inputs, S.PoseidonTranscript())
+        times.append(time.perf_counter() - t)
+    from testudo_amd.encoding import limbs_to_int
+    R = 0x12AB655E9A2CA55660B44D1E5C37B00159AA76FED00000010A11800000000001
+    az, bz, cz, azbz = [limbs_to_int(x) for x in proof.claims_phase2]
+    return {"num_cons": n_cons, "num_vars": n_vars, "num_inputs": 10, "prove_s": round(sorted(times[1:])[reps // 2], 4),
+            "first_call_s": round(times[0], 4), "reps": reps, "claims_consistent": azbz == az * bz % R,
+            "note": "R1CSProof::prove minus prove_verifier (Groth16): witness sqrt-PST commit, phase-one cubic and "
+                    "phase-two quad sum-checks on the device, PST opening at ry[1..]; instance + SRS set up "
+                    "before the timer"}
 
 
 def _wire_sizes(ctx, nv, pst_proof, mipp):
