@@ -134,6 +134,17 @@ __device__ __forceinline__ void glv_split(const uint32_t* k, uint32_t* k1, uint3
   }
 }
 
+// wave issue priority on its SIMD (s_setprio): the latency-bound reduction and
+// chain kernels of the window-grouped MSM share SIMDs with accumulation waves
+__device__ __forceinline__ void set_wave_prio(int prio) {
+  if (prio == 1)
+    __builtin_amdgcn_s_setprio(1);
+  else if (prio == 2)
+    __builtin_amdgcn_s_setprio(2);
+  else if (prio >= 3)
+    __builtin_amdgcn_s_setprio(3);
+}
+
 // ------------------------------------------------------ K2 decomposition --
 // entries (key = window*nb + |digit|-1, val = point index | sign<<31); with
 // GLV, point index i < n is P_i and n + i is phi(P_i)
@@ -338,7 +349,9 @@ __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
 template <class F>
 __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
     k_bucket_fixup_short(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend, size_t b0,
-                         size_t b1, int lg, const Xyzz<F>* __restrict__ part, Xyzz<F>* __restrict__ buckets) {
+                         size_t b1, int lg, const Xyzz<F>* __restrict__ part, Xyzz<F>* __restrict__ buckets,
+                         int prio) {
+  set_wave_prio(prio);
   const size_t b = b0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= b1) return;
   const uint32_t s = bstart[b], e = bend[b];
@@ -356,7 +369,8 @@ __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
 // segment (coop.h): 4 / 3 product latencies per addition / doubling.
 template <class F>
 __global__ void __launch_bounds__(64) k_seg_reduce_quad(const Xyzz<F>* __restrict__ buckets, uint32_t nb, uint32_t L,
-                                                        size_t nseg, Xyzz<F>* __restrict__ seg_out) {
+                                                        size_t nseg, Xyzz<F>* __restrict__ seg_out, int prio = 0) {
+  set_wave_prio(prio);
   const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
   const int qi = threadIdx.x & 3;
   if (t >= nseg) return;  // quad-uniform
@@ -377,7 +391,8 @@ __global__ void __launch_bounds__(64) k_seg_reduce_quad(const Xyzz<F>* __restric
 // one workgroup of BS / 4 quads per group: sum its S partial points
 template <class F, int BS>
 __global__ void __launch_bounds__(BS) k_group_reduce_quad(const Xyzz<F>* __restrict__ seg, uint32_t S,
-                                                          Xyzz<F>* __restrict__ out) {
+                                                          Xyzz<F>* __restrict__ out, int prio = 0) {
+  set_wave_prio(prio);
   constexpr int Q = BS / 4;
   __shared__ Xyzz<F> sh[Q];
   const size_t g = blockIdx.x;
@@ -406,6 +421,7 @@ static __global__ void __launch_bounds__(64, 1) k_window_chain(const Xyzz<F>* __
                                                               int c, const Xyzz<F>* __restrict__ extra, int nextra,
                                                               Xyzz<F>* __restrict__ out) {
   if (blockIdx.x != 0) return;
+  __builtin_amdgcn_s_setprio(3);  // a lone latency chain beside accumulation waves
   const int qi = threadIdx.x & 3;
   Xyzz<F> acc = load_xyzz(win, whi - 1);
   for (int w = whi - 2; w >= wlo; w--) {
@@ -511,20 +527,20 @@ static size_t reduce_scratch(size_t groups, uint32_t nb) {
 
 template <class F>
 static hipError_t reduce_buckets(Arena& ar, hipStream_t s, const Xyzz<F>* d_buckets, size_t groups, uint32_t nb,
-                                 Xyzz<F>* d_group_out) {
+                                 Xyzz<F>* d_group_out, int prio = 0) {
   const uint32_t L = reduce_seg_len(groups, nb);
   const uint32_t S = nb / L;
   const size_t nseg = groups * S;
   Xyzz<F>* seg = ar.take<Xyzz<F>>(nseg);
-  k_seg_reduce_quad<F><<<grid_for(4 * nseg, 64), 64, 0, s>>>(d_buckets, nb, L, nseg, seg);
+  k_seg_reduce_quad<F><<<grid_for(4 * nseg, 64), 64, 0, s>>>(d_buckets, nb, L, nseg, seg, prio);
   TPST_TRY(hipGetLastError());
   if (S >= 256 && S % 64 == 0) {  // two-pass tree: 64 -> 1, then per group
     Xyzz<F>* mid = ar.take<Xyzz<F>>(nseg / 64);
-    k_group_reduce_quad<F, 256><<<(unsigned)(nseg / 64), 256, 0, s>>>(seg, 64, mid);
+    k_group_reduce_quad<F, 256><<<(unsigned)(nseg / 64), 256, 0, s>>>(seg, 64, mid, prio);
     TPST_TRY(hipGetLastError());
-    k_group_reduce_quad<F, 256><<<(unsigned)groups, 256, 0, s>>>(mid, S / 64, d_group_out);
+    k_group_reduce_quad<F, 256><<<(unsigned)groups, 256, 0, s>>>(mid, S / 64, d_group_out, prio);
   } else {
-    k_group_reduce_quad<F, 256><<<(unsigned)groups, 256, 0, s>>>(seg, S, d_group_out);
+    k_group_reduce_quad<F, 256><<<(unsigned)groups, 256, 0, s>>>(seg, S, d_group_out, prio);
   }
   return hipGetLastError();
 }
@@ -538,7 +554,8 @@ static hipError_t reduce_buckets(Arena& ar, hipStream_t s, const Xyzz<F>* d_buck
 template <class F>
 __global__ void __launch_bounds__(64) k_seg_run_quad(const Xyzz<F>* __restrict__ buckets, uint32_t nb, uint32_t L,
                                                      size_t nseg, Xyzz<F>* __restrict__ S_out,
-                                                     Xyzz<F>* __restrict__ Tn) {
+                                                     Xyzz<F>* __restrict__ Tn, int prio = 0) {
+  set_wave_prio(prio);
   const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
   const int qi = threadIdx.x & 3;
   if (t >= nseg) return;  // quad-uniform
@@ -560,7 +577,9 @@ __global__ void __launch_bounds__(64) k_seg_run_quad(const Xyzz<F>* __restrict__
 // out[g] = a[g] + 2^lg b[g], one quad per group
 template <class F>
 __global__ void __launch_bounds__(64) k_lift_add_quad(const Xyzz<F>* __restrict__ a, const Xyzz<F>* __restrict__ b,
-                                                      int lg, size_t groups, Xyzz<F>* __restrict__ out) {
+                                                      int lg, size_t groups, Xyzz<F>* __restrict__ out,
+                                                      int prio = 0) {
+  set_wave_prio(prio);
   const size_t g = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
   const int qi = threadIdx.x & 3;
   if (g >= groups) return;
@@ -572,14 +591,15 @@ __global__ void __launch_bounds__(64) k_lift_add_quad(const Xyzz<F>* __restrict_
 
 // sum of S points per group (tree passes of k_group_reduce_quad)
 template <class F>
-static hipError_t sum_groups(Arena& ar, hipStream_t s, const Xyzz<F>* in, size_t groups, uint32_t S, Xyzz<F>* out) {
+static hipError_t sum_groups(Arena& ar, hipStream_t s, const Xyzz<F>* in, size_t groups, uint32_t S, Xyzz<F>* out,
+                             int prio) {
   if (S >= 256 && S % 64 == 0) {
     Xyzz<F>* mid = ar.take<Xyzz<F>>(groups * S / 64);
-    k_group_reduce_quad<F, 256><<<(unsigned)(groups * S / 64), 256, 0, s>>>(in, 64, mid);
+    k_group_reduce_quad<F, 256><<<(unsigned)(groups * S / 64), 256, 0, s>>>(in, 64, mid, prio);
     TPST_TRY(hipGetLastError());
-    k_group_reduce_quad<F, 256><<<(unsigned)groups, 256, 0, s>>>(mid, S / 64, out);
+    k_group_reduce_quad<F, 256><<<(unsigned)groups, 256, 0, s>>>(mid, S / 64, out, prio);
   } else {
-    k_group_reduce_quad<F, 256><<<(unsigned)groups, 256, 0, s>>>(in, S, out);
+    k_group_reduce_quad<F, 256><<<(unsigned)groups, 256, 0, s>>>(in, S, out, prio);
   }
   return hipGetLastError();
 }
@@ -597,19 +617,28 @@ static size_t reduce2_scratch(size_t groups, uint32_t nb) {
 
 template <class F>
 static hipError_t reduce_buckets2(Arena& ar, hipStream_t s, const Xyzz<F>* d_buckets, size_t groups, uint32_t nb,
-                                  Xyzz<F>* d_group_out) {
+                                  Xyzz<F>* d_group_out, int prio) {
   const uint32_t L1 = 1u << RED2_LG, S1 = nb / L1;
   const size_t nseg = groups * S1;
   Xyzz<F>* Sk = ar.take<Xyzz<F>>(nseg);
   Xyzz<F>* Tn = ar.take<Xyzz<F>>(nseg);
   Xyzz<F>* R = ar.take<Xyzz<F>>(groups);
   Xyzz<F>* SS = ar.take<Xyzz<F>>(groups);
-  k_seg_run_quad<F><<<grid_for(4 * nseg, 64), 64, 0, s>>>(d_buckets, nb, L1, nseg, Sk, Tn);
+  k_seg_run_quad<F><<<grid_for(4 * nseg, 64), 64, 0, s>>>(d_buckets, nb, L1, nseg, Sk, Tn, prio);
   TPST_TRY(hipGetLastError());
-  TPST_TRY(reduce_buckets<F>(ar, s, Tn, groups, S1, R));
-  TPST_TRY(sum_groups<F>(ar, s, Sk, groups, S1, SS));
-  k_lift_add_quad<F><<<grid_for(4 * groups, 64), 64, 0, s>>>(SS, R, RED2_LG, groups, d_group_out);
+  TPST_TRY(reduce_buckets<F>(ar, s, Tn, groups, S1, R, prio));
+  TPST_TRY(sum_groups<F>(ar, s, Sk, groups, S1, SS, prio));
+  k_lift_add_quad<F><<<grid_for(4 * groups, 64), 64, 0, s>>>(SS, R, RED2_LG, groups, d_group_out, prio);
   return hipGetLastError();
+}
+
+// TPST_MSM_PRIO: s_setprio level of the aux-stream reductions (default 2)
+static int red_prio() {
+  static const int v = [] {
+    const char* e = getenv("TPST_MSM_PRIO");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
 }
 
 // TPST_MSM_RED2: 0 = weighted-segment reduction everywhere, 1 (default) = the
@@ -789,13 +818,14 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
       TPST_TRY(hipEventRecord(ar.aux_ev[2 * g], bulk));
       TPST_TRY(hipStreamWaitEvent(a, ar.aux_ev[2 * g], 0));
     }
-    k_bucket_fixup_short<F><<<grid_for(b1 - b0, 64), 64, 0, a>>>(bstart, bend, b0, b1, lg, part, buckets);
+    k_bucket_fixup_short<F><<<grid_for(b1 - b0, 64), 64, 0, a>>>(bstart, bend, b0, b1, lg, part, buckets,
+                                                                  g ? red_prio() : 0);
     TPST_TRY(hipGetLastError());
     if (g == 0) break;
     if (red2_mode() >= 1 && red2_ok(nb))
-      TPST_TRY(reduce_buckets2<F>(ar, a, buckets + b0, (size_t)(whi - wlo), nb, win + wlo));
+      TPST_TRY(reduce_buckets2<F>(ar, a, buckets + b0, (size_t)(whi - wlo), nb, win + wlo, red_prio()));
     else
-      TPST_TRY(reduce_buckets<F>(ar, a, buckets + b0, (size_t)(whi - wlo), nb, win + wlo));
+      TPST_TRY(reduce_buckets<F>(ar, a, buckets + b0, (size_t)(whi - wlo), nb, win + wlo, red_prio()));
     k_window_chain<F><<<1, 64, 0, a>>>(win, wlo, whi, c, nullptr, 0, contrib + g);
     TPST_TRY(hipGetLastError());
     TPST_TRY(hipEventRecord(ar.aux_ev[2 * g + 1], a));
@@ -803,7 +833,7 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   const int w1 = wb[1];  // group 0 = windows [0, w1)
   pf->begin(ST_REDUCE, s);
   if (red2_mode() >= 2 && red2_ok(nb))
-    TPST_TRY(reduce_buckets2<F>(ar, s, buckets, (size_t)w1, nb, win));
+    TPST_TRY(reduce_buckets2<F>(ar, s, buckets, (size_t)w1, nb, win, 0));
   else
     TPST_TRY(reduce_buckets<F>(ar, s, buckets, (size_t)w1, nb, win));
   pf->end(ST_REDUCE, s);
