@@ -89,6 +89,14 @@ int tpst_g1_msm_batch(tpst_ctx* ctx, const tpst_gens* gens, const uint64_t* scal
                       size_t row_stride, size_t col_stride, uint64_t* out);
 int tpst_g1_msm_batch_dev(tpst_ctx* ctx, const tpst_gens* gens, const void* d_scalars, size_t rows, size_t cols,
                           size_t row_stride, size_t col_stride, void* d_out);
+/* MultiCommitGens::new (commitments.rs:17-39): Poseidon<Fr> over label || the
+ * compressed G1 generator, 32 squeezed bytes per generator -> StdRng (ChaCha12)
+ * -> Affine::rand (Fq::rand rejection sampling, square root, cofactor
+ * clearing; one device lane per generator).  Writes G_out (n G1) and h_out
+ * (the (n+1)-th), canonical affine; with out != NULL also loads them as a
+ * generator set (tpst_gens_load). */
+int tpst_gens_new(tpst_ctx* ctx, size_t n, const uint8_t* label, size_t label_len, uint64_t* G_out,
+                  uint64_t* h_out, tpst_gens** out);
 /* PedersenCommit::commit_slice (commitments.rs:79-86): msm(G, scalars) + h * blind;
  * n must equal gens->n (the reference assert_eq!s, here TPST_E_ARG). */
 int tpst_pedersen_commit_slice(tpst_ctx* ctx, const tpst_gens* gens, const uint64_t* scalars, size_t n,

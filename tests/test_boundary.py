@@ -179,3 +179,17 @@ def test_verify_rejects_malformed_proof_elements(ctx):
     badpt[0] = fr_array([O.R - 1])[0]
     badpt[0, 3] = 0xFFFFFFFFFFFFFFFF
     assert not S.verify(ctx, S.PoseidonTranscript(), U, badpt, v, pst_proof, mipp, T)
+
+
+# ---- MultiCommitGens::new (commitments.rs:17-39) ----------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,label", [(1, b""), (7, b"gens_r1cs_sat"), (40, b"gens_pc")])
+def test_gens_new_matches_oracle(ctx, n, label):
+    import gens as GN
+    from testudo_amd.engine import Gens
+    g = Gens.new(ctx, n, label)
+    G, h = GN.multi_commit_gens(n, label)
+    assert g1_from_array(g.G) == G and g1_from_array(g.h)[0] == h
+    # the loaded set commits like commit_slice over the same points
+    s, _ = orc.fr_stream(5, n)
+    assert np.array_equal(g.msm_batch(s, 1, 0, 1)[0], orc.g1_msm(g.G, s))

@@ -125,3 +125,23 @@ def test_msm_linearity_large():
     got = g1_from_array(orc.g1_msm(bases, s))[0]
     tot = sum(limbs_to_int(a) * limbs_to_int(b) for a, b in zip(s, k)) % O.R
     assert got == g1_from_array(orc.g1_mul_gen(fr_array([tot])))[0]
+
+
+# ---- MultiCommitGens::new oracle (oracle/py/gens.py) ----
+def test_chacha_block_known_answers():
+    """The ChaCha block of oracle/py/gens.py (shared by the 12-round StdRng)
+    against the published ChaCha20 vectors: the all-zero key stream (RFC 7539
+    A.1 #1, = rand_chacha's zero-seed ChaCha20 output) and RFC 7539 §2.3.2."""
+    import gens as GN
+    assert GN.chacha_block([0] * 8, 0, rounds=20)[:4] == [0xADE0B876, 0x903DF1A0, 0xE56A5D40, 0x28BD8653]
+    key = [int.from_bytes(bytes(range(4 * i, 4 * i + 4)), "little") for i in range(8)]
+    out = GN.chacha_block(key, 1 | (0x09000000 << 32), rounds=20, nonce=(0x4A000000, 0))
+    assert out[:4] == [0xE4E7F110, 0x15593BD1, 0x1FDD0F50, 0xC47120A3]
+
+
+def test_gens_oracle_points_valid():
+    import gens as GN
+    G, h = GN.multi_commit_gens(3, b"gens_test")
+    for p in G + [h]:
+        assert O.g1_on_curve(p) and O.g1_in_subgroup(p)
+    assert len(set(G + [h])) == 4

@@ -156,6 +156,19 @@ class Gens:
                                          C.byref(handle)), "tpst_gens_load")
         self.handle = handle
 
+    @classmethod
+    def new(cls, ctx: Context, n: int, label: bytes) -> "Gens":
+        """MultiCommitGens::new (commitments.rs:17-39): the generators of a
+        label, derived on the device (tpst_gens_new); .G (n, 12), .h (12,)."""
+        G = np.zeros((n, 12), dtype=np.uint64)
+        h = np.zeros(12, dtype=np.uint64)
+        handle = C.c_void_p()
+        ctx.check(ctx.lib.tpst_gens_new(ctx.h, n, bytes(label), len(label), ptr(G), ptr(h), C.byref(handle)),
+                  "tpst_gens_new")
+        obj = cls.__new__(cls)
+        obj.ctx, obj.n, obj.handle, obj.G, obj.h = ctx, n, handle, G, h
+        return obj
+
     def close(self):
         if self.handle:
             self.ctx.lib.tpst_gens_free(self.handle)
