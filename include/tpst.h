@@ -97,6 +97,8 @@ int tpst_g1_msm_batch_dev(tpst_ctx* ctx, const tpst_gens* gens, const void* d_sc
  * generator set (tpst_gens_load). */
 int tpst_gens_new(tpst_ctx* ctx, size_t n, const uint8_t* label, size_t label_len, uint64_t* G_out,
                   uint64_t* h_out, tpst_gens** out);
+/* its n + 1 32-byte StdRng seeds (host only; the squeezed sponge bytes) */
+int tpst_gens_seeds(size_t n, const uint8_t* label, size_t label_len, uint8_t* seeds);
 /* PedersenCommit::commit_slice (commitments.rs:79-86): msm(G, scalars) + h * blind;
  * n must equal gens->n (the reference assert_eq!s, here TPST_E_ARG). */
 int tpst_pedersen_commit_slice(tpst_ctx* ctx, const tpst_gens* gens, const uint64_t* scalars, size_t n,

@@ -145,3 +145,18 @@ def test_gens_oracle_points_valid():
     for p in G + [h]:
         assert O.g1_on_curve(p) and O.g1_in_subgroup(p)
     assert len(set(G + [h])) == 4
+
+
+def test_gens_seeds_match_oracle():
+    """Host Poseidon<Fr> sponge of tpst_gens_new (no GPU) vs oracle/py/gens.py."""
+    import ctypes as C
+    import gens as GN
+    from serialize import ser_g1
+    from testudo_amd import _lib
+    for n, label in ((3, b"gens_test"), (0, b""), (40, b"gens_pc")):
+        buf = C.create_string_buffer(32 * (n + 1))
+        assert _lib.load().tpst_gens_seeds(n, label, len(label), buf) == 0
+        sp = GN.FrSponge()
+        sp.absorb_bytes(label)
+        sp.absorb_bytes(ser_g1(O.G1_GEN))
+        assert buf.raw == b"".join(sp.squeeze_bytes(32) for _ in range(n + 1))

@@ -32,6 +32,7 @@ PROTOTYPES = [
     ("tpst_gens_load", C.c_int, [_vp, _u64p, _sz, _u64p, C.POINTER(_vp)]),
     ("tpst_gens_free", None, [_vp]),
     ("tpst_gens_new", C.c_int, [_vp, _sz, C.c_char_p, _sz, _u64p, _u64p, C.POINTER(_vp)]),
+    ("tpst_gens_seeds", C.c_int, [_sz, C.c_char_p, _sz, C.c_char_p]),
     ("tpst_g1_msm_batch", C.c_int, [_vp, _vp, _u64p, _sz, _sz, _sz, _sz, _u64p]),
     ("tpst_g1_msm_batch_dev", C.c_int, [_vp, _vp, _vp, _sz, _sz, _sz, _sz, _vp]),
     ("tpst_pedersen_commit_slice", C.c_int, [_vp, _vp, _u64p, _sz, _u64p, _u64p]),

@@ -231,7 +231,7 @@ __device__ int cmp_canon(const Fq& a, const Fq& b) {
 }
 
 // G1 cofactor (x - 1)^2 / 3 = 0x170b5d44300000000000000000000000 (125 bits)
-__constant__ uint32_t G1_COFACTOR[4] = {0x00000000u, 0x00000000u, 0x00000000u, 0x170b5d44u};
+__constant__ uint32_t G1_COFACTOR[4] = {0x00000000u, 0x00000000u, 0x30000000u, 0x170b5d44u};
 
 // one lane per generator: Affine::rand over ChaCha12(seed); canonical x || y out
 __global__ void __launch_bounds__(64) k_gens_from_seeds(const uint8_t* __restrict__ seeds, size_t n, SqrtConsts K,
@@ -319,17 +319,28 @@ void g1_gen_compressed(uint8_t* b) {
 
 }  // namespace
 
-extern "C" int tpst_gens_new(tpst_ctx* ctx, size_t n, const uint8_t* label, size_t label_len, uint64_t* G_out,
-                             uint64_t* h_out, tpst_gens** out) {
-  if (!ctx || !G_out || !h_out || (label_len && !label)) return fail(ctx, TPST_E_ARG, "null argument");
-  if (n == 0 || n > ((size_t)1 << 26)) return fail(ctx, TPST_E_ARG, "n out of range");
+// the n + 1 StdRng seeds of MultiCommitGens::new (host only)
+static void gens_seeds(size_t n, const uint8_t* label, size_t label_len, uint8_t* seeds) {
   FrSponge sp;
   sp.absorb_bytes(label, label_len);
   uint8_t gb[48];
   g1_gen_compressed(gb);
   sp.absorb_bytes(gb, 48);
+  for (size_t i = 0; i <= n; i++) sp.squeeze32(seeds + 32 * i);
+}
+
+extern "C" int tpst_gens_seeds(size_t n, const uint8_t* label, size_t label_len, uint8_t* seeds) {
+  if (!seeds || (label_len && !label)) return TPST_E_ARG;
+  gens_seeds(n, label, label_len, seeds);
+  return TPST_OK;
+}
+
+extern "C" int tpst_gens_new(tpst_ctx* ctx, size_t n, const uint8_t* label, size_t label_len, uint64_t* G_out,
+                             uint64_t* h_out, tpst_gens** out) {
+  if (!ctx || !G_out || !h_out || (label_len && !label)) return fail(ctx, TPST_E_ARG, "null argument");
+  if (n == 0 || n > ((size_t)1 << 26)) return fail(ctx, TPST_E_ARG, "n out of range");
   std::vector<uint8_t> seeds(32 * (n + 1));
-  for (size_t i = 0; i <= n; i++) sp.squeeze32(&seeds[32 * i]);
+  gens_seeds(n, label, label_len, seeds.data());
   static const SqrtConsts K = sqrt_consts();
   std::vector<uint64_t> pts(12 * (n + 1));
   {
