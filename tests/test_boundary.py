@@ -193,3 +193,23 @@ def test_gens_new_matches_oracle(ctx, n, label):
     # the loaded set commits like commit_slice over the same points
     s, _ = orc.fr_stream(5, n)
     assert np.array_equal(g.msm_batch(s, 1, 0, 1)[0], orc.g1_msm(g.G, s))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ell", [5, 8])
+def test_dense_commit_hyrax(ctx, ell):
+    """DensePolynomial::commit (dense_mlpoly.rs:349-377) over generators from
+    MultiCommitGens::new: rows of 2^(ell - ell/2), zero and random blinds."""
+    from testudo_amd.engine import Gens, dense_commit
+    L, Rn = 1 << (ell // 2), 1 << (ell - ell // 2)
+    g = Gens.new(ctx, Rn, b"gens_dense")
+    Z, _ = orc.fr_stream(900 + ell, 1 << ell)
+    got = dense_commit(g, Z)
+    for i in range(L):
+        assert np.array_equal(got[i], orc.g1_msm(g.G, Z[Rn * i:Rn * (i + 1)]))
+    bl, _ = orc.fr_stream(950 + ell, L)
+    got = dense_commit(g, Z, bl)
+    for i in range(L):
+        row = np.concatenate([g.G, g.h[None, :]])
+        sc = np.concatenate([Z[Rn * i:Rn * (i + 1)], bl[i:i + 1]])
+        assert np.array_equal(got[i], orc.g1_msm(row, sc))

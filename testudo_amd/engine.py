@@ -206,3 +206,21 @@ class Gens:
         self.ctx.check(self.ctx.lib.tpst_pedersen_commit_rows(self.ctx.h, self.handle, ptr(Z), len(Z), ptr(blinds),
                                                               len(blinds), ptr(out)), "commit_inner")
         return out
+
+
+def dense_commit(gens: Gens, Z: np.ndarray, blinds: np.ndarray = None) -> np.ndarray:
+    """DensePolynomial::commit (dense_mlpoly.rs:349-377), the Hyrax commitment:
+    ell = log2 |Z|, L = 2^(ell/2) rows of R = 2^(ell - ell/2) contiguous
+    evaluations, row i -> commit_slice(Z[R i .. R (i+1)], blinds[i]) with
+    gens.n == R; blinds default to zero (random_blinds = false, as in
+    Derefs::commit sparse_mlpoly.rs:75-81 and SparseMatPolynomial::multi_commit)."""
+    Z = np.ascontiguousarray(Z, dtype=np.uint64).reshape(-1, 4)
+    ell = len(Z).bit_length() - 1
+    if len(Z) != 1 << ell:
+        raise TpstError("|Z| must be a power of two")
+    L, R = 1 << (ell // 2), 1 << (ell - ell // 2)
+    if gens.n != R:
+        raise TpstError("gens.n must be 2^(ell - ell/2)")
+    if blinds is None:
+        blinds = np.zeros((L, 4), dtype=np.uint64)
+    return gens.commit_rows(Z, blinds)
