@@ -248,8 +248,70 @@ TPST_HD Fp<C> mul(const Fp<C>& a, const Fp<C>& b) {
 #endif
 }
 
+// Montgomery square: the same product scanning as mul, with each column's
+// cross products a_i a_j (i < j) taken once in a side accumulator that is
+// doubled before joining the column, plus the diagonal a_i^2 -- N (N + 1) / 2
+// limb products instead of N^2 before the reduction (78 of 144 for Fq).
 template <class C>
-TPST_HD Fp<C> sqr(const Fp<C>& a) { return mul(a, a); }
+TPST_HD Fp<C> sqr(const Fp<C>& a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  constexpr int N = C::N;
+  uint32_t m[N], t[N];
+  uint64_t acc = 0;
+  uint32_t hi = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; k++) {
+    uint64_t cacc = 0;
+    uint32_t chi = 0;
+    bool any = false;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      const int j = k - i;
+      if (i < j && j < N) {
+        mac_vv(cacc, chi, a.v[i], a.v[j]);
+        any = true;
+      }
+    }
+    if (any) {  // column += 2 * cross (a compile-time branch: loops are unrolled)
+      chi = (chi << 1) | (uint32_t)(cacc >> 63);
+      cacc <<= 1;
+      const uint64_t s2 = acc + cacc;
+      hi += chi + (s2 < acc ? 1u : 0u);
+      acc = s2;
+    }
+    if ((k & 1) == 0 && (k >> 1) < N) mac_vv(acc, hi, a.v[k >> 1], a.v[k >> 1]);
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      const int j = k - i;
+      if (i < k && j >= 1 && j < N) mac_vs(acc, hi, m[i], C::p(j));
+    }
+    if (k < N) {
+      if constexpr (C::P0_IS_ONE) {
+        const uint32_t lo = (uint32_t)acc;
+        m[k] = 0u - lo;
+        acc = ((acc >> 32) | ((uint64_t)hi << 32)) + (lo != 0u ? 1u : 0u);
+        hi = 0;
+        continue;
+      } else {
+        m[k] = (uint32_t)acc * C::INV;
+        mac_vs(acc, hi, m[k], C::p(0));
+      }
+    } else {
+      t[k - N] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+  t[N - 1] = (uint32_t)acc;
+  Fp<C> r;
+#pragma unroll
+  for (int j = 0; j < N; j++) r.v[j] = t[j];
+  reduce_once(r);
+  return r;
+#else
+  return mul(a, a);
+#endif
+}
 
 template <class C>
 TPST_HD Fp<C> to_mont(const Fp<C>& a) {  // canonical -> Montgomery
