@@ -265,6 +265,8 @@ def test_commit_homomorphism_n23_long_chunks(ctx):
     C = 1 << (n // 2)
     for i in (0, 1, 1000, C - 1):
         assert np.array_equal(comms[i], ctx.g1_msm(pg0, Z[i::C])), i
+    for i in (1, C - 1):  # and against the CPU oracle (not only HIP vs HIP)
+        assert np.array_equal(comms[i], orc.g1_msm(pg0, np.ascontiguousarray(Z[i::C]), parallel=True)), i
     del pl
 
 

@@ -34,11 +34,20 @@ static inline int num_windows(int c) { return num_windows_bits(c, 254); }
 // largest in [5, 8] that still leaves >= TPST_ACC_WAVES (default 8) waves per
 // SIMD.  Long chunks matter for the batch commit, whose buckets (~44 entries
 // at 2^24) would otherwise nearly all straddle chunk boundaries.
+// SIMDs of the current device (4 per CU on CDNA)
+static size_t device_simds() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;  // MI355X
+  return (size_t)cus * 4;
+}
+
 static int acc_chunk_lg(size_t m) {
   static const size_t threads = [] {
     const char* e = getenv("TPST_ACC_WAVES");
     const int w = e ? atoi(e) : 0;
-    return (size_t)(w > 0 ? w : 8) * 64 * 1024;  // 1024 SIMDs (256 CUs x 4)
+    return (size_t)(w > 0 ? w : 8) * 64 * device_simds();
   }();
   int lg = 5;
   while (lg < 8 && (m >> (lg + 1)) >= threads) lg++;
@@ -723,8 +732,9 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
       const char* e = getenv("TPST_MSM_LG");
       return e ? atoi(e) : 0;
     }();
+    static const size_t simds = device_simds();
     lg = 4;
-    while (lg < 8 && ((m / NG) >> (lg + 1)) >= (size_t)4 * 64 * 1024) lg++;
+    while (lg < 8 && ((m / NG) >> (lg + 1)) >= (size_t)4 * 64 * simds) lg++;
     if (env_lg >= 3 && env_lg <= 8) lg = env_lg;
   } else {
     lg = acc_chunk_lg(m);

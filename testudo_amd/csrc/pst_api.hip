@@ -546,6 +546,10 @@ extern "C" int tpst_srs_export(tpst_ctx* ctx, uint64_t* flat) {
 }
 
 // ============================================================ transcript ==
+// internal (r1cs.hip): the device copy of a whole polynomial's evaluations
+// (canonical Fr, original order), or nullptr for a column shard
+const uint32_t* tpst_internal_poly_evals(const tpst_poly* p) { return p && !p->ncols ? p->d_Z : nullptr; }
+
 extern "C" void tpst_transcript_init(tpst_transcript* t) {
   if (!t) return;
   memset(t, 0, sizeof *t);

@@ -24,6 +24,8 @@
 
 using namespace tpst;
 
+const uint32_t* tpst_internal_poly_evals(const tpst_poly* p);  // pst_api.hip
+
 #define TPST_TRY_HIP(x)                \
   do {                                 \
     hipError_t _e = (x);               \
@@ -304,6 +306,14 @@ struct tpst_r1cs {
   size_t nnz[3] = {0, 0, 0};
   Buf rptr[3], ridx[3], rval[3];  // CSR over rows (multiply_vec)
   Buf cptr[3], cidx[3], cval[3];  // CSC over the 2 num_vars columns of z (eval table)
+  void* pin = nullptr;            // 4 KiB pinned host staging of the sum-check rounds
+  void* pinned() {
+    if (!pin && hipHostMalloc(&pin, 4096, hipHostMallocDefault) != hipSuccess) pin = nullptr;
+    return pin;
+  }
+  ~tpst_r1cs() {
+    if (pin) (void)hipHostFree(pin);
+  }
 };
 
 // CSR (by key = rows) or CSC (by key = cols) of one matrix from device triples
@@ -426,7 +436,7 @@ extern "C" void tpst_r1cs_free(tpst_r1cs* r) { delete r; }
 // one sum-check (K = 4 cubic with additive term, K = 2 quad) over device
 // tables of length 2^rounds; transcript on the host between rounds
 template <int K>
-static int sumcheck(tpst_ctx* ctx, uint32_t* const* tabs, int rounds, Fr claim, tpst_transcript* tr,
+static int sumcheck(tpst_ctx* ctx, void* pin, uint32_t* const* tabs, int rounds, Fr claim, tpst_transcript* tr,
                     uint64_t* polys, Fr* rs, Fr* finals) {
   hipStream_t s = ctx->stream;
   const size_t n0 = (size_t)1 << rounds;
@@ -435,6 +445,11 @@ static int sumcheck(tpst_ctx* ctx, uint32_t* const* tabs, int rounds, Fr claim, 
   TPST_HIP(ctx, partial.alloc(nblk0 * 3 * 32));
   TPST_HIP(ctx, sums.alloc(3 * 32));
   TPST_HIP(ctx, dr.alloc(32));
+  // pinned staging (the instance's, allocated once): the round sums down, the
+  // challenge up -- one round trip per round
+  if (!pin) return fail(ctx, TPST_E_HIP, "hipHostMalloc");
+  uint64_t(*hs)[4] = reinterpret_cast<uint64_t(*)[4]>(pin);
+  uint32_t* rpin = reinterpret_cast<uint32_t*>((char*)pin + 1024);
   uint32_t* t[4] = {tabs[0], tabs[1], K == 4 ? tabs[2] : nullptr, K == 4 ? tabs[3] : nullptr};
   Fr e = claim;
   constexpr int NC = K == 4 ? 4 : 3;  // coefficients per round polynomial
@@ -446,8 +461,7 @@ static int sumcheck(tpst_ctx* ctx, uint32_t* const* tabs, int rounds, Fr claim, 
     TPST_HIP(ctx, hipGetLastError());
     k_sc_reduce<<<1, SC_BS, 0, s>>>(partial.u(), nblk, sums.u());
     TPST_HIP(ctx, hipGetLastError());
-    uint64_t hs[3][4];
-    TPST_HIP(ctx, hipMemcpyAsync(hs, sums.p, sizeof(hs), hipMemcpyDeviceToHost, s));
+    TPST_HIP(ctx, hipMemcpyAsync(hs, sums.p, 96, hipMemcpyDeviceToHost, s));
     TPST_HIP(ctx, hipStreamSynchronize(s));
     // evals at 0, 1 (= e - eval(0)), 2, 3 (sumcheck.rs:127-128, 427)
     Fr ev[4] = {frc(hs[0]), Fr::zero(), frc(hs[1]), frc(hs[2])};
@@ -463,7 +477,8 @@ static int sumcheck(tpst_ctx* ctx, uint32_t* const* tabs, int rounds, Fr claim, 
     tpst_transcript_challenge(tr, rc);
     rs[j] = frc(rc);
     e = uni_eval(cs, NC, rs[j]);
-    TPST_HIP(ctx, hipMemcpyAsync(dr.p, rs[j].v, 32, hipMemcpyHostToDevice, s));
+    memcpy(rpin, rs[j].v, 32);
+    TPST_HIP(ctx, hipMemcpyAsync(dr.p, rpin, 32, hipMemcpyHostToDevice, s));
   }
   // bind the last challenge: length 2 -> 1; the finals are the tables' [0]
   k_sc_round<K><<<1, SC_BS, 0, s>>>(t[0], t[1], t[2], t[3], 1, dr.u(), 0, partial.u());
@@ -517,15 +532,15 @@ extern "C" int tpst_r1cs_prove(tpst_ctx* ctx, tpst_r1cs* R, const uint64_t* vars
     TPST_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
     const size_t M = R->num_cons, Nz = R->ncols;
-    Buf dvars, dins, z, ttau, tabs[4], dtau, drx, coef, abc;
-    TPST_HIP(ctx, dvars.alloc(R->num_vars * 32));
+    Buf dins, z, tabs[4], dtau, drx, coef, abc;
+    const uint32_t* d_vars = tpst_internal_poly_evals(pl);  // uploaded once, by from_evaluations
+    if (!d_vars) return fail(ctx, TPST_E_STATE, "witness polynomial not resident");
     TPST_HIP(ctx, dins.alloc(R->num_inputs * 32 + 32));
     TPST_HIP(ctx, z.alloc(Nz * 32));
     TPST_HIP(ctx, dtau.alloc(rx_n * 32));
     for (auto& b : tabs) TPST_HIP(ctx, b.alloc(M * 32));
-    TPST_HIP(ctx, hipMemcpyAsync(dvars.p, vars, R->num_vars * 32, hipMemcpyHostToDevice, s));
     if (R->num_inputs) TPST_HIP(ctx, hipMemcpyAsync(dins.p, inputs, R->num_inputs * 32, hipMemcpyHostToDevice, s));
-    k_make_z<<<grid_for(Nz, 256), 256, 0, s>>>(dvars.u(), R->num_vars, dins.u(), R->num_inputs, Nz, z.u());
+    k_make_z<<<grid_for(Nz, 256), 256, 0, s>>>(d_vars, R->num_vars, dins.u(), R->num_inputs, Nz, z.u());
     TPST_HIP(ctx, hipGetLastError());
     TPST_HIP(ctx, hipMemcpyAsync(dtau.p, tau.data(), rx_n * 32, hipMemcpyHostToDevice, s));
     k_eq_evals<<<grid_for(M, 256), 256, 0, s>>>(dtau.u(), rx_n, M, tabs[0].u());
@@ -536,7 +551,7 @@ extern "C" int tpst_r1cs_prove(tpst_ctx* ctx, tpst_r1cs* R, const uint64_t* vars
       TPST_HIP(ctx, hipGetLastError());
     }
     uint32_t* t4[4] = {tabs[0].u(), tabs[1].u(), tabs[2].u(), tabs[3].u()};
-    if (int rc = sumcheck<4>(ctx, t4, rx_n, Fr::zero(), tr, &out->sc1[0][0][0], rx.data(), fin1)) return rc;
+    if (int rc = sumcheck<4>(ctx, R->pinned(), t4, rx_n, Fr::zero(), tr, &out->sc1[0][0][0], rx.data(), fin1)) return rc;
     // claims_phase2 = (Az, Bz, Cz, Az Bz) at rx (r1csproof.rs:299-306)
     const Fr az = fin1[1], bz = fin1[2], cz = fin1[3];
     fr_copy_out(az, out->claims_phase2[0]);
@@ -569,7 +584,7 @@ extern "C" int tpst_r1cs_prove(tpst_ctx* ctx, tpst_r1cs* R, const uint64_t* vars
     k_eval_table<<<grid_for(Nz, 256), 256, 0, s>>>(csc, tabs[0].u(), coef.u(), Nz, abc.u());
     TPST_HIP(ctx, hipGetLastError());
     uint32_t* t2[2] = {z.u(), abc.u()};
-    if (int rc = sumcheck<2>(ctx, t2, ry_n, claim2, tr, &out->sc2[0][0][0], ry.data(), fin2)) return rc;
+    if (int rc = sumcheck<2>(ctx, R->pinned(), t2, ry_n, claim2, tr, &out->sc2[0][0][0], ry.data(), fin2)) return rc;
     fr_copy_out(fin2[0], out->claims_phase2_z_abc[0]);
     fr_copy_out(fin2[1], out->claims_phase2_z_abc[1]);
   }
