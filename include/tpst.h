@@ -249,6 +249,17 @@ int tpst_r1cs_synthetic(tpst_ctx* ctx, size_t num_cons, size_t num_vars, size_t 
                         tpst_r1cs** out, uint64_t* vars, uint64_t* inputs);
 void tpst_r1cs_free(tpst_r1cs* r);
 
+/* R1CSInstance::commit (r1csinstance.rs:313-344) = SparseMatPolynomial::
+ * multi_commit over (A, B, C) (sparse_mlpoly.rs:490-517): the SPARK dense
+ * representation (addresses, memory-checking read / audit timestamps, values)
+ * built on the device, comb_ops and comb_mem each committed with
+ * DensePolynomial::commit (Hyrax rows, zero blinds) over the generators of
+ * PolyCommitmentGens::setup(num_vars, label).  ops_rows / mem_rows receive the
+ * row counts (the G1 points of each PolyCommitment); with comm_ops or
+ * comm_mem NULL only the sizes are reported. */
+int tpst_r1cs_commit(tpst_ctx* ctx, tpst_r1cs* r1cs, const uint8_t* label, size_t label_len, uint64_t* comm_ops,
+                     size_t* ops_rows, uint64_t* comm_mem, size_t* mem_rows);
+
 #define TPST_R1CS_MAX_ROUNDS 48
 /* R1CSProof (r1csproof.rs:24-38) without the Groth16 part; canonical Fr.
  * sc1: cubic round polynomials (4 coefficients, constant first), sc2: quad

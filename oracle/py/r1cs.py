@@ -209,3 +209,58 @@ def r1cs_prove(mats, num_cons, num_vars, vars_, inputs, srs, tr):
             "claims_phase2": (az, bz, cz, az * bz % R), "sc2": p2, "ry": ry, "claims2": cl2,
             "r_abc": (r_A, r_B, r_C), "transcript_sat_state": sat_state, "eval_vars_at_ry": v,
             "U": U, "pst_proof": pst_proof, "mipp": mipp, "n_vars": n_vars}
+
+
+def spark_multi_commit(mats, num_cons, num_vars, label):
+    """R1CSInstance::commit (r1csinstance.rs:313-344) = SparseMatPolynomial::
+    multi_commit (sparse_mlpoly.rs:373-437, 490-517): dense representation
+    (sparse_to_dense_vecs, AddrTimestamps::new, DensePolynomial::merge) and two
+    DensePolynomial::commit (dense_mlpoly.rs:349-377, zero blinds) over
+    PolyCommitmentGens::setup's Hyrax generators (nizk/mod.rs:25-28: the first R
+    of MultiCommitGens::new(R + 1, label))."""
+    import gens as GN
+    nnz = max(len(M) for M in mats)
+    N = 1
+    while N < nnz:
+        N *= 2
+    vx, vy = log2(num_cons), log2(2 * num_vars)
+    cells = 1 << max(vx, vy)
+
+    def dense(M):
+        rows = [e[0] for e in M] + [0] * (N - len(M))
+        cols = [e[1] for e in M] + [0] * (N - len(M))
+        vals = [e[2] % R for e in M] + [0] * (N - len(M))
+        return rows, cols, vals
+
+    reps = [dense(M) for M in mats]
+
+    def timestamps(ops):
+        audit = [0] * cells
+        read = []
+        for inst in ops:
+            r = []
+            for a in inst:
+                r.append(audit[a])
+                audit[a] += 1
+            read.append(r)
+        return read, audit
+
+    row_ops = [r[0] for r in reps]
+    col_ops = [r[1] for r in reps]
+    row_read, row_audit = timestamps(row_ops)
+    col_read, col_audit = timestamps(col_ops)
+    comb_ops = sum(row_ops, []) + sum(row_read, []) + sum(col_ops, []) + sum(col_read, []) + sum([r[2] for r in reps], [])
+    size = 1
+    while size < len(comb_ops):
+        size *= 2
+    comb_ops += [0] * (size - len(comb_ops))
+    comb_mem = row_audit + col_audit
+
+    def hyrax(Z):
+        ell = log2(len(Z))
+        Lr, Rn = 1 << (ell // 2), 1 << (ell - ell // 2)
+        G, _ = GN.multi_commit_gens(Rn + 1, label)
+        return [O.g1_msm(G[:Rn], Z[Rn * i:Rn * (i + 1)]) for i in range(Lr)]
+
+    return hyrax(comb_ops), hyrax(comb_mem)
+

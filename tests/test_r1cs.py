@@ -189,3 +189,27 @@ def test_r1cs_prove_2p18_verifier_checks(ctx):
     for coef, M in zip((ra, rb, rc), mats):
         tot += coef * sum(ex[r] * ey[c] * val for r, c, val in M)
     assert abcr == tot % R
+
+
+@pytest.mark.gpu
+def test_r1cs_commit_spark_vs_oracle(ctx):
+    """R1CSInstance::commit (SPARK dense representation + Hyrax commitments of
+    comb_ops / comb_mem) against oracle/py/r1cs.py, synthetic and loaded
+    (shuffled, repeated cells) instances."""
+    from testudo_amd import r1cs as D
+    num_cons, num_vars, num_inputs = 16, 16, 3
+    inst, vars_, inputs = D.R1CSInstance.produce_synthetic_r1cs(ctx, num_cons, num_vars, num_inputs, 31)
+    mats, v, x = Q.synthetic_r1cs(num_cons, num_vars, num_inputs, 31)
+    ops, mem = inst.commit(b"gens_r1cs_eval")
+    r_ops, r_mem = Q.spark_multi_commit(mats, num_cons, num_vars, b"gens_r1cs_eval")
+    assert g1_from_array(ops) == r_ops and g1_from_array(mem) == r_mem
+    # general matrices: different nnz per matrix, entries in caller order
+    rng = np.random.default_rng(9)
+    A = [(int(rng.integers(16)), int(rng.integers(32)), int(rng.integers(1, 1000))) for _ in range(21)]
+    B = [(int(rng.integers(16)), int(rng.integers(32)), int(rng.integers(1, 1000))) for _ in range(7)]
+    Cm = [(3, 5, 7)]
+    enc = lambda M: [(r, c, fr_array([val])[0]) for (r, c, val) in M]  # noqa: E731
+    inst2 = D.R1CSInstance.new(ctx, 16, 16, 3, enc(A), enc(B), enc(Cm))
+    ops, mem = inst2.commit(b"lbl")
+    r_ops, r_mem = Q.spark_multi_commit((A, B, Cm), 16, 16, b"lbl")
+    assert g1_from_array(ops) == r_ops and g1_from_array(mem) == r_mem

@@ -79,6 +79,7 @@ PROTOTYPES = [
                                  C.POINTER(_vp)]),
     ("tpst_r1cs_synthetic", C.c_int, [_vp, _sz, _sz, _sz, C.c_uint64, C.POINTER(_vp), _u64p, _u64p]),
     ("tpst_r1cs_free", None, [_vp]),
+    ("tpst_r1cs_commit", C.c_int, [_vp, _vp, C.c_char_p, _sz, _u64p, C.POINTER(_sz), _u64p, C.POINTER(_sz)]),
     ("tpst_r1cs_prove", C.c_int, [_vp, _vp, _u64p, _u64p, _vp, _vp]),
     ("tpst_ser_g1", C.c_int, [_u64p, C.c_char_p]),
     ("tpst_ser_g2", C.c_int, [_u64p, C.c_char_p]),

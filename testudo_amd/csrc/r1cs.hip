@@ -239,6 +239,72 @@ __global__ void __launch_bounds__(SC_BS) k_sc_reduce(const uint32_t* __restrict_
   if (threadIdx.x < 3) store_f<Fr>(out + 8 * threadIdx.x, from_mont(sh[threadIdx.x][0]));
 }
 
+// ---------------------------------------------- SPARK dense representation --
+// (SparseMatPolynomial::multi_sparse_to_dense_rep, sparse_mlpoly.rs:358-437)
+// addresses of the batch's ops, instance after instance, each padded to N with
+// address 0 (sparse_to_dense_vecs); pos = position in that sequence
+__global__ void k_ops_addr(const uint32_t* __restrict__ a0, const uint32_t* __restrict__ a1,
+                           const uint32_t* __restrict__ a2, uint32_t n0, uint32_t n1, uint32_t n2, size_t N,
+                           uint32_t* __restrict__ addr, uint32_t* __restrict__ pos) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 3 * N) return;
+  const size_t b = i / N, e = i % N;
+  const uint32_t* src = b == 0 ? a0 : b == 1 ? a1 : a2;
+  const uint32_t nn = b == 0 ? n0 : b == 1 ? n1 : n2;
+  addr[i] = e < nn ? src[e] : 0u;
+  pos[i] = (uint32_t)i;
+}
+
+// over the stably sorted (addr, pos): the read timestamp of position pos is
+// its rank among the earlier accesses of the same cell (AddrTimestamps::new,
+// sparse_mlpoly.rs:227-261); the audit timestamp of a cell = its access count
+__global__ void k_timestamps(const uint32_t* __restrict__ skey, const uint32_t* __restrict__ spos, size_t m,
+                             uint32_t* __restrict__ read_ts, uint32_t* __restrict__ audit) {
+  const size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= m) return;
+  const uint32_t k = skey[s];
+  // segment start by binary search (the keys are sorted)
+  size_t lo = 0, hi = s;
+  while (lo < hi) {
+    const size_t mid = (lo + hi) >> 1;
+    if (skey[mid] < k)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  read_ts[spos[s]] = (uint32_t)(s - lo);
+  if (s + 1 == m || skey[s + 1] != k) audit[k] = (uint32_t)(s + 1 - lo);
+}
+
+// Fr (canonical) out[i] = small integer in[i]
+__global__ void k_u32_to_fr(const uint32_t* __restrict__ in, size_t n, uint32_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint4* o = reinterpret_cast<uint4*>(out + 8 * i);
+  o[0] = make_uint4(in[i], 0u, 0u, 0u);
+  o[1] = make_uint4(0u, 0u, 0u, 0u);
+}
+
+// padded values of instance b (canonical Fr) -> out[b N + e]
+__global__ void k_vals_padded(const uint32_t* __restrict__ v0, const uint32_t* __restrict__ v1,
+                              const uint32_t* __restrict__ v2, uint32_t n0, uint32_t n1, uint32_t n2, size_t N,
+                              uint32_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 3 * N) return;
+  const size_t b = i / N, e = i % N;
+  const uint32_t* src = b == 0 ? v0 : b == 1 ? v1 : v2;
+  const uint32_t nn = b == 0 ? n0 : b == 1 ? n1 : n2;
+  uint4* o = reinterpret_cast<uint4*>(out + 8 * i);
+  if (e < nn) {
+    const uint4* q = reinterpret_cast<const uint4*>(src + 8 * e);
+    o[0] = q[0];
+    o[1] = q[1];
+  } else {
+    o[0] = make_uint4(0u, 0u, 0u, 0u);
+    o[1] = o[0];
+  }
+}
+
 // ------------------------------------------------------ host Fr helpers ----
 Fr frc(const uint64_t* c) {  // canonical -> Montgomery
   Fr a;
@@ -306,6 +372,7 @@ struct tpst_r1cs {
   size_t nnz[3] = {0, 0, 0};
   Buf rptr[3], ridx[3], rval[3];  // CSR over rows (multiply_vec)
   Buf cptr[3], cidx[3], cval[3];  // CSC over the 2 num_vars columns of z (eval table)
+  Buf orow[3], ocol[3], oval[3];  // the entries in the caller's order (SPARK dense rep)
   void* pin = nullptr;            // 4 KiB pinned host staging of the sum-check rounds
   void* pinned() {
     if (!pin && hipHostMalloc(&pin, 4096, hipHostMallocDefault) != hipSuccess) pin = nullptr;
@@ -342,6 +409,15 @@ static hipError_t build_compressed(hipStream_t s, const uint32_t* key, const uin
 static int r1cs_from_device(tpst_ctx* ctx, tpst_r1cs* R, const uint32_t* const rows[3], const uint32_t* const cols[3],
                             const uint32_t* const vals[3]) {
   for (int m = 0; m < 3; m++) {
+    const size_t k = R->nnz[m];
+    TPST_HIP(ctx, R->orow[m].alloc(k * 4 + 4));
+    TPST_HIP(ctx, R->ocol[m].alloc(k * 4 + 4));
+    TPST_HIP(ctx, R->oval[m].alloc(k * 32 + 32));
+    if (k) {
+      TPST_HIP(ctx, hipMemcpyAsync(R->orow[m].p, rows[m], k * 4, hipMemcpyDeviceToDevice, ctx->stream));
+      TPST_HIP(ctx, hipMemcpyAsync(R->ocol[m].p, cols[m], k * 4, hipMemcpyDeviceToDevice, ctx->stream));
+      TPST_HIP(ctx, hipMemcpyAsync(R->oval[m].p, vals[m], k * 32, hipMemcpyDeviceToDevice, ctx->stream));
+    }
     TPST_HIP(ctx, build_compressed(ctx->stream, rows[m], cols[m], vals[m], R->nnz[m], R->num_cons, R->rptr[m],
                                    R->ridx[m], R->rval[m]));
     TPST_HIP(ctx, build_compressed(ctx->stream, cols[m], rows[m], vals[m], R->nnz[m], R->ncols, R->cptr[m],
@@ -599,5 +675,94 @@ extern "C" int tpst_r1cs_prove(tpst_ctx* ctx, tpst_r1cs* R, const uint64_t* vars
   const uint64_t* point = &out->ry[1][0];
   if (int rc = tpst_poly_eval(ctx, pl, point, out->eval_vars_at_ry)) return rc;
   if (int rc = tpst_poly_open(ctx, pl, tr, comms.data(), point, out->T, &out->open)) return rc;
+  return TPST_OK;
+}
+
+// R1CSInstance::commit -> SparseMatPolynomial::multi_commit over (A, B, C)
+// (r1csinstance.rs:313-344, sparse_mlpoly.rs:490-517): the SPARK dense
+// representation (row / col addresses and memory-checking timestamps, values)
+// built on the device, merged into comb_ops (16 N) and comb_mem (2 cells), each
+// committed with DensePolynomial::commit (Hyrax rows, zero blinds) over the
+// generators PolyCommitmentGens::setup(num_vars, label) derives
+// (DotProductProofGens: the first R of MultiCommitGens::new(R + 1, label)).
+extern "C" int tpst_r1cs_commit(tpst_ctx* ctx, tpst_r1cs* R, const uint8_t* label, size_t label_len,
+                                uint64_t* comm_ops, size_t* ops_rows, uint64_t* comm_mem, size_t* mem_rows) {
+  if (!ctx || !R || !ops_rows || !mem_rows || (label_len && !label)) return fail(ctx, TPST_E_ARG, "null argument");
+  size_t maxnz = 1;
+  for (int m = 0; m < 3; m++) maxnz = R->nnz[m] > maxnz ? R->nnz[m] : maxnz;
+  size_t N = 1;
+  while (N < maxnz) N <<= 1;
+  const int vx = log2_exact(R->num_cons), vy = log2_exact(R->ncols);
+  const int vmax = vx > vy ? vx : vy;
+  const size_t cells = (size_t)1 << vmax;
+  const int ell_ops = log2_exact(N) + 4, ell_mem = vmax + 1;  // batch 3: (3 * 5).next_power_of_two() = 16
+  const size_t L_ops = (size_t)1 << (ell_ops / 2), R_ops = (size_t)1 << (ell_ops - ell_ops / 2);
+  const size_t L_mem = (size_t)1 << (ell_mem / 2), R_mem = (size_t)1 << (ell_mem - ell_mem / 2);
+  *ops_rows = L_ops;
+  *mem_rows = L_mem;
+  if (!comm_ops || !comm_mem) return TPST_OK;  // size query
+  if (3 * N >= ((size_t)1 << 31)) return fail(ctx, TPST_E_ARG, "instance too large");
+  Buf ops, mem;
+  {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    TPST_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const size_t M3 = 3 * N;
+    TPST_HIP(ctx, ops.alloc(16 * N * 32));
+    TPST_HIP(ctx, mem.alloc(2 * cells * 32));
+    TPST_HIP(ctx, hipMemsetAsync(ops.p, 0, 16 * N * 32, s));
+    Buf addr, pos, skey, spos, rts, audit, tmp;
+    TPST_HIP(ctx, addr.alloc(M3 * 4));
+    TPST_HIP(ctx, pos.alloc(M3 * 4));
+    TPST_HIP(ctx, skey.alloc(M3 * 4));
+    TPST_HIP(ctx, spos.alloc(M3 * 4));
+    TPST_HIP(ctx, rts.alloc(M3 * 4));
+    TPST_HIP(ctx, audit.alloc(cells * 4));
+    size_t sb = 0;
+    TPST_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, sb, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                     (uint32_t*)nullptr, (uint32_t*)nullptr, (int)M3, 0, vmax + 1, s));
+    TPST_HIP(ctx, tmp.alloc(sb));
+    for (int rc = 0; rc < 2; rc++) {  // rows, then columns
+      const Buf* o = rc ? R->ocol : R->orow;
+      k_ops_addr<<<grid_for(M3, 256), 256, 0, s>>>(o[0].u(), o[1].u(), o[2].u(), (uint32_t)R->nnz[0],
+                                                   (uint32_t)R->nnz[1], (uint32_t)R->nnz[2], N, addr.u(), pos.u());
+      TPST_HIP(ctx, hipGetLastError());
+      TPST_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(tmp.p, sb, addr.u(), skey.u(), pos.u(), spos.u(), (int)M3, 0,
+                                                       vmax + 1, s));
+      TPST_HIP(ctx, hipMemsetAsync(audit.p, 0, cells * 4, s));
+      k_timestamps<<<grid_for(M3, 256), 256, 0, s>>>(skey.u(), spos.u(), M3, rts.u(), audit.u());
+      TPST_HIP(ctx, hipGetLastError());
+      // comb_ops segments: row.ops_addr | row.read_ts | col.ops_addr | col.read_ts | val | 0
+      uint32_t* base = ops.u() + 8 * (size_t)(rc * 2) * M3;
+      k_u32_to_fr<<<grid_for(M3, 256), 256, 0, s>>>(addr.u(), M3, base);
+      k_u32_to_fr<<<grid_for(M3, 256), 256, 0, s>>>(rts.u(), M3, base + 8 * M3);
+      // comb_mem = row.audit_ts | col.audit_ts
+      k_u32_to_fr<<<grid_for(cells, 256), 256, 0, s>>>(audit.u(), cells, mem.u() + 8 * (size_t)rc * cells);
+      TPST_HIP(ctx, hipGetLastError());
+    }
+    k_vals_padded<<<grid_for(M3, 256), 256, 0, s>>>(R->oval[0].u(), R->oval[1].u(), R->oval[2].u(),
+                                                    (uint32_t)R->nnz[0], (uint32_t)R->nnz[1], (uint32_t)R->nnz[2], N,
+                                                    ops.u() + 8 * 4 * M3);
+    TPST_HIP(ctx, hipGetLastError());
+    TPST_HIP(ctx, hipStreamSynchronize(s));
+  }
+  // the two Hyrax commitments (the library calls below take the context lock)
+  struct Job {
+    const Buf* buf;
+    size_t L, Rn;
+    uint64_t* out;
+  } jobs[2] = {{&ops, L_ops, R_ops, comm_ops}, {&mem, L_mem, R_mem, comm_mem}};
+  for (const Job& j : jobs) {
+    std::vector<uint64_t> G((j.Rn + 1) * 12), h(12);
+    if (int rc = tpst_gens_new(ctx, j.Rn + 1, label, label_len, G.data(), h.data(), nullptr)) return rc;
+    tpst_gens* gens = nullptr;
+    if (int rc = tpst_gens_load(ctx, G.data(), j.Rn, h.data(), &gens)) return rc;
+    std::unique_ptr<tpst_gens, void (*)(tpst_gens*)> gg(gens, tpst_gens_free);
+    Buf dout;
+    TPST_HIP(ctx, dout.alloc(j.L * 96));
+    if (int rc = tpst_g1_msm_batch_dev(ctx, gens, j.buf->p, j.L, j.Rn, j.Rn, 1, dout.p)) return rc;
+    TPST_HIP(ctx, hipMemcpyAsync(j.out, dout.p, j.L * 96, hipMemcpyDeviceToHost, ctx->stream));
+    TPST_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  }
   return TPST_OK;
 }

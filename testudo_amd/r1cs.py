@@ -76,6 +76,19 @@ class R1CSInstance:
                                               ptr(inputs)), "tpst_r1cs_synthetic")
         return cls(ctx, h, num_cons, num_vars, num_inputs), vars_, inputs[:num_inputs]
 
+    def commit(self, label: bytes):
+        """R1CSInstance::commit (r1csinstance.rs:313-344): SparseMatPolynomial::
+        multi_commit over (A, B, C) -> (comm_comb_ops, comm_comb_mem) G1 rows."""
+        ctx = self.ctx
+        n_ops, n_mem = C.c_size_t(0), C.c_size_t(0)
+        ctx.check(ctx.lib.tpst_r1cs_commit(ctx.h, self.h, bytes(label), len(label), None, C.byref(n_ops), None,
+                                           C.byref(n_mem)), "tpst_r1cs_commit")
+        ops = np.zeros((n_ops.value, 12), dtype=np.uint64)
+        mem = np.zeros((n_mem.value, 12), dtype=np.uint64)
+        ctx.check(ctx.lib.tpst_r1cs_commit(ctx.h, self.h, bytes(label), len(label), ptr(ops), C.byref(n_ops),
+                                           ptr(mem), C.byref(n_mem)), "tpst_r1cs_commit")
+        return ops, mem
+
     def __del__(self):
         try:
             if self.h:
