@@ -359,6 +359,9 @@ def pst_leg(ctx, log_n, reps=5):
                     "SRS tables built in srs_setup"}
 
 
+_R1CS_LAST = None
+
+
 def r1cs_leg(ctx, log_cons, reps=3):
     """R1CSProof::prove (r1csproof.rs:237-370, Groth16 step excluded) on a
     synthetic 2^log_cons-constraint instance with as many variables: the live
@@ -383,6 +386,8 @@ def r1cs_leg(ctx, log_cons, reps=3):
     ops, mem = inst.commit(b"gens_r1cs_eval")
     commit_s = time.perf_counter() - t
     from testudo_amd.encoding import limbs_to_int
+    global _R1CS_LAST
+    _R1CS_LAST = {"log_cons": log_cons, "seed": SEED + 7, "proof": proof}
     R = 0x12AB655E9A2CA55660B44D1E5C37B00159AA76FED00000010A11800000000001
     az, bz, cz, azbz = [limbs_to_int(x) for x in proof.claims_phase2]
     return {"num_cons": n_cons, "num_vars": n_vars, "num_inputs": 10, "prove_s": round(sorted(times[1:])[reps // 2], 4),
@@ -527,6 +532,28 @@ def cpu_leg(ctx, bk, sc, gpu_out, result):
                                   "sample": "256 of 4096 row MSMs (4096 points each) + their Miller loops, x16"}
     except Exception as e:  # the headline CPU line must survive
         res["pst_error"] = repr(e)
+    # R1CSProof::prove's sum-check section on the CPU (oracle/cpu, OpenMP) from
+    # the GPU proof's T on: same transcript, so rx / ry must match exactly
+    try:
+        if _R1CS_LAST is not None:
+            lc, pr = _R1CS_LAST["log_cons"], _R1CS_LAST["proof"]
+            t = time.perf_counter()
+            cpu = orc.r1cs_sumchecks(1 << lc, 1 << lc, 10, _R1CS_LAST["seed"], pr.T)
+            sc_s = time.perf_counter() - t
+            pst = res.get("pst", {})
+            rr = {"num_cons": 1 << lc, "sumchecks_s": round(sc_s, 3), "cores": threads,
+                  "matches_gpu": bool(np.array_equal(cpu["rx"], pr.rx) and np.array_equal(cpu["ry"], pr.ry)
+                                      and np.array_equal(cpu["sc1"], pr.sc_proof_phase1)
+                                      and np.array_equal(cpu["sc2"], pr.sc_proof_phase2)),
+                  "sample": "full 2^%d-constraint sum-checks (eq tables, mat-vecs, phase one + two); prove_s = "
+                            "this + the CPU 2^20 commit + open of the pst leg (same witness size)" % lc}
+            if pst.get("commit_s") is not None and lc == 20:
+                rr["prove_s"] = round(sc_s + pst["commit_s"] + pst["open_s"], 3)
+                g = result.get("r1cs", {}).get("prove_s")
+                rr["gpu_speedup"] = round(rr["prove_s"] / g, 1) if g else None
+            res["r1cs"] = rr
+    except Exception as e:
+        res["r1cs_error"] = repr(e)
     return res
 
 

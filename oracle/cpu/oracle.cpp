@@ -1177,3 +1177,207 @@ int orc_pst_verify(const orc_srs* s, int n, const u64* point, const u64* v_in, c
 }
 
 }  // extern "C"
+
+// ----------------------------------------------------------------- R1CS ---
+// R1CSProof::prove between the witness commitment and the PST opening
+// (r1csproof.rs:248-340): synthetic instance (r1csinstance.rs:166-242 over the
+// seeded stream), the transcript from T on, EqPolynomial tables, multiply_vec,
+// the phase-one cubic and phase-two quad sum-checks (sumcheck.rs:67-148,
+// 387-444), compute_eval_table_sparse; OpenMP over the table loops.  The
+// bench's R1CS CPU leg and a checker of csrc/r1cs.hip.
+namespace {
+std::vector<Fr> eq_table(const std::vector<Fr>& r) {  // dense_mlpoly.rs:231-250
+  std::vector<Fr> e(size_t(1) << r.size(), Fr::one());
+  size_t size = 1;
+  for (size_t j = 0; j < r.size(); j++) {
+    size *= 2;
+    for (size_t i = size - 1; i >= 1; i -= 2) {
+      Fr s = e[i / 2];
+      e[i] = s * r[j];
+      e[i - 1] = s - e[i];
+      if (i == 1) break;
+    }
+  }
+  return e;
+}
+
+Fr fr_small(u64 v) {
+  u64 l[4] = {v, 0, 0, 0};
+  return Fr::from_canon(l);
+}
+
+void from_evals(const Fr* e, int n, Fr* cs) {  // unipoly.rs:15-45
+  static const Fr i2 = fr_small(2).inv(), i6 = fr_small(6).inv();
+  if (n == 3) {
+    Fr c = e[0], a = i2 * (e[2] - e[1] - e[1] + c);
+    cs[0] = c;
+    cs[1] = e[1] - c - a;
+    cs[2] = a;
+    return;
+  }
+  Fr d = e[0];
+  Fr a = i6 * (e[3] - fr_small(3) * e[2] + fr_small(3) * e[1] - e[0]);
+  Fr b = i2 * (e[0] + e[0] - fr_small(5) * e[1] + fr_small(4) * e[2] - e[3]);
+  cs[0] = d;
+  cs[1] = e[1] - d - a - b;
+  cs[2] = b;
+  cs[3] = a;
+}
+
+Fr uni_eval(const Fr* cs, int n, const Fr& r) {
+  Fr out = cs[0], pw = r;
+  for (int i = 1; i < n; i++) {
+    out = out + pw * cs[i];
+    pw = pw * r;
+  }
+  return out;
+}
+
+void append_fr(Poseidon& tr, const Fr& x) {  // append_scalar: one Fq of the same value
+  u64 c[4], l[6] = {0, 0, 0, 0, 0, 0};
+  x.to_canon(c);
+  memcpy(l, c, 32);
+  tr.absorb_elems({Fq::from_canon(l)});
+}
+
+void reset_fr(Poseidon& tr, const Fr& x) {  // new_from_state2
+  tr = make_poseidon(g_ark.data(), g_mds.data());
+  u64 c[4];
+  x.to_canon(c);
+  tr.absorb_bytes((const uint8_t*)c, 32);
+}
+
+// K = 4: tau (A B - C); K = 2: A B.  Tables are consumed (bound in place).
+template <int K>
+void sumcheck(std::vector<Fr>* t, int rounds, Fr e, Poseidon& tr, u64* polys, std::vector<Fr>& rs) {
+  const int NC = K == 4 ? 4 : 3;
+  for (int j = 0; j < rounds; j++) {
+    const size_t n = t[0].size() / 2;
+    Fr s0 = Fr::zero(), s2 = Fr::zero(), s3 = Fr::zero();
+#pragma omp parallel
+    {
+      Fr a0 = Fr::zero(), a2 = Fr::zero(), a3 = Fr::zero();
+#pragma omp for schedule(static)
+      for (long long i = 0; i < (long long)n; i++) {
+        Fr lo[K], p[K], q[K];
+        for (int k = 0; k < K; k++) {
+          lo[k] = t[k][i];
+          const Fr d = t[k][n + i] - lo[k];
+          p[k] = t[k][n + i] + d;
+          q[k] = p[k] + d;
+        }
+        if (K == 4) {
+          a0 = a0 + lo[0] * (lo[1] * lo[2] - lo[3]);
+          a2 = a2 + p[0] * (p[1] * p[2] - p[3]);
+          a3 = a3 + q[0] * (q[1] * q[2] - q[3]);
+        } else {
+          a0 = a0 + lo[0] * lo[1];
+          a2 = a2 + p[0] * p[1];
+        }
+      }
+#pragma omp critical
+      {
+        s0 = s0 + a0;
+        s2 = s2 + a2;
+        s3 = s3 + a3;
+      }
+    }
+    Fr ev[4] = {s0, e - s0, s2, s3}, cs[4];
+    from_evals(ev, NC, cs);
+    for (int c = 0; c < NC; c++) {
+      cs[c].to_canon(polys + 4 * ((size_t)j * NC + c));
+      append_fr(tr, cs[c]);
+    }
+    const Fr r = tr.challenge();
+    rs.push_back(r);
+    e = uni_eval(cs, NC, r);
+    for (int k = 0; k < K; k++) {
+#pragma omp parallel for schedule(static)
+      for (long long i = 0; i < (long long)n; i++) t[k][i] = t[k][i] + r * (t[k][n + i] - t[k][i]);
+      t[k].resize(n);
+    }
+  }
+}
+}  // namespace
+
+extern "C" int orc_r1cs_sumchecks(size_t num_cons, size_t num_vars, size_t num_inputs, u64 seed, const u64* T,
+                                  u64* sc1, u64* sc2, u64* rx_out, u64* ry_out, u64* claims, u64* sat_state) {
+  if (g_ark.empty()) return -2;
+  const size_t sz = num_vars + num_inputs + 1;
+  std::vector<u64> zc(4 * sz);
+  orc_fr_stream(seed, sz, 0, zc.data());
+  std::vector<Fr> Z(sz);
+  for (size_t i = 0; i < sz; i++) Z[i] = fr_in(&zc[4 * i]);
+  Z[num_vars] = Fr::one();
+  // C values Z[a] Z[b] / Z[c]: one batch inversion (Montgomery's trick)
+  std::vector<Fr> den(num_cons), pre(num_cons);
+  Fr acc = Fr::one();
+  for (size_t i = 0; i < num_cons; i++) {
+    Fr zc3 = Z[(i + 3) % sz];
+    den[i] = zc3.is_zero() ? Fr::one() : zc3;
+    pre[i] = acc;
+    acc = acc * den[i];
+  }
+  Fr inv = acc.inv();
+  std::vector<Fr> cval(num_cons);
+  std::vector<size_t> ccol(num_cons);
+  for (size_t ii = num_cons; ii-- > 0;) {
+    const Fr di = inv * pre[ii];
+    inv = inv * den[ii];
+    const size_t a = ii % sz, b = (ii + 2) % sz, c = (ii + 3) % sz;
+    const Fr ab = Z[a] * Z[b];
+    if (Z[c].is_zero()) {
+      ccol[ii] = num_vars;
+      cval[ii] = ab;
+    } else {
+      ccol[ii] = c;
+      cval[ii] = ab * di;
+    }
+  }
+  // transcript from the witness commitment on (r1csproof.rs:256-283)
+  Poseidon tr = make_poseidon(g_ark.data(), g_mds.data());
+  tr.absorb_bytes((const uint8_t*)T, 576);
+  const Fr init = tr.challenge();
+  reset_fr(tr, init);
+  for (size_t i = 0; i < num_inputs; i++) append_fr(tr, Z[num_vars + 1 + i]);
+  const size_t nz = 2 * num_vars;
+  std::vector<Fr> z(nz, Fr::zero());
+  for (size_t i = 0; i <= num_vars + num_inputs; i++) z[i] = Z[i];
+  int rx_n = 0, ry_n = 0;
+  while ((size_t(1) << rx_n) < num_cons) rx_n++;
+  while ((size_t(1) << ry_n) < nz) ry_n++;
+  std::vector<Fr> tau(rx_n);
+  for (int j = 0; j < rx_n; j++) tau[j] = tr.challenge();
+  std::vector<Fr> t4[4];
+  t4[0] = eq_table(tau);
+  for (int k = 1; k < 4; k++) t4[k].resize(num_cons);
+#pragma omp parallel for schedule(static)
+  for (long long i = 0; i < (long long)num_cons; i++) {
+    t4[1][i] = z[i % sz];
+    t4[2][i] = z[(i + 2) % sz];
+    t4[3][i] = z[ccol[i]] * cval[i];
+  }
+  std::vector<Fr> rx, ry;
+  sumcheck<4>(t4, rx_n, Fr::zero(), tr, sc1, rx);
+  const Fr az = t4[1][0], bz = t4[2][0], cz = t4[3][0];
+  az.to_canon(claims);
+  bz.to_canon(claims + 4);
+  cz.to_canon(claims + 8);
+  (az * bz).to_canon(claims + 12);
+  const Fr rA = tr.challenge(), rB = tr.challenge(), rC = tr.challenge();
+  const Fr claim2 = rA * az + rB * bz + rC * cz;
+  std::vector<Fr> ex = eq_table(rx);
+  std::vector<Fr> t2[2];
+  t2[0] = z;
+  t2[1].assign(nz, Fr::zero());
+  for (size_t i = 0; i < num_cons; i++) {  // compute_eval_table_sparse, combined
+    t2[1][i % sz] = t2[1][i % sz] + rA * ex[i];
+    t2[1][(i + 2) % sz] = t2[1][(i + 2) % sz] + rB * ex[i];
+    t2[1][ccol[i]] = t2[1][ccol[i]] + rC * ex[i] * cval[i];
+  }
+  sumcheck<2>(t2, ry_n, claim2, tr, sc2, ry);
+  for (int j = 0; j < rx_n; j++) rx[j].to_canon(rx_out + 4 * j);
+  for (int j = 0; j < ry_n; j++) ry[j].to_canon(ry_out + 4 * j);
+  tr.challenge().to_canon(sat_state);
+  return 0;
+}

@@ -59,6 +59,7 @@ def load():
         "orc_pst_commit": (i, [vp, _u64p, i, _u64p, _u64p]),
         "orc_pst_open": (i, [vp, _u64p, i, _u64p, _u64p] + [_u64p] * 7),
         "orc_pst_verify": (i, [vp, i] + [_u64p] * 10),
+        "orc_r1cs_sumchecks": (i, [sz, sz, sz, C.c_uint64, _u64p] + [_u64p] * 6),
     }
     for name, (res, args) in protos.items():
         f = getattr(lib, name)
@@ -218,3 +219,23 @@ def pst_verify(srs, n, point, v, proof, T):
          (point, v, proof["U"], proof["pst_proof"], proof["comms_t"], proof["comms_u"], proof["final_a"],
           proof["final_h"], proof["pst_proof_h"], T)]
     return lib.orc_pst_verify(srs.h, n, *[_p(x) for x in a]) == 1
+
+
+def r1cs_sumchecks(num_cons, num_vars, num_inputs, seed, T):
+    """R1CSProof::prove's sum-check section (r1csproof.rs:256-340) on the CPU,
+    from the witness commitment's T on -> dict of canonical limb arrays."""
+    lib = load()
+    rx_n = (num_cons - 1).bit_length()
+    ry_n = (2 * num_vars - 1).bit_length()
+    sc1 = np.zeros((rx_n, 4, 4), dtype=np.uint64)
+    sc2 = np.zeros((ry_n, 3, 4), dtype=np.uint64)
+    rx = np.zeros((rx_n, 4), dtype=np.uint64)
+    ry = np.zeros((ry_n, 4), dtype=np.uint64)
+    claims = np.zeros((4, 4), dtype=np.uint64)
+    sat = np.zeros(4, dtype=np.uint64)
+    T = np.ascontiguousarray(T, dtype=np.uint64).reshape(72)
+    rc = lib.orc_r1cs_sumchecks(num_cons, num_vars, num_inputs, seed, _p(T), _p(sc1), _p(sc2), _p(rx), _p(ry),
+                                _p(claims), _p(sat))
+    assert rc == 0
+    return {"sc1": sc1, "sc2": sc2, "rx": rx, "ry": ry, "claims_phase2": claims, "sat_state": sat}
+
