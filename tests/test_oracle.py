@@ -160,3 +160,20 @@ def test_gens_seeds_match_oracle():
         sp.absorb_bytes(label)
         sp.absorb_bytes(ser_g1(O.G1_GEN))
         assert buf.raw == b"".join(sp.squeeze_bytes(32) for _ in range(n + 1))
+
+
+def test_cpp_r1cs_sumchecks_match_python_oracle():
+    """oracle/cpu orc_r1cs_sumchecks (the bench's R1CS CPU leg) == oracle/py/r1cs.py."""
+    import r1cs as Q
+    num_cons, num_vars, ni, seed = 64, 16, 5, 1064
+    mats, v, x = Q.synthetic_r1cs(num_cons, num_vars, ni, seed)
+    out = Q.r1cs_prove(mats, num_cons, num_vars, v, x, P.SRS(2, 0x7E57D1), P.PoseidonTranscript())
+    T = np.zeros((12, 6), dtype=np.uint64)
+    for k, c in enumerate(O.fq12_to_tower(out["T"])):
+        T[k] = [(c >> (64 * q)) & (2 ** 64 - 1) for q in range(6)]
+    r = orc.r1cs_sumchecks(num_cons, num_vars, ni, seed, T.reshape(-1))
+    ints = lambda a: [limbs_to_int(z) for z in np.asarray(a).reshape(-1, 4)]  # noqa: E731
+    assert [ints(p) for p in r["sc1"]] == out["sc1"] and [ints(p) for p in r["sc2"]] == out["sc2"]
+    assert ints(r["rx"]) == out["rx"] and ints(r["ry"]) == out["ry"]
+    assert ints(r["claims_phase2"]) == list(out["claims_phase2"])
+    assert limbs_to_int(r["sat_state"]) == out["transcript_sat_state"]
