@@ -69,6 +69,7 @@ def parse():
     ap.add_argument("--sharded-log-n", type=int, default=24)
     ap.add_argument("--no-r1cs", action="store_true", help="skip the R1CSProof::prove leg")
     ap.add_argument("--r1cs-log-cons", type=int, default=20)
+    ap.add_argument("--no-groth16", action="store_true", help="skip the Groth16 prove leg")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the launcher / rendezvous / timing plumbing only (gloo)")
     return ap.parse_args()
@@ -305,6 +306,11 @@ def main():
             result["r1cs"] = r1cs_leg(ctx, args.r1cs_log_cons)
         except Exception as e:  # never lose the bench line to the secondary leg
             result["r1cs"] = {"error": repr(e)}
+    if not args.no_groth16 and world == 1:
+        try:
+            result["groth16"] = groth16_leg(ctx, args.r1cs_log_cons)
+        except Exception as e:  # never lose the bench line to the secondary leg
+            result["groth16"] = {"error": repr(e)}
     if not args.no_cpu and world == 1:
         result["cpu_baseline"] = cpu_leg(ctx, bk, sc, out, result)
     print(json.dumps(result), flush=True)
@@ -396,6 +402,38 @@ def r1cs_leg(ctx, log_cons, reps=3):
             "note": "R1CSProof::prove minus prove_verifier (Groth16): witness sqrt-PST commit, phase-one cubic and "
                     "phase-two quad sum-checks on the device, PST opening at ry[1..]; instance + SRS set up "
                     "before the timer"}
+
+
+def groth16_leg(ctx, log_cons, reps=3):
+    """Groth16::prove (r1csproof.rs:421, ark-groth16 LibsnarkReduction) over the
+    synthetic 2^log_cons-constraint R1CS instance with as many variables:
+    witness map (7 NTTs over the 2^(log_cons+1) domain) + four device MSMs
+    (A: G1, B: G2 and G1, C: G1 over L, H and the constants).  Key generation
+    before the timer; the proof checked by the pairing equation."""
+    from testudo_amd import groth16 as D
+    from testudo_amd import r1cs as S
+    from testudo_amd.encoding import fr_array
+    n_cons = n_vars = 1 << log_cons
+    inst, vars_, inputs = S.R1CSInstance.produce_synthetic_r1cs(ctx, n_cons, n_vars, 10, SEED + 7)
+    t = time.perf_counter()
+    pk = D.ProvingKey.setup(inst, fr_array([SEED + 11, SEED + 12, SEED + 13, SEED + 14, SEED + 15]))
+    ctx.synchronize()
+    setup_s = time.perf_counter() - t
+    r, s = fr_array([SEED + 21]), fr_array([SEED + 22])
+    times = []
+    for _ in range(reps + 1):
+        ctx.synchronize()
+        t = time.perf_counter()
+        proof = D.prove(pk, inst, vars_, inputs, r, s)
+        times.append(time.perf_counter() - t)
+    t = time.perf_counter()
+    ok = D.verify(ctx, pk.vk(), inputs, proof)
+    verify_s = time.perf_counter() - t
+    return {"num_cons": n_cons, "num_vars": n_vars, "num_inputs": 10, "domain": pk.domain_size,
+            "prove_s": round(sorted(times[1:])[reps // 2], 4), "first_call_s": round(times[0], 4), "reps": reps,
+            "setup_s": round(setup_s, 3), "verify_s": round(verify_s, 4), "verified": ok,
+            "note": "Groth16 prover of the R1CS instance itself (the reference proves its verifier circuit, "
+                    "constraints.rs, out of scope); toxic waste and (r, s) fixed; key generation before the timer"}
 
 
 def _wire_sizes(ctx, nv, pst_proof, mipp):

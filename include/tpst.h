@@ -286,6 +286,31 @@ typedef struct {
 int tpst_r1cs_prove(tpst_ctx* ctx, tpst_r1cs* r1cs, const uint64_t* vars, const uint64_t* inputs,
                     tpst_transcript* tr, tpst_r1cs_proof* out);
 
+/* ---- Groth16 over BLS12-377 (csrc/groth16.hip) ----
+ * The prover behind R1CSProof::prove_verifier (r1csproof.rs:374-434,
+ * Groth16::<E>::prove at :421): ark-groth16 create_proof with the
+ * LibsnarkReduction QAP, over any tpst_r1cs instance (variables in the
+ * Spartan z order: witness z[0..num_vars), instance (1, inputs)).  The
+ * reference's thread_rng draws are arguments here. */
+typedef struct tpst_groth16_pk tpst_groth16_pk;
+/* generate_random_parameters_with_reduction: toxic = (tau, alpha, beta,
+ * gamma, delta) canonical Fr (5 x 4 u64, nonzero, tau outside the domain).
+ * Keeps the proving key (query points) on the device. */
+int tpst_groth16_setup(tpst_ctx* ctx, tpst_r1cs* r1cs, const uint64_t* toxic, tpst_groth16_pk** out);
+void tpst_groth16_pk_free(tpst_groth16_pk* pk);
+/* QAP domain size n = next_pow2(num_cons + num_inputs + 1) */
+int tpst_groth16_domain(const tpst_groth16_pk* pk, size_t* n);
+/* VerifyingKey: alpha_g1 (12 u64), beta_g2 / gamma_g2 / delta_g2 (24 u64
+ * each), gamma_abc_g1 (num_inputs + 1 points), affine canonical */
+int tpst_groth16_vk(tpst_ctx* ctx, const tpst_groth16_pk* pk, uint64_t* alpha_g1, uint64_t* beta_g2,
+                    uint64_t* gamma_g2, uint64_t* delta_g2, uint64_t* gamma_abc_g1);
+/* LibsnarkReduction::witness_map: the first n - 1 coefficients of h (canonical) */
+int tpst_groth16_witness_map(tpst_ctx* ctx, tpst_groth16_pk* pk, tpst_r1cs* r1cs, const uint64_t* vars,
+                             const uint64_t* inputs, uint64_t* h);
+/* create_proof_with_reduction: rs = (r, s) canonical; Proof { a: G1, b: G2, c: G1 } */
+int tpst_groth16_prove(tpst_ctx* ctx, tpst_groth16_pk* pk, tpst_r1cs* r1cs, const uint64_t* vars,
+                       const uint64_t* inputs, const uint64_t* rs, uint64_t* A, uint64_t* B, uint64_t* C);
+
 /* ---- arkworks wire format (csrc/serialize.hip; host only, no context) ------
  * CanonicalSerialize with Compress::Yes (ark-serialize 0.4): G1 48 B, G2 96 B
  * (x with SWFlags in the top bits of the last byte: 0x80 y negative, 0x40

@@ -81,6 +81,12 @@ PROTOTYPES = [
     ("tpst_r1cs_free", None, [_vp]),
     ("tpst_r1cs_commit", C.c_int, [_vp, _vp, C.c_char_p, _sz, _u64p, C.POINTER(_sz), _u64p, C.POINTER(_sz)]),
     ("tpst_r1cs_prove", C.c_int, [_vp, _vp, _u64p, _u64p, _vp, _vp]),
+    ("tpst_groth16_setup", C.c_int, [_vp, _vp, _u64p, C.POINTER(_vp)]),
+    ("tpst_groth16_pk_free", None, [_vp]),
+    ("tpst_groth16_domain", C.c_int, [_vp, C.POINTER(_sz)]),
+    ("tpst_groth16_vk", C.c_int, [_vp, _vp, _u64p, _u64p, _u64p, _u64p, _u64p]),
+    ("tpst_groth16_witness_map", C.c_int, [_vp, _vp, _vp, _u64p, _u64p, _u64p]),
+    ("tpst_groth16_prove", C.c_int, [_vp, _vp, _vp, _u64p, _u64p, _u64p, _u64p, _u64p, _u64p]),
     ("tpst_ser_g1", C.c_int, [_u64p, C.c_char_p]),
     ("tpst_ser_g2", C.c_int, [_u64p, C.c_char_p]),
     ("tpst_de_g1", C.c_int, [C.c_char_p, _u64p]),

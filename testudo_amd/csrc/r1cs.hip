@@ -21,6 +21,7 @@
 #include "../../include/tpst.h"
 #include "ctx.h"
 #include "device_util.h"
+#include "r1cs_state.h"
 
 using namespace tpst;
 
@@ -35,19 +36,6 @@ const uint32_t* tpst_internal_poly_evals(const tpst_poly* p);  // pst_api.hip
 namespace {
 
 inline unsigned grid_for(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
-
-struct Buf {
-  void* p = nullptr;
-  ~Buf() {
-    if (p) (void)hipFree(p);
-  }
-  hipError_t alloc(size_t bytes) {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    return bytes ? hipMalloc(&p, bytes) : hipSuccess;
-  }
-  uint32_t* u() const { return (uint32_t*)p; }
-};
 
 // ------------------------------------------------------------ kernels ----
 // out[i] = prod_j (bit (ell-1-j) of i ? r_j : 1 - r_j)   (MSB-first, r Montgomery)
@@ -306,15 +294,6 @@ __global__ void k_vals_padded(const uint32_t* __restrict__ v0, const uint32_t* _
 }
 
 // ------------------------------------------------------ host Fr helpers ----
-Fr frc(const uint64_t* c) {  // canonical -> Montgomery
-  Fr a;
-  memcpy(a.v, c, 32);
-  return to_mont(a);
-}
-void fro(const Fr& a, uint64_t* c) {
-  const Fr r = from_mont(a);
-  memcpy(c, r.v, 32);
-}
 Fr fr_small(uint32_t v) {
   Fr a = Fr::zero();
   a.v[0] = v;
@@ -350,38 +329,7 @@ Fr uni_eval(const Fr* cs, int n, const Fr& r) {
   return out;
 }
 
-bool fr_ok_host(const uint64_t* v) {
-  static const uint64_t rp[4] = {0x0a11800000000001ull, 0x59aa76fed0000001ull, 0x60b44d1e5c37b001ull,
-                                 0x12ab655e9a2ca556ull};
-  for (int k = 3; k >= 0; k--)
-    if (v[k] != rp[k]) return v[k] < rp[k];
-  return false;
-}
-
-int log2_exact(size_t n) {
-  int l = 0;
-  while (((size_t)1 << l) < n) l++;
-  return ((size_t)1 << l) == n ? l : -1;
-}
-
 }  // namespace
-
-// ================================================================ state ==
-struct tpst_r1cs {
-  size_t num_cons = 0, num_vars = 0, num_inputs = 0, ncols = 0;
-  size_t nnz[3] = {0, 0, 0};
-  Buf rptr[3], ridx[3], rval[3];  // CSR over rows (multiply_vec)
-  Buf cptr[3], cidx[3], cval[3];  // CSC over the 2 num_vars columns of z (eval table)
-  Buf orow[3], ocol[3], oval[3];  // the entries in the caller's order (SPARK dense rep)
-  void* pin = nullptr;            // 4 KiB pinned host staging of the sum-check rounds
-  void* pinned() {
-    if (!pin && hipHostMalloc(&pin, 4096, hipHostMallocDefault) != hipSuccess) pin = nullptr;
-    return pin;
-  }
-  ~tpst_r1cs() {
-    if (pin) (void)hipHostFree(pin);
-  }
-};
 
 // CSR (by key = rows) or CSC (by key = cols) of one matrix from device triples
 static hipError_t build_compressed(hipStream_t s, const uint32_t* key, const uint32_t* other, const uint32_t* val,
