@@ -288,6 +288,23 @@ struct tpst_groth16_pk {
   Buf vk;             // alpha_g1 | beta_g2 | gamma_g2 | delta_g2 (Montgomery)
   // prove-time scratch
   Buf a, b, c, zm, sA, sB, sC, in, out_x, out_aff;
+  // the G2 MSM runs on its own stream + scratch arena, beside the G1 MSMs
+  Arena ar2;
+  hipStream_t s2 = nullptr;
+  hipEvent_t ev_in = nullptr, ev_b2 = nullptr;
+  hipError_t side_init() {
+    if (s2) return hipSuccess;
+    TPST_TRY(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    TPST_TRY(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
+    return hipEventCreateWithFlags(&ev_b2, hipEventDisableTiming);
+  }
+  ~tpst_groth16_pk() {
+    if (s2) (void)hipStreamSynchronize(s2);
+    ar2.release();
+    if (ev_in) (void)hipEventDestroy(ev_in);
+    if (ev_b2) (void)hipEventDestroy(ev_b2);
+    if (s2) (void)hipStreamDestroy(s2);
+  }
 };
 
 static int setup_fail(tpst_ctx* ctx, const char* m) { return fail(ctx, TPST_E_ARG, m); }
@@ -537,7 +554,6 @@ extern "C" int tpst_groth16_prove(tpst_ctx* ctx, tpst_groth16_pk* pk, tpst_r1cs*
   tpst_groth16_pk* P = pk;
   const Fr r = frc(rs), sv = frc(rs + 4);
   if (int rc = upload_assignment(ctx, P, vars, inputs)) return rc;
-  TPST_HIP(ctx, witness_map(P, R, s));
   // constant terms of each MSM (canonical scalars after the variables)
   const size_t nA = P->nq + 2, tc = P->nv + P->n - 1;
   {
@@ -566,12 +582,21 @@ extern "C" int tpst_groth16_prove(tpst_ctx* ctx, tpst_groth16_pk* pk, tpst_r1cs*
   Xyzz<Fq>* xB1 = xA + 1;
   Xyzz<Fq>* xC = xA + 2;
   Xyzz<Fq2>* xB2 = (Xyzz<Fq2>*)(xA + 3);
+  // B in G2 on the side stream once its scalars are in place (the G2 bucket
+  // accumulation runs at low occupancy: the witness map and the G1 MSMs fill
+  // the rest of the chip)
+  TPST_HIP(ctx, P->side_init());
+  TPST_HIP(ctx, hipEventRecord(P->ev_in, s));
+  TPST_HIP(ctx, hipStreamWaitEvent(P->s2, P->ev_in, 0));
+  TPST_HIP(ctx, msm_var<Fq2>(P->ar2, P->s2, P->bB2.u(), P->sB.u(), nA, xB2));
+  TPST_HIP(ctx, hipEventRecord(P->ev_b2, P->s2));
+  TPST_HIP(ctx, witness_map(P, R, s));
   TPST_HIP(ctx, msm_var<Fq>(ctx->arena, s, P->bA.u(), P->sA.u(), nA, xA));
   TPST_HIP(ctx, msm_var<Fq>(ctx->arena, s, P->bB1.u(), P->sB.u(), nA, xB1));
   // A and B1 become bases of the C MSM (slots after L and H)
   TPST_HIP(ctx, xyzz_to_affine_mont<Fq>(s, xA, P->bC.u() + 24 * tc, 2));
   TPST_HIP(ctx, msm_var<Fq>(ctx->arena, s, P->bC.u(), P->sC.u(), P->nC, xC));
-  TPST_HIP(ctx, msm_var<Fq2>(ctx->arena, s, P->bB2.u(), P->sB.u(), nA, xB2));
+  TPST_HIP(ctx, hipStreamWaitEvent(s, P->ev_b2, 0));
   uint32_t* o = P->out_aff.u();
   TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(s, xA, o, 1));
   TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(s, xC, o + 24, 1));

@@ -196,12 +196,27 @@ static __global__ void k_bucket_bounds(const uint32_t* __restrict__ keys, size_t
   if (i == m - 1 || keys[i + 1] != k) bend[k] = (uint32_t)i + 1;
 }
 
-// phi(P) = (beta x, y), the GLV endomorphism (phi(P) = [x^2 - 1] P)
+// phi(P) = (beta x, y), the GLV endomorphism (phi(P) = [x^2 - 1] P on G1).
+// On G2 (E'(Fq2), also j = 0) the same beta has eigenvalue lambda^2, so G2
+// uses beta^2: (beta^2 x, y) = [x^2 - 1] Q, and one scalar decomposition
+// serves both groups.
+__constant__ uint32_t G2_GLV_BETA[12] = {0x5a7b8727u, 0x2c766f92u, 0x253d58b5u, 0x03d7f6b0u,
+                                         0xec122131u, 0x838ec0deu, 0xf658bb10u, 0xbd5eb3e9u,
+                                         0x6ed3e52eu, 0x6942bd12u, 0xdd04ed6au, 0x01673786u};  // Montgomery
+template <class F>
 static __global__ void k_glv_phi(const uint32_t* __restrict__ bases, size_t n, uint32_t* __restrict__ out) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  G1A p = load_affine<Fq>(bases, i);
-  if (!is_inf(p)) p.x = mul(p.x, Fq::from_limbs(params::G1_BETA));
+  Affine<F> p = load_affine<F>(bases, i);
+  if (!is_inf(p)) {
+    if constexpr (sizeof(F) == sizeof(Fq)) {
+      p.x = mul(p.x, Fq::from_limbs(params::G1_BETA));
+    } else {
+      const Fq b2 = Fq::from_limbs(G2_GLV_BETA);
+      p.x.c0 = mul(p.x.c0, b2);
+      p.x.c1 = mul(p.x.c1, b2);
+    }
+  }
   store_affine(out, i, p);
 }
 
@@ -708,8 +723,8 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
     return hipMemcpyAsync(d_out, &inf, sizeof(inf), hipMemcpyHostToDevice, s);
   }
   if (n > MSM_MAX_POINTS) return hipErrorInvalidValue;
-  constexpr bool kGlv = sizeof(F) == sizeof(Fq);  // G1: phi(x, y) = (beta x, y)
-  const bool glv = kGlv && n >= 64;
+  const bool glv = n >= 64;  // phi(x, y) = (beta x, y) on G1, (beta^2 x, y) on G2
+  constexpr size_t PW = 2 * Words<F>::n;
   const int c = msm_window_bits(glv ? 2 * n : n);
   const int W = glv ? num_windows_bits(c, 128) : num_windows(c);
   const uint32_t nb = 1u << (c - 1);
@@ -750,7 +765,7 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   size_t need = Arena::need(m, 4) * 4 + Arena::need(nbk, 4) * 2 + Arena::need(nbk, sizeof(Xyzz<F>)) +
                 Arena::need(2 * nchunk, sizeof(Xyzz<F>)) + Arena::need(nblk, sizeof(Xyzz<F>)) + red_need +
                 Arena::need(W, sizeof(Xyzz<F>)) + Arena::need(NG, sizeof(Xyzz<F>)) + Arena::need(W + 1, 4) +
-                Arena::need(glv ? n * 24 : 1, 4) + Arena::need(sort_bytes, 1) + 8192;
+                Arena::need(glv ? n * PW : 1, 4) + Arena::need(sort_bytes, 1) + 8192;
   ar.reset();
   TPST_TRY(ar.reserve(need));
   uint32_t* keys = ar.take<uint32_t>(m);
@@ -765,7 +780,7 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   Xyzz<F>* win = ar.take<Xyzz<F>>(W);
   Xyzz<F>* contrib = ar.take<Xyzz<F>>(NG);
   uint32_t* range = ar.take<uint32_t>(W + 1);
-  uint32_t* phib = ar.take<uint32_t>(glv ? n * 24 : 1);
+  uint32_t* phib = ar.take<uint32_t>(glv ? n * PW : 1);
   void* tmp = ar.take<char>(sort_bytes);
 
   Profiler* pf = ar.prof;
@@ -775,7 +790,7 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   k_decompose_var<<<grid_for(n, 256), 256, 0, s>>>(d_scalars, n, c, W, glv ? 1 : 0, sent, keys, vals);
   TPST_TRY(hipGetLastError());
   if (glv) {
-    k_glv_phi<<<grid_for(n, 256), 256, 0, s>>>(d_bases, n, phib);
+    k_glv_phi<F><<<grid_for(n, 256), 256, 0, s>>>(d_bases, n, phib);
     TPST_TRY(hipGetLastError());
   }
   pf->end(ST_DECOMPOSE, s);
