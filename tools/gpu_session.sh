@@ -12,7 +12,7 @@ if [ "$2" != "notests" ]; then
 fi
 timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || exit 1
 cd /tmp && export TMPDIR=/tmp
-SHORT="$GRAFT_REPO_ROOT/bench.py --no-cpu --no-pst --no-sharded --steps 5 --warmup 2"
+SHORT="$GRAFT_REPO_ROOT/bench.py --no-cpu --no-pst --no-sharded --no-r1cs --no-groth16 --steps 5 --warmup 2"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu > $OUT/bench_prof.json 2> $OUT/prof.err || exit 1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 $SHORT > $OUT/pmc_fetch.log 2>&1 || exit 1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 $SHORT > $OUT/pmc_write.log 2>&1 || exit 1
