@@ -93,3 +93,24 @@ def test_fullsize_commit_open_n20(ctx):
 def test_fullsize_commit_open_n24(ctx):
     """BASELINE configs[3] on one GPU: 2^24-variable commit + open, bit-exact."""
     _check_fullsize(ctx, 24)
+
+
+@pytest.mark.gpu
+def test_fullsize_groth16_2p20(ctx):
+    """Groth16 at the R1CS leg's size (2^20 constraints and variables, 10
+    inputs, domain 2^21): the device proof satisfies the pairing equation, a
+    wrong public input or a broken witness does not."""
+    from testudo_amd import groth16 as D
+    from testudo_amd import r1cs as S
+    inst, vars_, inputs = S.R1CSInstance.produce_synthetic_r1cs(ctx, 1 << 20, 1 << 20, 10, 2024)
+    pk = D.ProvingKey.setup(inst, fr_array([3, 5, 7, 11, 13]))
+    assert pk.domain_size == 1 << 21
+    vk = pk.vk()
+    proof = D.prove(pk, inst, vars_, inputs, fr_array([17]), fr_array([19]))
+    assert D.verify(ctx, vk, inputs, proof)
+    bad = inputs.copy()
+    bad[9, 0] ^= 2
+    assert not D.verify(ctx, vk, bad, proof)
+    v2 = vars_.copy()
+    v2[(1 << 20) - 1, 1] ^= 1
+    assert not D.verify(ctx, vk, inputs, D.prove(pk, inst, v2, inputs, fr_array([17]), fr_array([19])))
