@@ -262,6 +262,7 @@ __global__ void __launch_bounds__(64) k_mb_wave_prof(int op, int iters, unsigned
     const uint32_t hdr1 = __builtin_amdgcn_readfirstlane(blk[1]);
     const int np = hdr & 0xff, no = (hdr >> 8) & 0xff, nc = hdr >> 24;
     const int tx = hdr1 & 0xff, ty = (hdr1 >> 8) & 0xff, tc = (hdr1 >> 16) & 0xff;
+    const bool sq = (hdr >> 17) & 1;
     const uint64_t bases = wave::pack_bases(e, A, B);
     const wave::lds_t* X = blk + 2;
     const wave::lds_t* Y = X + tx * np;
@@ -272,7 +273,7 @@ __global__ void __launch_bounds__(64) k_mb_wave_prof(int op, int iters, unsigned
     Fq x, y, pr;
     if (lane < np) {
       wave::form(e, X + lane, np, tx, bases, xw);
-      wave::form(e, Y + lane, np, ty, bases, yw);
+      if (!sq) wave::form(e, Y + lane, np, ty, bases, yw);
 #pragma unroll
       for (int i = 0; i < 12; i++) {
         x.v[i] = xw[i];
@@ -280,7 +281,7 @@ __global__ void __launch_bounds__(64) k_mb_wave_prof(int op, int iters, unsigned
       }
     }
     unsigned long long t1 = clock64();
-    if (lane < np) pr = mul(x, y);
+    if (lane < np) pr = sq ? sqr(x) : mul(x, y);
     unsigned long long t2 = clock64();
     if (lane < np) wave::put_slot(vals, base + lane, pr);
     wave::wave_sync();

@@ -92,9 +92,8 @@ __device__ __forceinline__ void fetch_term(const Eng& e, uint32_t term, uint64_t
 
 // sum of coef * slot over the `cnt` terms of one linear form -> 13 limbs.
 // Term j of this lane is t[j * stride]; cnt is wave-uniform (lists padded
-// with zero terms), so the term words are all fetched up front and the data
-// of term j+1 is loaded while term j's multiply-adds run.  One
-// v_mad_u64_u32 per limb and term (coefficients < 256).
+// with zero terms), so the term words and then every term's slot are
+// fetched up front.  One v_mad_u64_u32 per limb and term (coefficients < 256).
 __device__ __forceinline__ void form(const Eng& e, const lds_t* t, int stride, int cnt, uint64_t bases,
                                      uint32_t out[13]) {
   uint32_t tw[8];
@@ -103,25 +102,25 @@ __device__ __forceinline__ void form(const Eng& e, const lds_t* t, int stride, i
   uint64_t acc[12];
 #pragma unroll
   for (int i = 0; i < 12; i++) acc[i] = 0;
-  v4u q0 = v4u{0, 0, 0, 0}, q1 = q0, q2 = q0;
-  uint32_t c = 0;
-  if (cnt > 0) fetch_term(e, tw[0], bases, q0, q1, q2, c);
+  // every term's slot is read before the first multiply-add: the engine runs
+  // one wave per chain, so the LDS reads overlap each other instead of each
+  // term waiting out a full LDS round trip (the VGPRs are free at this
+  // occupancy)
+  v4u q0[8], q1[8], q2[8];
+  uint32_t c[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++)
+    if (j < cnt) fetch_term(e, tw[j], bases, q0[j], q1[j], q2[j], c[j]);
 #pragma unroll
   for (int j = 0; j < 8; j++) {
     if (j < cnt) {
-      v4u n0 = q0, n1 = q1, n2 = q2;
-      uint32_t nc = 0;
-      if (j + 1 < cnt) fetch_term(e, tw[j + 1 < 8 ? j + 1 : 7], bases, n0, n1, n2, nc);
-      acc[0] += (uint64_t)c * q0.x; acc[1] += (uint64_t)c * q0.y;
-      acc[2] += (uint64_t)c * q0.z; acc[3] += (uint64_t)c * q0.w;
-      acc[4] += (uint64_t)c * q1.x; acc[5] += (uint64_t)c * q1.y;
-      acc[6] += (uint64_t)c * q1.z; acc[7] += (uint64_t)c * q1.w;
-      acc[8] += (uint64_t)c * q2.x; acc[9] += (uint64_t)c * q2.y;
-      acc[10] += (uint64_t)c * q2.z; acc[11] += (uint64_t)c * q2.w;
-      q0 = n0;
-      q1 = n1;
-      q2 = n2;
-      c = nc;
+      const uint32_t cj = c[j];
+      acc[0] += (uint64_t)cj * q0[j].x; acc[1] += (uint64_t)cj * q0[j].y;
+      acc[2] += (uint64_t)cj * q0[j].z; acc[3] += (uint64_t)cj * q0[j].w;
+      acc[4] += (uint64_t)cj * q1[j].x; acc[5] += (uint64_t)cj * q1[j].y;
+      acc[6] += (uint64_t)cj * q1[j].z; acc[7] += (uint64_t)cj * q1[j].w;
+      acc[8] += (uint64_t)cj * q2[j].x; acc[9] += (uint64_t)cj * q2[j].y;
+      acc[10] += (uint64_t)cj * q2[j].z; acc[11] += (uint64_t)cj * q2[j].w;
     }
   }
   uint64_t cr = 0;
@@ -155,7 +154,7 @@ __device__ __forceinline__ Fq reduce_wide(const uint32_t v[13]) {
 }
 
 // one stage: C/D = op(A, B).
-// block: [hdr0 = np | no << 8 | red << 16 | nc << 24, hdr1 = TX | TY << 8 | TC << 16,
+// block: [hdr0 = np | no << 8 | red << 16 | sq << 17 | nc << 24, hdr1 = TX | TY << 8 | TC << 16,
 //         X terms (TX x np, term-major), Y terms (TY x np), chunk terms (TC x nc),
 //         out[no] = first chunk << 8 | chunks, dst[no]]
 // Output forms longer than a few terms are split into chunks summed by
@@ -168,6 +167,7 @@ __device__ __forceinline__ void run(const Eng& e, const lds_t* blk, int a, int b
   const int np = hdr & 0xff, no = (hdr >> 8) & 0xff, nc = hdr >> 24;
   const int tx = hdr1 & 0xff, ty = (hdr1 >> 8) & 0xff, tc = (hdr1 >> 16) & 0xff;
   const bool red = (hdr >> 16) & 1;
+  const bool sq = (hdr >> 17) & 1;  // every product a square: no Y forms (wave-uniform)
   const uint64_t bases = pack_bases(e, a, b);
   const lds_t* X = blk + 2;
   const lds_t* Y = X + tx * np;
@@ -175,21 +175,29 @@ __device__ __forceinline__ void run(const Eng& e, const lds_t* blk, int a, int b
   const lds_t* O = CH + tc * nc;
   const lds_t* DST = O + no;
   if (lane < np) {
-    uint32_t xw[13], yw[13];
+    uint32_t xw[13];
     form(e, X + lane, np, tx, bases, xw);
-    form(e, Y + lane, np, ty, bases, yw);
-    Fq x, y;
+    Fq x;
     if (red) {
       x = reduce_wide(xw);
-      y = reduce_wide(yw);
     } else {
 #pragma unroll
-      for (int i = 0; i < 12; i++) {
-        x.v[i] = xw[i];
-        y.v[i] = yw[i];
-      }
+      for (int i = 0; i < 12; i++) x.v[i] = xw[i];
     }
-    put_slot(e.lds, e.prod + lane, mul(x, y));
+    if (sq) {
+      put_slot(e.lds, e.prod + lane, sqr(x));
+    } else {
+      uint32_t yw[13];
+      form(e, Y + lane, np, ty, bases, yw);
+      Fq y;
+      if (red) {
+        y = reduce_wide(yw);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 12; i++) y.v[i] = yw[i];
+      }
+      put_slot(e.lds, e.prod + lane, mul(x, y));
+    }
   }
   wave_sync();
   if (nc == no) {

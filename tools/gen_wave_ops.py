@@ -71,6 +71,15 @@ class Prog:
         self.products.append((x, y))
         return atom("P", len(self.products) - 1)
 
+    def sqr(self, x):
+        """x^2: the same object as both factors marks a square; a stage whose
+        products are all squares skips its Y forms and runs the Montgomery
+        squaring (78 instead of 144 limb products)."""
+        return self.mul(x, x)
+
+    def all_squares(self):
+        return bool(self.products) and all(x is y for x, y in self.products)
+
     def const(self, v):
         v %= P
         if v not in self.consts:
@@ -159,14 +168,26 @@ def f12_mul_by_034(pg, f, c0, c3, c4):
     return (f6_add(a, f6_mul_by_v(b)), f6_sub(e, f6_add(a, b)))
 
 
+def f2_sqr_sq(pg, a):
+    """a^2 from three Fq squares: (a0^2 - 5 a1^2, (a0 + a1)^2 - a0^2 - a1^2)."""
+    s0 = pg.sqr(a[0])
+    s1 = pg.sqr(a[1])
+    s01 = pg.sqr(a[0] + a[1])
+    return (s0 - s1.sc(5), s01 - s0 - s1)
+
+
 def cyclotomic_sqr(pg, f):
     r0, r4, r3 = f[0]
     r2, r1, r5 = f[1]
 
+    # Fp4 square of x + y s: t = x^2 + u y^2, 2xy = (x + y)^2 - x^2 - y^2 --
+    # the same values as the Karatsuba form (x y, (x + y)(x + u y)), from 27
+    # Fq squares instead of 18 products, so the stage is all squares
     def part(x, y):
-        tmp = f2_mul(pg, x, y)
-        t = f2_sub(f2_sub(f2_mul(pg, f2_add(x, y), f2_add(f2_mul_by_u(y), x)), tmp), f2_mul_by_u(tmp))
-        return t, f2_sc(tmp, 2)
+        x2 = f2_sqr_sq(pg, x)
+        y2 = f2_sqr_sq(pg, y)
+        s2 = f2_sqr_sq(pg, f2_add(x, y))
+        return f2_add(x2, f2_mul_by_u(y2)), f2_sub(f2_sub(s2, x2), y2)
     t0, t1 = part(r0, r1)
     t2, t3 = part(r2, r3)
     t4, t5 = part(r4, r5)
@@ -203,7 +224,29 @@ def op_f12_mul(pg):
     return {"C": flat12(f12_mul(pg, reg12("A"), reg12("B")))}
 
 
+def f6_sqr_sq(pg, c):
+    """(c0 + c1 v + c2 v^2)^2 from six Fq2 squares (v^3 = u):
+    c0^2 + u 2c1c2, 2c0c1 + u c2^2, c1^2 + 2c0c2 with 2xy = (x + y)^2 - x^2 - y^2."""
+    c0, c1, c2 = c
+    s0, s1, s2 = f2_sqr_sq(pg, c0), f2_sqr_sq(pg, c1), f2_sqr_sq(pg, c2)
+    t12 = f2_sub(f2_sub(f2_sqr_sq(pg, f2_add(c1, c2)), s1), s2)
+    t01 = f2_sub(f2_sub(f2_sqr_sq(pg, f2_add(c0, c1)), s0), s1)
+    t02 = f2_sub(f2_sub(f2_sqr_sq(pg, f2_add(c0, c2)), s0), s2)
+    return (f2_add(s0, f2_mul_by_u(t12)), f2_add(t01, f2_mul_by_u(s2)), f2_add(s1, t02))
+
+
+def f12_sqr_sq(pg, a):
+    """(a0 + a1 w)^2 = a0^2 + v a1^2 + ((a0 + a1)^2 - a0^2 - a1^2) w: 54 Fq squares."""
+    q0, q1 = f6_sqr_sq(pg, a[0]), f6_sqr_sq(pg, a[1])
+    q01 = f6_sqr_sq(pg, f6_add(a[0], a[1]))
+    return (f6_add(q0, f6_mul_by_v(q1)), f6_sub(f6_sub(q01, q0), q1))
+
+
 def op_f12_sqr(pg):
+    return {"C": flat12(f12_sqr_sq(pg, reg12("A")))}
+
+
+def op_f12_sqr_prod(pg):
     return {"C": flat12(f12_mul(pg, reg12("A"), reg12("A")))}
 
 
@@ -225,12 +268,12 @@ def op_line_prep(pg):
 
 
 def op_sqr_lp1(pg):
-    c = op_f12_sqr(pg)["C"]
+    c = op_f12_sqr_prod(pg)["C"]
     return {"C": c, "D": line_prep(pg, 0)}
 
 
 def op_sqr_lp2(pg):
-    c = op_f12_sqr(pg)["C"]
+    c = op_f12_sqr_prod(pg)["C"]
     d0 = line_prep(pg, 0)
     # second line: coefficients at B[8..14), same point (px, py) = B[6], B[7]
     c0, c1, c2 = reg_f2("B", 4), reg_f2("B", 5), reg_f2("B", 6)
@@ -648,8 +691,9 @@ def main():
         assert nc <= 64
         # term lists padded to a per-op uniform length (zero words = 0 * A[0])
         # and stored term-major: term j of lane l at [j * lanes + l]
+        sq = int(pg.all_squares())
         xs = [sorted(x.items()) for x, _ in pg.products]
-        ys = [sorted(y.items()) for _, y in pg.products]
+        ys = [] if sq else [sorted(y.items()) for _, y in pg.products]
         tx = max((len(v) for v in xs), default=0)
         ty = max((len(v) for v in ys), default=0)
         tc = max((len(v) for v in chunks), default=0)
@@ -663,14 +707,14 @@ def main():
             return out
         maxw = max((lin.weight() for _, lin in olist), default=0)
         assert maxw < 1024, (name, maxw)
-        block = ([np_ | no << 8 | need_red << 16 | nc << 24, tx | ty << 8 | tc << 16] + major(xs, tx) + major(ys, ty) +
-                 major(chunks, tc) + info_o + [d for d, _ in olist])
+        block = ([np_ | no << 8 | need_red << 16 | sq << 17 | nc << 24, tx | ty << 8 | tc << 16] + major(xs, tx) +
+                 major(ys, ty) + major(chunks, tc) + info_o + [d for d, _ in olist])
         offs.append(len(blob))
         lens.append(len(block))
         blob += block
         names.append(name)
-        stats.append("//   %-10s products %2d (terms %d x %d)  outputs %2d  chunks %2d (<= %d terms)  max weight %3d  words %4d"
-                     % (name, np_, tx, ty, no, nc, tc, maxw, len(block)))
+        stats.append("//   %-10s %s %2d (terms %d x %d)  outputs %2d  chunks %2d (<= %d terms)  max weight %3d  words %4d"
+                     % (name, "squares " if sq else "products", np_, tx, ty, no, nc, tc, maxw, len(block)))
     lines += stats
     lines.append("enum OpId {%s, N_OPS};" % ", ".join("OP_" + n for n in names))
     lines.append("static constexpr uint32_t OP_OFF[N_OPS] = {%s};" % ", ".join(map(str, offs)))
