@@ -640,7 +640,9 @@ def enc_term(kind, i, c):
     return OPCODE[kind] | (i << 8) | ((1 if c < 0 else 0) << 2) | (abs(c) << 24)
 
 
-def main():
+def render():
+    """Build every op, check it numerically against the oracle, and return
+    (text of wave_ops.inc, per-op stats lines)."""
     random.seed(377)
     consts = []
     built = {}
@@ -722,11 +724,18 @@ def main():
     lines.append("static TPST_WAVE_CONST uint32_t BLOB[%d] = {%s};" % (len(blob), ", ".join("0x%08xu" % t for t in blob)))
     lines.append("static constexpr double INV_P320 = %r;  // 2^320 / p" % (2.0 ** 320 / P))
     lines.append("}}  // namespace tpst::wave")
-    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "testudo_amd", "csrc",
+    return "\n".join(lines) + "\n", stats
+
+
+INC_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "testudo_amd", "csrc",
                         "wave_ops.inc")
-    open(path, "w").write("\n".join(lines) + "\n")
+
+
+def main():
+    text, stats = render()
+    open(INC_PATH, "w").write(text)
     print("\n".join(stats))
-    print("blob words", len(blob), "consts", len(consts), "wrote", path)
+    print("wrote", INC_PATH)
 
 
 if __name__ == "__main__":
