@@ -116,7 +116,7 @@ def _max_over_ranks(dist, dev, x):
     import torch
     if dist is None:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    t = torch.tensor([x], dtype=torch.float64, device="cpu" if dist.get_backend() == "gloo" else dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -165,8 +165,16 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        if os.environ.get("TPST_BENCH_SHARED_GPU") == "1":
+            # rehearsal of the multi-rank path on a box with fewer GPUs than
+            # ranks: ranks share cards and talk over gloo (RCCL refuses two
+            # ranks on one GPU); timings are not scaling numbers
+            local %= max(1, torch.cuda.device_count())
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl")
     from testudo_amd import Context
     from testudo_amd.sqrt_pst import fr_stream
 

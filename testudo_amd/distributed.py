@@ -37,6 +37,8 @@ def sharded_commit(n: int, commit_rows_partial: Callable[[int, int], Tuple[np.nd
     commit_rows_partial(r0, r1) -> (comms (r1-r0, 12), miller partial (72,));
     finalize(partials (world, 72)) -> T, run on rank 0 only."""
     import torch
+    if dist.get_backend() == "gloo":  # gloo gathers host tensors only
+        device = "cpu"
     world = dist.get_world_size()
     rank = dist.get_rank()
     m_col = n // 2
