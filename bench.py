@@ -470,17 +470,18 @@ def sharded_leg(ctx, log_n, dist, dev):
     rank = dist.get_rank() if dist else 0
     world = dist.get_world_size() if dist else 1
     r0, r1 = shard_rows(1 << (log_n // 2), world, rank)
-    t = time.perf_counter()
-    pl = S.Polynomial.from_evaluations(ctx, Z)
-    h2d_full_s = time.perf_counter() - t
+    pl = None
+    h2d_full_s = None
+    if rank == 0:  # rank 0 opens, so it holds the whole polynomial
+        t = time.perf_counter()
+        pl = S.Polynomial.from_evaluations(ctx, Z)
+        h2d_full_s = time.perf_counter() - t
     shard = pl
     h2d_s = h2d_full_s
     if dist and rank != 0:  # the rank-local column block only
-        del pl
         t = time.perf_counter()
         shard = S.Polynomial.from_evaluations_cols(ctx, Z, r0, r1)
         h2d_s = time.perf_counter() - t
-        pl = None
     if rank == 0:
         v = pl.eval(pt)
     reps = 2
@@ -515,8 +516,9 @@ def sharded_leg(ctx, log_n, dist, dev):
             "ranks": world, "rows_per_rank": r1 - r0, "verified": ok,
             "h2d_s_rank0_full": round(h2d_full_s, 4), "h2d_s_rank0_shard": round(h2d_s, 4),
             "srs_setup_s": round(setup_s, 3),
-            "exchange": ("per-rank column-block upload; RCCL all_gather of [96-B row commitments | 576-B Miller "
-                         "partial] per rank; final exponentiation + open on rank 0") if dist else "none"}
+            "exchange": ("per-rank column-block upload; %s all_gather of [96-B row commitments | 576-B Miller "
+                         "partial] per rank; final exponentiation + open on rank 0"
+                         % ("RCCL" if dist.get_backend() == "nccl" else "gloo")) if dist else "none"}
 
 
 def cpu_leg(ctx, bk, sc, gpu_out, result):
