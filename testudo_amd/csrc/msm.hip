@@ -5,6 +5,7 @@
 #include "device_util.h"
 #include "coop.h"
 #include "msm.h"
+#include <type_traits>
 
 namespace tpst {
 
@@ -412,6 +413,29 @@ __global__ void __launch_bounds__(64) k_seg_reduce_quad(const Xyzz<F>* __restric
   if (qi == 0) store_xyzz(seg_out, t, sum);
 }
 
+// the same segment sums, one lane per segment: for reductions with enough
+// segments to fill the chip (the 4096-row commit at 2^24: 262 144 segments)
+// the quad-cooperative form only adds exchange overhead to a throughput-bound
+// pass
+template <class F>
+__global__ void __launch_bounds__(64) k_seg_reduce_lane(const Xyzz<F>* __restrict__ buckets, uint32_t nb, uint32_t L,
+                                                        size_t nseg, Xyzz<F>* __restrict__ seg_out) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nseg) return;
+  const uint32_t S = nb / L;
+  const size_t g = t / S;
+  const uint32_t k = (uint32_t)(t % S);
+  const size_t base = g * nb + (size_t)k * L;
+  Xyzz<F> acc = Xyzz<F>::inf(), sum = Xyzz<F>::inf();
+  for (int b = (int)L - 1; b >= 0; b--) {
+    acc = add(acc, load_xyzz(buckets, base + b));
+    sum = add(sum, acc);
+  }
+  const uint32_t s0 = k * L;
+  if (s0 != 0 && !is_inf(acc)) sum = add(sum, scalar_mul_xyzz(acc, &s0, 32 - __builtin_clz(s0)));
+  store_xyzz(seg_out, t, sum);
+}
+
 // one workgroup of BS / 4 quads per group: sum its S partial points
 template <class F, int BS>
 __global__ void __launch_bounds__(BS) k_group_reduce_quad(const Xyzz<F>* __restrict__ seg, uint32_t S,
@@ -556,7 +580,10 @@ static hipError_t reduce_buckets(Arena& ar, hipStream_t s, const Xyzz<F>* d_buck
   const uint32_t S = nb / L;
   const size_t nseg = groups * S;
   Xyzz<F>* seg = ar.take<Xyzz<F>>(nseg);
-  k_seg_reduce_quad<F><<<grid_for(4 * nseg, 64), 64, 0, s>>>(d_buckets, nb, L, nseg, seg, prio);
+  if (std::is_same<F, Fq>::value && nseg >= ((size_t)1 << 18))
+    k_seg_reduce_lane<F><<<grid_for(nseg, 64), 64, 0, s>>>(d_buckets, nb, L, nseg, seg);
+  else
+    k_seg_reduce_quad<F><<<grid_for(4 * nseg, 64), 64, 0, s>>>(d_buckets, nb, L, nseg, seg, prio);
   TPST_TRY(hipGetLastError());
   if (S >= 256 && S % 64 == 0) {  // two-pass tree: 64 -> 1, then per group
     Xyzz<F>* mid = ar.take<Xyzz<F>>(nseg / 64);
