@@ -9,6 +9,6 @@ if [ -n "$3" ]; then
 fi
 for p in $2; do
   IFS=: read g l r sp pr <<< "$p"
-  TPST_MSM_GROUPS=$g TPST_MSM_LG=$l TPST_MSM_RED2=$r TPST_MSM_SPLIT=$sp TPST_MSM_PRIO=$pr timeout -k 10 200 python -u bench.py --no-cpu --no-pst --no-sharded > $OUT/bench_${g}_${l}_${r}_${sp}_${pr}.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
+  TPST_MSM_GROUPS=$g TPST_MSM_LG=$l TPST_MSM_RED2=$r TPST_MSM_SPLIT=$sp TPST_MSM_PRIO=$pr timeout -k 10 200 python -u bench.py --no-cpu --no-pst --no-sharded --no-r1cs --no-groth16 > $OUT/bench_${g}_${l}_${r}_${sp}_${pr}.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
   python -c "import json,sys; d=json.load(open('$OUT/bench_${g}_${l}_${r}_${sp}_${pr}.json')); print('g $g lg $l red2 $r split $sp prio $pr', d['value'], d['ms_per_step'], d['stages_ms_per_step'], d['parity_ok'])"
 done
