@@ -719,13 +719,23 @@ static int msm_groups(size_t n, int W) {
 }
 
 // window boundaries wb[0..NG] of the groups: TPST_MSM_SPLIT = window counts
-// from the bottom group up ("2,3,3"), else an even split
+// from the bottom group up ("1,3,4"), else a short bottom group (~W/8
+// windows: its reduction and chain are the tail left after the accumulation)
+// and an even split of the rest -- 1,3,4 for the 2^20 G1 MSM, 1.3 % faster
+// than 2,3,3 in an interleaved A/B (profiles/r02/sw2)
 static void msm_group_bounds(int W, int NG, int* wb) {
   static const std::string env = [] {
     const char* e = getenv("TPST_MSM_SPLIT");
     return std::string(e ? e : "");
   }();
-  for (int g = 0; g <= NG; g++) wb[g] = g * W / NG;
+  if (NG == 1) {
+    wb[0] = 0;
+    wb[1] = W;
+  } else {
+    const int lo = W / 8 > 1 ? W / 8 : 1;
+    wb[0] = 0;
+    for (int g = 1; g <= NG; g++) wb[g] = lo + (g - 1) * (W - lo) / (NG - 1);
+  }
   if (env.empty()) return;
   int cnt[16], k = 0, tot = 0;
   for (size_t i = 0; i < env.size() && k < 16;) {
