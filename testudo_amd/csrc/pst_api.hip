@@ -102,6 +102,61 @@ Fq hmul(const Fq& a, const Fq& b) {
   return out;
 }
 
+// sum of three Montgomery products with one reduction: the 768-bit products
+// are added unreduced (3 p^2 < p R) and reduced once, so an MDS row costs
+// three multiplications and one REDC instead of three of each
+Fq hmul3(const Fq& a0, const Fq& b0, const Fq& a1, const Fq& b1, const Fq& a2, const Fq& b2) {
+  typedef unsigned __int128 u128;
+  const HostP64& P = hp64();
+  uint64_t t[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const Fq* as[3] = {&a0, &a1, &a2};
+  const Fq* bs[3] = {&b0, &b1, &b2};
+  for (int k = 0; k < 3; k++) {
+    uint64_t x[6], y[6];
+    memcpy(x, as[k]->v, 48);
+    memcpy(y, bs[k]->v, 48);
+    for (int i = 0; i < 6; i++) {
+      u128 c = 0;
+      for (int j = 0; j < 6; j++) {
+        c += (u128)x[j] * y[i] + t[i + j];
+        t[i + j] = (uint64_t)c;
+        c >>= 64;
+      }
+      for (int j = i + 6; j < 13 && c; j++) {
+        c += t[j];
+        t[j] = (uint64_t)c;
+        c >>= 64;
+      }
+    }
+  }
+  for (int i = 0; i < 6; i++) {  // REDC, word by word
+    const uint64_t m = t[i] * P.inv;
+    u128 c = 0;
+    for (int j = 0; j < 6; j++) {
+      c += (u128)m * P.p[j] + t[i + j];
+      t[i + j] = (uint64_t)c;
+      c >>= 64;
+    }
+    for (int j = i + 6; j < 13 && c; j++) {
+      c += t[j];
+      t[j] = (uint64_t)c;
+      c >>= 64;
+    }
+  }
+  // (T + M p) / R < 2p: one conditional subtraction of t[6..12]
+  uint64_t r[6];
+  u128 br = 0;
+  for (int j = 0; j < 6; j++) {
+    const u128 d = (u128)t[6 + j] - P.p[j] - (uint64_t)br;
+    r[j] = (uint64_t)d;
+    br = (d >> 64) & 1;
+  }
+  const bool ge = t[12] || !br;
+  Fq out;
+  memcpy(out.v, ge ? r : t + 6, 48);
+  return out;
+}
+
 // ------------------------------------------------------------ Poseidon ----
 struct PoseidonParams {
   Fq ark[39][3];
@@ -144,8 +199,7 @@ struct Sponge {
         st[i] = hmul(x16, x);
       }
       Fq ns[3];
-      for (int i = 0; i < 3; i++)
-        ns[i] = add(add(hmul(P.mds[i][0], st[0]), hmul(P.mds[i][1], st[1])), hmul(P.mds[i][2], st[2]));
+      for (int i = 0; i < 3; i++) ns[i] = hmul3(P.mds[i][0], st[0], P.mds[i][1], st[1], P.mds[i][2], st[2]);
       for (int i = 0; i < 3; i++) st[i] = ns[i];
     }
   }
@@ -1276,17 +1330,20 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
       sp.absorb_bytes(b, 96);
       have_U = true;
     }
+    // comms_u (stream B) is ready well before comms_t (the final
+    // exponentiations): absorb it while stream A finishes (mipp.rs:97-100
+    // order: u_l, u_r, t_l, t_r)
     TPST_HIP(ctx, hipEventSynchronize(ev_b(r)));
-    TPST_HIP(ctx, hipEventSynchronize(ev_a(r)));
     memcpy(proof->comms_u[r][0], dn_r, 96);
     memcpy(proof->comms_u[r][1], dn_r + 96, 96);
-    memcpy(proof->comms_t[r][0], dn_r + 192, 576);
-    memcpy(proof->comms_t[r][1], dn_r + 192 + 576, 576);
     uint8_t b[96];
     g1_bytes(proof->comms_u[r][0], b);
     sp.absorb_bytes(b, 96);
     g1_bytes(proof->comms_u[r][1], b);
     sp.absorb_bytes(b, 96);
+    TPST_HIP(ctx, hipEventSynchronize(ev_a(r)));
+    memcpy(proof->comms_t[r][0], dn_r + 192, 576);
+    memcpy(proof->comms_t[r][1], dn_r + 192 + 576, 576);
     sp.absorb_bytes((const uint8_t*)proof->comms_t[r][0], 576);
     sp.absorb_bytes((const uint8_t*)proof->comms_t[r][1], 576);
     uint64_t ci_c[4];
