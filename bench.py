@@ -319,7 +319,7 @@ def main():
             result["groth16"] = groth16_leg(ctx, args.r1cs_log_cons)
         except Exception as e:  # never lose the bench line to the secondary leg
             result["groth16"] = {"error": repr(e)}
-    if not args.no_cpu and world == 1:
+    if not args.no_cpu:  # rank 0 (at N > 1 the other ranks wait at the closing barrier)
         result["cpu_baseline"] = cpu_leg(ctx, bk, sc, out, result)
     print(json.dumps(result), flush=True)
     if dist:
@@ -357,6 +357,7 @@ def pst_leg(ctx, log_n, reps=5):
         U, pst_proof, mipp = pl.open(tr, comms, pt, T)
         open_s = time.perf_counter() - t
         runs.append((commit_s, open_s, h2d_s))
+    _PST_LAST[log_n] = {"comms": comms, "T": T, "U": U, "comms_t": mipp.comms_t}
     cold = runs[0]
     warm = sorted(runs[1:], key=lambda r: r[0] + r[1])[len(runs[1:]) // 2]
     t = time.perf_counter()
@@ -374,6 +375,7 @@ def pst_leg(ctx, log_n, reps=5):
 
 
 _R1CS_LAST = None
+_PST_LAST = {}  # log_n -> the GPU legs' commitments and proof parts, for the CPU leg's parity check
 
 
 def r1cs_leg(ctx, log_cons, reps=3):
@@ -509,6 +511,7 @@ def sharded_leg(ctx, log_n, dist, dev):
     if rank != 0:
         return None
     ok = S.verify(ctx, S.PoseidonTranscript(), U, pt, v, pst_proof, mipp, T)
+    _PST_LAST[log_n] = {"comms": comms, "T": T, "U": U, "comms_t": mipp.comms_t}
     c, o = min(commits[1:]), min(opens[1:])
     return {"log_n": log_n, "commit_s": round(c, 4), "open_s": round(o, 4), "commit_plus_open_s": round(c + o, 4),
             **_wire_sizes(ctx, nv, pst_proof, mipp),
@@ -523,8 +526,8 @@ def sharded_leg(ctx, log_n, dist, dev):
 
 def cpu_leg(ctx, bk, sc, gpu_out, result):
     """C++ CPU restatement (oracle/cpu: arkworks-shaped msm_bigint_wnaf,
-    OpenMP) on this host's cores: the 2^20 MSM in full, the 2^20 sqrt-PST
-    commit + open in full, and a bounded row sample of the 2^24 commit."""
+    OpenMP) on this host's cores: the 2^20 MSM, the 2^20 and the 2^24 sqrt-PST
+    commit + open, each in full and checked against the GPU legs' outputs."""
     sys.path.insert(0, os.path.join(ROOT, "oracle", "cpu"))
     import orc
     from testudo_amd import sqrt_pst as S
@@ -558,26 +561,35 @@ def cpu_leg(ctx, bk, sc, gpu_out, result):
                       "gpu_speedup": (round((c_s + o_s) / gpu["commit_plus_open_s"], 1)
                                       if gpu.get("commit_plus_open_s") else None),
                       "sample": "full 2^20 commit + open (open includes get_q, as orc.pst_open computes it)"}
+        g20 = _PST_LAST.get(20)
+        if g20 is not None:
+            res["pst"]["matches_gpu"] = bool(np.array_equal(comms, g20["comms"]) and np.array_equal(T, g20["T"]))
         del Z
-        # 2^24: 256 of the 4096 row MSMs + their Miller loops, scaled by 16
+        # 2^24: the full commit + open (same inputs as the GPU 2^24 leg)
         lg = 24
-        nv = (lg + 1) // 2
-        srs = orc.SRS(nv, SEED + 1)
-        flat = srs.export()
-        Nr = 1 << nv
-        C = 1 << (lg // 2)
-        pg0 = flat[36:36 + Nr * 12].reshape(Nr, 12)
-        hv = flat[36 + Nr * 12:36 + Nr * 36].reshape(Nr, 24)[:C]
-        rows = 256
-        Zs, _ = orc.fr_stream(SEED + 24, rows * Nr)  # a sample block of the same shape (row-major)
+        srs = orc.SRS((lg + 1) // 2, SEED + 1)
+        Z, k = orc.fr_stream(SEED, 1 << lg)
+        pt, _ = orc.fr_stream(SEED, lg, k)
         t = time.perf_counter()
-        cm = orc.g1_msm_batch(pg0, Zs, rows, Nr, 1)
-        orc.miller_product(cm, hv[:rows])
-        s_s = time.perf_counter() - t
-        res["pst_2p24_commit"] = {"log_n": lg, "rows_sampled": rows, "rows_total": C,
-                                  "commit_s_extrapolated": round(s_s * C / rows, 2), "sample_s": round(s_s, 2),
-                                  "cores": threads,
-                                  "sample": "256 of 4096 row MSMs (4096 points each) + their Miller loops, x16"}
+        comms, T = orc.pst_commit(srs, Z, lg)
+        c_s = time.perf_counter() - t
+        t = time.perf_counter()
+        pr = orc.pst_open(srs, Z, lg, pt, comms)
+        o_s = time.perf_counter() - t
+        gpu = result.get("pst_2p24", {})
+        ent = {"log_n": lg, "commit_s": round(c_s, 3), "open_s": round(o_s, 3),
+               "commit_plus_open_s": round(c_s + o_s, 3), "cores": threads,
+               "gpu_speedup": (round((c_s + o_s) / gpu["commit_plus_open_s"], 1)
+                               if gpu.get("commit_plus_open_s") else None),
+               "sample": "full 2^24 commit (4096 row MSMs of 4096 points + 4096-pair IPP) + open (get_q, U, "
+                         "12-round MIPP, PST open), measured"}
+        g24 = _PST_LAST.get(24)
+        if g24 is not None:
+            ent["matches_gpu"] = bool(np.array_equal(comms, g24["comms"]) and np.array_equal(T, g24["T"])
+                                      and np.array_equal(pr["U"], g24["U"])
+                                      and np.array_equal(pr["comms_t"], g24["comms_t"]))
+        res["pst_2p24"] = ent
+        del Z
     except Exception as e:  # the headline CPU line must survive
         res["pst_error"] = repr(e)
     # R1CSProof::prove's sum-check section on the CPU (oracle/cpu, OpenMP) from

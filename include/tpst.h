@@ -232,6 +232,10 @@ int tpst_mlpc_check_2(tpst_ctx* ctx, int nv, const uint64_t* comm_h, const uint6
  * new_from_state2 -- a fresh sponge that absorbs the 32-byte uncompressed Fr. */
 int tpst_transcript_append_fr(tpst_transcript* t, const uint64_t* fr);
 int tpst_transcript_reset_fr(tpst_transcript* t, const uint64_t* fr);
+/* append_bytes (poseidon_transcript.rs:67-69): absorb a byte vector (u64
+ * length prefix, 47-byte chunks); `append` of any value = this over its
+ * Compress::No serialisation (poseidon_transcript.rs:22-28). */
+int tpst_transcript_append_bytes(tpst_transcript* t, const uint8_t* bytes, size_t n);
 
 /* ---- Spartan R1CS sum-checks (csrc/r1cs.hip) ------
  * R1CSInstance (r1csinstance.rs): num_cons x (2 num_vars) sparse A, B, C;
@@ -248,6 +252,12 @@ int tpst_r1cs_load(tpst_ctx* ctx, size_t num_cons, size_t num_vars, size_t num_i
 int tpst_r1cs_synthetic(tpst_ctx* ctx, size_t num_cons, size_t num_vars, size_t num_inputs, uint64_t seed,
                         tpst_r1cs** out, uint64_t* vars, uint64_t* inputs);
 void tpst_r1cs_free(tpst_r1cs* r);
+/* UniPoly::from_evals (unipoly.rs:15-45): n = 3 or 4 canonical evaluations at
+ * 0..n-1 -> n coefficients, constant first (host; the sum-check round encoding). */
+int tpst_unipoly_from_evals(const uint64_t* evals, int n, uint64_t* coeffs);
+/* EqPolynomial::evals (dense_mlpoly.rs:231-250): the MSB-first chi table of
+ * r[0..ell) (ell <= 30), computed on the device; out = 2^ell canonical Fr. */
+int tpst_eq_evals(tpst_ctx* ctx, const uint64_t* r, int ell, uint64_t* out);
 
 /* R1CSInstance::commit (r1csinstance.rs:313-344) = SparseMatPolynomial::
  * multi_commit over (A, B, C) (sparse_mlpoly.rs:490-517): the SPARK dense
@@ -310,6 +320,14 @@ int tpst_groth16_witness_map(tpst_ctx* ctx, tpst_groth16_pk* pk, tpst_r1cs* r1cs
 /* create_proof_with_reduction: rs = (r, s) canonical; Proof { a: G1, b: G2, c: G1 } */
 int tpst_groth16_prove(tpst_ctx* ctx, tpst_groth16_pk* pk, tpst_r1cs* r1cs, const uint64_t* vars,
                        const uint64_t* inputs, const uint64_t* rs, uint64_t* A, uint64_t* B, uint64_t* C);
+/* Groth16::verify_proof (ark-groth16 verifier.rs): TPST_OK if the proof
+ * verifies, TPST_E_VERIFY if it does not or if any element is malformed
+ * (coordinate >= p, off the curve, outside the r-torsion subgroup, input >= r:
+ * what Validate::Yes deserialisation rejects); TPST_E_ARG if n_abc !=
+ * n_inputs + 1.  Canonical affine points, vk as tpst_groth16_vk returns it. */
+int tpst_groth16_verify(tpst_ctx* ctx, const uint64_t* alpha_g1, const uint64_t* beta_g2, const uint64_t* gamma_g2,
+                        const uint64_t* delta_g2, const uint64_t* gamma_abc_g1, size_t n_abc, const uint64_t* inputs,
+                        size_t n_inputs, const uint64_t* A, const uint64_t* B, const uint64_t* C);
 
 /* ---- arkworks wire format (csrc/serialize.hip; host only, no context) ------
  * CanonicalSerialize with Compress::Yes (ark-serialize 0.4): G1 48 B, G2 96 B
@@ -334,7 +352,8 @@ int tpst_de_open_proof(const uint8_t* pst, size_t pst_len, const uint8_t* mipp, 
                        tpst_open_proof* out);
 /* CommitterKey { nv, powers_of_g, powers_of_h, g, h } from the flat SRS of
  * tpst_srs_export (benches/pst.rs:43-46) */
-int tpst_ser_committer_key(int nv, const uint64_t* srs_flat, uint8_t* out, size_t cap, size_t* len);
+int tpst_ser_committer_key(int nv, const uint64_t* srs_flat, size_t flat_len, uint8_t* out, size_t cap,
+                           size_t* len);  /* flat_len == tpst_srs_flat_len(nv) */
 
 /* ---- utilities ----------------------------------------------------------- */
 /* out[i] = scalars[i] * G1 generator (affine, canonical); synthetic bases */

@@ -174,6 +174,22 @@ def test_verify_rejects_malformed_proof_elements(ctx):
     m3 = S.MippProof(mipp.comms_t.copy(), mipp.comms_u, mipp.final_a, mipp.final_h, mipp.pst_proof_h)
     m3.comms_t[0, 1] = shifted(mipp.comms_t[0, 1])
     assert not S.verify(ctx, S.PoseidonTranscript(), U, pt, v, pst_proof, m3, T)
+    # comms_t outside GT: a canonical Fq12 that is not a pairing output (ark's
+    # PairingOutput deserialisation rejects it), and a cyclotomic element of
+    # the wrong order (t_l times a non-GT element of the cyclotomic subgroup)
+    m4 = S.MippProof(mipp.comms_t.copy(), mipp.comms_u, mipp.final_a, mipp.final_h, mipp.pst_proof_h)
+    m4.comms_t[0, 0] = G.gt_array([("%x" % (k + 2)) for k in range(12)])
+    assert not S.verify(ctx, S.PoseidonTranscript(), U, pt, v, pst_proof, m4, T)
+    t0 = O.fq12_from_tower([limbs_to_int(mipp.comms_t[0, 0][6 * i:6 * i + 6]) for i in range(12)])
+    z = O.fq12_from_tower([k + 3 for k in range(12)])
+    cyc = O.f12_mul(O.f12_frob(O.f12_mul(O.f12_conj(z), O.f12_inv(z)), 2), O.f12_mul(O.f12_conj(z), O.f12_inv(z)))
+    assert O.f12_pow(cyc, O.R) != O.f12_one()  # cyclotomic, not in GT
+    m5 = S.MippProof(mipp.comms_t.copy(), mipp.comms_u, mipp.final_a, mipp.final_h, mipp.pst_proof_h)
+    m5.comms_t[0, 0] = G.gt_array(["%x" % c for c in O.fq12_to_tower(O.f12_mul(t0, cyc))])
+    assert not S.verify(ctx, S.PoseidonTranscript(), U, pt, v, pst_proof, m5, T)
+    # a valid GT element in the wrong place: t_l <-> t_r swapped
+    m6 = S.MippProof(mipp.comms_t[:, ::-1].copy(), mipp.comms_u, mipp.final_a, mipp.final_h, mipp.pst_proof_h)
+    assert not S.verify(ctx, S.PoseidonTranscript(), U, pt, v, pst_proof, m6, T)
     # a wrong-sized proof vector or an out-of-range scalar
     badpt = pt.copy()
     badpt[0] = fr_array([O.R - 1])[0]

@@ -10,7 +10,7 @@ import pytest
 import bls377 as O
 import groth16 as G
 import r1cs as Q
-from testudo_amd.encoding import fr_array, g1_from_array, g2_from_array, limbs_to_int
+from testudo_amd.encoding import fr_array, g1_from_array, g2_array, g2_from_array, limbs_to_int
 
 R = O.R
 TOXIC = (0x1234567, 0xA1FA, 0xBE7A, 0x6A33A, 0xDE17A)
@@ -152,3 +152,58 @@ def test_groth16_2p14_verifies(ctx):
     assert pk.domain_size == 1 << 15
     proof = D.prove(pk, inst, vars_, inputs, fr_array([0x1111]), fr_array([0x2222]))
     assert D.verify(ctx, pk.vk(), inputs, proof)
+
+
+@pytest.mark.gpu
+def test_groth16_verify_rejects_malformed_elements(ctx):
+    """tpst_groth16_verify validates before pairing: an off-curve
+    A, a B on the twist but outside the r-torsion subgroup, a coordinate >= p,
+    an input >= r and a malformed verifying-key point are invalid proofs."""
+    import serialize as SZ
+    D, inst, vars_, inputs, pk = _gpu(ctx, 32, 16, 3, 78)
+    vk = pk.vk()
+    proof = D.prove(pk, inst, vars_, inputs, fr_array([5]), fr_array([6]))
+    assert D.verify(ctx, vk, inputs, proof)
+    off = proof.a.copy()
+    off[6] ^= 1  # y + - 1: off the curve
+    assert not O.g1_on_curve(g1_from_array(off)[0])
+    assert not D.verify(ctx, vk, inputs, D.Proof(off, proof.b, proof.c))
+    # a twist point of the full group order (no cofactor clearing)
+    k = 1
+    while True:
+        x = (k, 1)
+        y2 = O.f2_add(O.f2_mul(O.f2_sqr(x), x), O.G2_B)
+        y = SZ._fq2_sqrt(y2)
+        if y is not None and not O.g2_in_subgroup((x, y)):
+            break
+        k += 1
+    bad_b = g2_array([(x, y)])[0]
+    assert not D.verify(ctx, vk, inputs, D.Proof(proof.a, bad_b, proof.c))
+    big = proof.c.copy()
+    big[:6] = np.array([(O.P >> (64 * i)) & (2 ** 64 - 1) for i in range(6)], dtype=np.uint64)
+    assert not D.verify(ctx, vk, inputs, D.Proof(proof.a, proof.b, big))
+    ge_r = inputs.copy()
+    ge_r[0] = fr_array([0])[0] + np.array([(O.R >> (64 * i)) & (2 ** 64 - 1) for i in range(4)], dtype=np.uint64)
+    assert not D.verify(ctx, vk, ge_r, proof)
+    vk2 = D.VerifyingKey(vk.alpha_g1, vk.beta_g2, vk.gamma_g2, bad_b, vk.gamma_abc_g1)
+    assert not D.verify(ctx, vk2, inputs, proof)
+
+
+@pytest.mark.gpu
+def test_groth16_key_bound_to_context(ctx):
+    """A proving key or instance presented through a context other than the
+    one that built it is an argument error (TPST_E_ARG), never a launch on
+    another context's stream and arena."""
+    from testudo_amd import Context
+    from testudo_amd.encoding import ptr
+    D, inst, vars_, inputs, pk = _gpu(ctx, 16, 16, 2, 79)
+    other = Context(0)
+    try:
+        bufs = [np.zeros(w, dtype=np.uint64) for w in (12, 24, 24, 24, 36)]
+        assert other.lib.tpst_groth16_vk(other.h, pk.h, *[ptr(b) for b in bufs]) == -1
+        a, b, c = (np.zeros(w, dtype=np.uint64) for w in (12, 24, 12))
+        rs = fr_array([5, 6])
+        assert other.lib.tpst_groth16_prove(other.h, pk.h, inst.h, ptr(np.ascontiguousarray(vars_)),
+                                            ptr(np.ascontiguousarray(inputs)), ptr(rs), ptr(a), ptr(b), ptr(c)) == -1
+    finally:
+        other.close()

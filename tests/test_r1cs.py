@@ -213,3 +213,29 @@ def test_r1cs_commit_spark_vs_oracle(ctx):
     ops, mem = inst2.commit(b"lbl")
     r_ops, r_mem = Q.spark_multi_commit((A, B, Cm), 16, 16, b"lbl")
     assert g1_from_array(ops) == r_ops and g1_from_array(mem) == r_mem
+
+
+@pytest.mark.gpu
+def test_r1cs_prove_2p20_vs_cpu_oracle(ctx):
+    """BASELINE configs[4]'s live path at full size: R1CSProof::prove over a
+    2^20-constraint, 2^20-variable synthetic instance (the bench's), bit-exact
+    against the C++ restatement (oracle/cpu, OpenMP): the witness commitment's
+    T from orc.pst_commit, then every sum-check round polynomial, rx, ry, the
+    phase-two claims and the transcript state after the sum-checks."""
+    import orc
+    from testudo_amd import r1cs as D
+    from testudo_amd import sqrt_pst as S
+    log_cons, seed, srs_seed = 20, 0x7E57D0 + 7, 0x7E57D0 + 1
+    n = 1 << log_cons
+    S.srs_setup(ctx, (log_cons + 1) // 2, srs_seed)
+    inst, vars_, inputs = D.R1CSInstance.produce_synthetic_r1cs(ctx, n, n, 10, seed)
+    proof, rx, ry = D.R1CSProof.prove(inst, vars_, inputs, S.PoseidonTranscript())
+    srs = orc.SRS((log_cons + 1) // 2, srs_seed)
+    _, T = orc.pst_commit(srs, vars_, log_cons)
+    assert np.array_equal(np.asarray(proof.T, dtype=np.uint64).reshape(72), np.asarray(T).reshape(72))
+    cpu = orc.r1cs_sumchecks(n, n, 10, seed, proof.T)
+    assert np.array_equal(cpu["sc1"], proof.sc_proof_phase1)
+    assert np.array_equal(cpu["sc2"], proof.sc_proof_phase2)
+    assert np.array_equal(cpu["rx"], proof.rx) and np.array_equal(cpu["ry"], proof.ry)
+    assert np.array_equal(cpu["claims_phase2"], proof.claims_phase2)
+    assert np.array_equal(cpu["sat_state"], proof.transcript_sat_state)

@@ -117,3 +117,33 @@ def test_invalid_encodings_rejected():
         S.de_open_proof(b_pst[:-1], b_mipp)
     with pytest.raises(S.SerializationError):
         S.de_open_proof(b_pst, b_mipp + b"\x00")
+
+
+def test_committer_key_length_checked():
+    """tpst_ser_committer_key takes the flat length and rejects a mismatch
+    (short array or wrong nv) instead of reading past the buffer."""
+    d = G.load("sqrt_pst_n5.json")
+    flat = G.srs_flat(d)
+    nv = d["srs_nv"]
+    assert len(S.ser_committer_key(nv, flat)) > 0
+    with pytest.raises(S.SerializationError):
+        S.ser_committer_key(nv, flat[:-1])
+    with pytest.raises(S.SerializationError):
+        S.ser_committer_key(nv + 1, flat)
+
+
+def test_multilinear_pc_rejects_non_power_of_two():
+    """MultilinearPC calls raise on a non-power-of-two evaluation vector (the
+    reference's MultilinearExtension has 2^nv evaluations) before any device
+    work: no context is needed to see the error."""
+    from testudo_amd.engine import TpstError
+    from testudo_amd.sqrt_pst import MultilinearPC
+    bad = np.zeros((3, 4), dtype=np.uint64)
+    for fn in (MultilinearPC.commit, MultilinearPC.commit_g2):
+        with pytest.raises(TpstError):
+            fn(None, bad)
+    for fn in (MultilinearPC.open, MultilinearPC.open_g1):
+        with pytest.raises(TpstError):
+            fn(None, bad, np.zeros((1, 4), dtype=np.uint64))
+    with pytest.raises(TpstError):
+        MultilinearPC.commit(None, np.zeros((0, 4), dtype=np.uint64))

@@ -75,6 +75,9 @@ PROTOTYPES = [
     ("tpst_mlpc_check_2", C.c_int, [_vp, C.c_int, _u64p, _u64p, _u64p, _u64p]),
     ("tpst_transcript_append_fr", C.c_int, [_vp, _u64p]),
     ("tpst_transcript_reset_fr", C.c_int, [_vp, _u64p]),
+    ("tpst_transcript_append_bytes", C.c_int, [_vp, C.c_char_p, _sz]),
+    ("tpst_unipoly_from_evals", C.c_int, [_u64p, C.c_int, _u64p]),
+    ("tpst_eq_evals", C.c_int, [_vp, _u64p, C.c_int, _u64p]),
     ("tpst_r1cs_load", C.c_int, [_vp, _sz, _sz, _sz, C.POINTER(_sz), C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp),
                                  C.POINTER(_vp)]),
     ("tpst_r1cs_synthetic", C.c_int, [_vp, _sz, _sz, _sz, C.c_uint64, C.POINTER(_vp), _u64p, _u64p]),
@@ -87,6 +90,8 @@ PROTOTYPES = [
     ("tpst_groth16_vk", C.c_int, [_vp, _vp, _u64p, _u64p, _u64p, _u64p, _u64p]),
     ("tpst_groth16_witness_map", C.c_int, [_vp, _vp, _vp, _u64p, _u64p, _u64p]),
     ("tpst_groth16_prove", C.c_int, [_vp, _vp, _vp, _u64p, _u64p, _u64p, _u64p, _u64p, _u64p]),
+    ("tpst_groth16_verify", C.c_int, [_vp, _u64p, _u64p, _u64p, _u64p, _u64p, _sz, _u64p, _sz, _u64p, _u64p,
+                                      _u64p]),
     ("tpst_ser_g1", C.c_int, [_u64p, C.c_char_p]),
     ("tpst_ser_g2", C.c_int, [_u64p, C.c_char_p]),
     ("tpst_de_g1", C.c_int, [C.c_char_p, _u64p]),
@@ -95,7 +100,7 @@ PROTOTYPES = [
     ("tpst_ser_pst_proof", C.c_int, [_vp, C.c_char_p, _sz, C.POINTER(_sz)]),
     ("tpst_ser_mipp_proof", C.c_int, [_vp, C.c_char_p, _sz, C.POINTER(_sz)]),
     ("tpst_de_open_proof", C.c_int, [C.c_char_p, _sz, C.c_char_p, _sz, _vp]),
-    ("tpst_ser_committer_key", C.c_int, [C.c_int, _u64p, C.c_char_p, _sz, C.POINTER(_sz)]),
+    ("tpst_ser_committer_key", C.c_int, [C.c_int, _u64p, _sz, C.c_char_p, _sz, C.POINTER(_sz)]),
     ("tpst_profile_enable", C.c_int, [_vp, C.c_int]),
     ("tpst_profile_reset", C.c_int, [_vp]),
     ("tpst_profile_read", C.c_int, [_vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),

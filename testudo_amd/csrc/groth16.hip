@@ -275,6 +275,7 @@ void fr_canon(const Fr& a, uint32_t* o) {
 
 // ================================================================ state ==
 struct tpst_groth16_pk {
+  const tpst_ctx* owner = nullptr;  // the context whose device, stream and arena the key uses
   size_t num_cons = 0, nv = 0, ni = 0, ncols = 0;
   size_t nq = 0;      // variables in the QAP: nv witness + 1 + ni instance
   size_t n = 0;       // domain size
@@ -322,6 +323,7 @@ static hipError_t ntt(hipStream_t s, uint32_t* a, size_t n, int lg, const uint32
 
 extern "C" int tpst_groth16_setup(tpst_ctx* ctx, tpst_r1cs* R, const uint64_t* toxic, tpst_groth16_pk** out) {
   if (!ctx || !R || !toxic || !out) return setup_fail(ctx, "null argument");
+  if (R->owner != ctx) return setup_fail(ctx, "instance belongs to another context");
   *out = nullptr;
   for (int k = 0; k < 5; k++) {
     if (!fr_ok_host(toxic + 4 * k)) return setup_fail(ctx, "toxic waste value >= r");
@@ -332,6 +334,7 @@ extern "C" int tpst_groth16_setup(tpst_ctx* ctx, tpst_r1cs* R, const uint64_t* t
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
   std::unique_ptr<tpst_groth16_pk> P(new tpst_groth16_pk());
+  P->owner = ctx;
   P->num_cons = R->num_cons;
   P->nv = R->num_vars;
   P->ni = R->num_inputs;
@@ -460,6 +463,7 @@ extern "C" int tpst_groth16_vk(tpst_ctx* ctx, const tpst_groth16_pk* pk, uint64_
                                uint64_t* gamma_g2, uint64_t* delta_g2, uint64_t* gamma_abc_g1) {
   if (!ctx || !pk || !alpha_g1 || !beta_g2 || !gamma_g2 || !delta_g2 || !gamma_abc_g1)
     return fail(ctx, TPST_E_ARG, "null argument");
+  if (pk->owner != ctx) return fail(ctx, TPST_E_ARG, "proving key belongs to another context");
   std::lock_guard<std::mutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
@@ -508,6 +512,7 @@ static hipError_t witness_map(tpst_groth16_pk* P, const tpst_r1cs* R, hipStream_
 
 static int check_inputs(tpst_ctx* ctx, const tpst_groth16_pk* P, const tpst_r1cs* R, const uint64_t* vars,
                         const uint64_t* inputs) {
+  if (P->owner != ctx || R->owner != ctx) return fail(ctx, TPST_E_ARG, "key or instance belongs to another context");
   if (R->num_cons != P->num_cons || R->num_vars != P->nv || R->num_inputs != P->ni)
     return fail(ctx, TPST_E_ARG, "proving key does not match the instance");
   for (size_t i = 0; i < P->nv; i++)
@@ -608,4 +613,66 @@ extern "C" int tpst_groth16_prove(tpst_ctx* ctx, tpst_groth16_pk* pk, tpst_r1cs*
   memcpy(C, h + 12, 96);
   memcpy(B, h + 24, 192);
   return TPST_OK;
+}
+
+// Groth16::verify_proof (ark-groth16 verifier.rs, r1csproof.rs verifier side):
+// every element is validated first -- canonical coordinates, on the curve, in
+// the r-torsion subgroup, inputs < r -- as arkworks' deserialisation with
+// Validate::Yes would; then e(A, B) == e(alpha, beta) e(IC, gamma) e(C, delta)
+// with IC = gamma_abc[0] + sum_i inputs_i gamma_abc[i + 1] (device MSM), as one
+// device multi-pairing of (A, B), (-alpha, beta), (-IC, gamma), (-C, delta).
+bool tpst_internal_g1_valid(const uint64_t* p);  // pst_api.hip
+bool tpst_internal_g2_valid(const uint64_t* p);
+
+extern "C" int tpst_groth16_verify(tpst_ctx* ctx, const uint64_t* alpha_g1, const uint64_t* beta_g2,
+                                   const uint64_t* gamma_g2, const uint64_t* delta_g2, const uint64_t* gamma_abc_g1,
+                                   size_t n_abc, const uint64_t* inputs, size_t n_inputs, const uint64_t* A,
+                                   const uint64_t* B, const uint64_t* C) {
+  if (!ctx || !alpha_g1 || !beta_g2 || !gamma_g2 || !delta_g2 || !gamma_abc_g1 || (n_inputs && !inputs) || !A ||
+      !B || !C)
+    return fail(ctx, TPST_E_ARG, "null argument");
+  if (n_abc != n_inputs + 1) return fail(ctx, TPST_E_ARG, "wrong number of public inputs");
+  for (size_t i = 0; i < n_inputs; i++)
+    if (!fr_ok_host(inputs + 4 * i)) return fail(ctx, TPST_E_VERIFY, "public input >= r");
+  if (!tpst_internal_g1_valid(A) || !tpst_internal_g2_valid(B) || !tpst_internal_g1_valid(C))
+    return fail(ctx, TPST_E_VERIFY, "malformed proof element");
+  if (!tpst_internal_g1_valid(alpha_g1) || !tpst_internal_g2_valid(beta_g2) || !tpst_internal_g2_valid(gamma_g2) ||
+      !tpst_internal_g2_valid(delta_g2))
+    return fail(ctx, TPST_E_VERIFY, "malformed verifying key");
+  for (size_t i = 0; i < n_abc; i++)
+    if (!tpst_internal_g1_valid(gamma_abc_g1 + 12 * i)) return fail(ctx, TPST_E_VERIFY, "malformed verifying key");
+  std::vector<uint64_t> sc(4 * n_abc, 0);
+  sc[0] = 1;
+  if (n_inputs) memcpy(sc.data() + 4, inputs, n_inputs * 32);
+  uint64_t ic[12];
+  if (int rc = tpst_g1_msm(ctx, gamma_abc_g1, n_abc, sc.data(), n_abc, ic)) return rc;
+  // -P of an affine point: y -> p - y (infinity, all-zero, stays)
+  auto neg = [](const uint64_t* p, uint64_t* o) {
+    memcpy(o, p, 96);
+    bool inf = true;
+    for (int k = 0; k < 12; k++) inf = inf && !p[k];
+    if (inf) return;
+    static const uint64_t P6[6] = {0x8508c00000000001ull, 0x170b5d4430000000ull, 0x1ef3622fba094800ull,
+                                   0x1a22d9f300f5138full, 0xc63b05c06ca1493bull, 0x01ae3a4617c510eaull};
+    unsigned __int128 borrow = 0;
+    for (int k = 0; k < 6; k++) {
+      const unsigned __int128 d = (unsigned __int128)P6[k] - p[6 + k] - borrow;
+      o[6 + k] = (uint64_t)d;
+      borrow = (d >> 64) ? 1 : 0;
+    }
+  };
+  uint64_t g1[4 * 12], g2[4 * 24];
+  memcpy(g1, A, 96);
+  neg(alpha_g1, g1 + 12);
+  neg(ic, g1 + 24);
+  neg(C, g1 + 36);
+  memcpy(g2, B, 192);
+  memcpy(g2 + 24, beta_g2, 192);
+  memcpy(g2 + 48, gamma_g2, 192);
+  memcpy(g2 + 72, delta_g2, 192);
+  uint64_t gt[72];
+  if (int rc = tpst_multi_pairing(ctx, g1, g2, 4, gt)) return rc;
+  bool one = gt[0] == 1;
+  for (int k = 1; k < 72; k++) one = one && !gt[k];
+  return one ? TPST_OK : fail(ctx, TPST_E_VERIFY, "pairing check failed");
 }

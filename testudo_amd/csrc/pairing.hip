@@ -471,6 +471,100 @@ hipError_t multi_pairing(Arena& ar, hipStream_t s, const uint32_t* d_g1, const u
   return multi_pairing_prepared(ar, s, d_g1, d_g2, coeffs, groups, n, d_out);
 }
 
+// ---- GT exponentiation on the wave engine (MippProof::verify, mipp.rs:263-283)
+// For f in GT (order r), f^p = f^x since p = x (mod r).  With e = sum_i e_i x^i
+// (base-x digits; e < r < x^4, so the digits are exact, each < 2^64),
+//     f^e = prod_i frob^i(f)^(e_i),
+// a 4-way simultaneous exponentiation with 64-bit digits: 63 cyclotomic
+// squarings and <= 64 products from the 16-entry subset table of
+// (f, f^p, f^p^2, f^p^3), where the plain square-and-multiply needs 253
+// squarings.  Membership first -- what arkworks' Validate::Yes
+// deserialisation of a PairingOutput checks: f^(p^4) f == f^(p^2) puts f in
+// the cyclotomic subgroup (order Phi12(p), so cyclotomic squaring applies),
+// and then f^p == f^x puts it in GT, because gcd(p - x, Phi12(p)) = r for
+// BLS12-377 (tests/test_kat_ref.py checks it).  ok[i] = 1 iff f_i is in GT
+// (out[i] is only meaningful then).
+constexpr int GP_REGS = 20;  // R0 scratch, T1..T15 subset table, ACC, TMP, X1, X2
+constexpr size_t GP_LDS = (size_t)(FW_PROG + (wave::N_CONSTS + 64 + 12 * GP_REGS) * wave::SLOT) * 4;
+static_assert(GP_LDS <= 65536, "GT pow kernel LDS");
+
+__device__ bool regs_equal(const wave::lds_t* lds, int a, int b) {
+  const int lane = threadIdx.x & 63;
+  const bool same = lane >= 12 || eq(wave::get_slot(lds, a + lane), wave::get_slot(lds, b + lane));
+  return __all(same ? 1 : 0) != 0;
+}
+
+__global__ void __launch_bounds__(64) k_gt_pow_wave(const Fq12* __restrict__ base, const uint64_t* __restrict__ digits,
+                                                    size_t n, Fq12* __restrict__ out, uint32_t* __restrict__ ok) {
+  extern __shared__ uint4 smem4[];
+  wave::lds_t* prog = (wave::lds_t*)(smem4);
+  wave::lds_t* vals = prog + FW_PROG;
+  wave::load_set(prog, FE_SET);
+  wave::load_consts(vals, 0);
+  __syncthreads();
+  const size_t i = blockIdx.x;
+  if (i >= n) return;
+  const wave::Eng e{vals, wave::N_CONSTS, 0};
+#define R(k) (wave::N_CONSTS + 64 + 12 * (k))
+  const int ACC = R(16), TMP = R(17), X1 = R(18), X2 = R(19);
+  const wave::lds_t* P = prog;
+  wave::load_f12(vals, R(1), base + i);
+  // cyclotomic subgroup: f^(p^4) f == f^(p^2)
+  wave::run(e, P + FE_SET.off[FE_FROB2], R(1), 0, X1);
+  wave::run(e, P + FE_SET.off[FE_FROB2], X1, 0, X2);
+  wave::run(e, P + FE_SET.off[FE_MUL], X2, R(1), R(0));
+  bool good = regs_equal(vals, R(0), X1);
+  // GT: f^p == f^x
+  wave::run(e, P + FE_SET.off[FE_FROB1], R(1), 0, R(2));
+  if (good) {
+    const int fx = fe_exp_by_x(e, P, R(1), X1, X2);
+    good = regs_equal(vals, fx, R(2));
+  }
+  const int lane = threadIdx.x & 63;
+  if (lane == 0) ok[i] = good ? 1u : 0u;
+  if (!good) return;
+  // subset table T[m] = prod_{bit j of m} f^(p^j)
+  wave::run(e, P + FE_SET.off[FE_FROB2], R(1), 0, R(4));
+  wave::run(e, P + FE_SET.off[FE_FROB1], R(4), 0, R(8));
+  for (int m = 3; m < 16; m++) {
+    if ((m & (m - 1)) == 0) continue;  // powers of two are the bases themselves
+    const int hi = 1 << (31 - __builtin_clz(m));
+    wave::run(e, P + FE_SET.off[FE_MUL], R(m - hi), R(hi), R(m));
+  }
+  const uint64_t* d = digits + 4 * i;
+  int acc = -1;
+  for (int b = 63; b >= 0; b--) {
+    if (acc >= 0) {
+      const int nxt = acc == ACC ? TMP : ACC;
+      wave::run(e, P + FE_SET.off[FE_CYC], acc, 0, nxt);
+      acc = nxt;
+    }
+    const int mask = (int)((d[0] >> b) & 1) | (int)(((d[1] >> b) & 1) << 1) | (int)(((d[2] >> b) & 1) << 2) |
+                     (int)(((d[3] >> b) & 1) << 3);
+    if (!mask) continue;
+    if (acc < 0) {
+      acc = R(mask);
+    } else {
+      const int nxt = acc == ACC ? TMP : ACC;
+      wave::run(e, P + FE_SET.off[FE_MUL], acc, R(mask), nxt);
+      acc = nxt;
+    }
+  }
+  if (acc < 0) {
+    wave::set_one(vals, ACC);
+    acc = ACC;
+  }
+  wave::store_f12(vals, acc, out + i);
+#undef R
+}
+
+hipError_t gt_pow_wave(hipStream_t s, const Fq12* d_base, const uint64_t* d_digits, size_t n, Fq12* d_out,
+                       uint32_t* d_ok) {
+  if (!n) return hipSuccess;
+  k_gt_pow_wave<<<(unsigned)n, 64, GP_LDS, s>>>(d_base, d_digits, n, d_out, d_ok);
+  return hipGetLastError();
+}
+
 __global__ void k_fq12_from_mont(const Fq12* __restrict__ in, uint32_t* __restrict__ out, size_t n) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n * 12) return;

@@ -42,6 +42,12 @@ hipError_t gt_product_final(Arena& ar, hipStream_t s, const Fq12* d_partials, si
 hipError_t multi_pairing(Arena& ar, hipStream_t s, const uint32_t* d_g1, const uint32_t* d_g2, size_t groups,
                          size_t n, Fq12* d_out);
 
+// GT exponentiations (verifier): out[i] = base[i]^e_i with e_i given by its
+// base-x digits (4 x u64, e = sum_j digits[4 i + j] x^j) after a GT membership
+// test of base[i]; ok[i] = 1 iff base[i] is in GT.  Montgomery Fq12.
+hipError_t gt_pow_wave(hipStream_t s, const Fq12* d_base, const uint64_t* d_digits, size_t n, Fq12* d_out,
+                       uint32_t* d_ok);
+
 hipError_t fq12_from_mont(hipStream_t s, const Fq12* d_in, uint32_t* d_out, size_t n);
 
 }  // namespace tpst

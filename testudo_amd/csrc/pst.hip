@@ -201,25 +201,6 @@ hipError_t affine_rot(hipStream_t s, const uint32_t* d_in, uint32_t* d_out, size
   return hipGetLastError();
 }
 
-__global__ void k_gt_pow(const Fq12* __restrict__ base, const uint32_t* __restrict__ exps, size_t n,
-                         Fq12* __restrict__ out) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const Fq12 b = base[i];
-  Fq12 r = Fq12::one();
-  for (int bit = 252; bit >= 0; bit--) {
-    r = sqr(r);
-    if ((exps[8 * i + (bit >> 5)] >> (bit & 31)) & 1) r = mul(r, b);
-  }
-  out[i] = r;
-}
-
-hipError_t gt_pow(hipStream_t s, const Fq12* d_base, const uint32_t* d_exps, size_t n, Fq12* d_out) {
-  if (!n) return hipSuccess;
-  k_gt_pow<<<grid_for(n, 32), 32, 0, s>>>(d_base, d_exps, n, d_out);
-  return hipGetLastError();
-}
-
 // MIPP fold scalars over the original bases (fbt.h strided groups):
 // fold:  out[k] = W[k / len]                      (a^(r)_i = sum_t W_t a_{i + t len})
 // cross: out[k] = W[k / len] * y[(k % len + s) % len]   (u_l / u_r, mipp.rs:66-75)

@@ -237,7 +237,7 @@ struct Sponge {
     std::vector<uint8_t> buf(8 + n);
     const uint64_t len = n;
     memcpy(buf.data(), &len, 8);
-    memcpy(buf.data() + 8, d, n);
+    if (n) memcpy(buf.data() + 8, d, n);
     std::vector<Fq> e;
     for (size_t o = 0; o < buf.size(); o += 47) {
       uint64_t l[6] = {0, 0, 0, 0, 0, 0};
@@ -599,6 +599,10 @@ extern "C" int tpst_srs_export(tpst_ctx* ctx, uint64_t* flat) {
   return TPST_OK;
 }
 
+// internal (groth16.hip): the same element validation as the PST verifier
+bool tpst_internal_g1_valid(const uint64_t* p) { return point_valid<Fq>(p); }
+bool tpst_internal_g2_valid(const uint64_t* p) { return point_valid<Fq2>(p); }
+
 // ============================================================ transcript ==
 // internal (r1cs.hip): the device copy of a whole polynomial's evaluations
 // (canonical Fr, original order), or nullptr for a column shard
@@ -625,6 +629,18 @@ extern "C" int tpst_transcript_append_gt(tpst_transcript* t, const uint64_t* gt)
   Sponge sp;
   sp.load(t);
   sp.absorb_bytes((const uint8_t*)gt, 576);
+  sp.store(t);
+  return TPST_OK;
+}
+
+// append_bytes (poseidon_transcript.rs:67-69): Absorb of a Vec<u8> (u64 length
+// prefix, 47-byte chunks); `append` of any CanonicalSerialize value is this
+// over its Compress::No bytes (poseidon_transcript.rs:22-28)
+extern "C" int tpst_transcript_append_bytes(tpst_transcript* t, const uint8_t* b, size_t n) {
+  if (!t || (n && !b)) return TPST_E_ARG;
+  Sponge sp;
+  sp.load(t);
+  sp.absorb_bytes(b, n);
   sp.store(t);
   return TPST_OK;
 }
@@ -1793,17 +1809,38 @@ extern "C" int tpst_pst_verify(tpst_ctx* ctx, tpst_transcript* tr, int n, const 
       for (int q = 0; q < 12; q++) c[q] = fq_canon(T + 6 * q);
     }
     if (k) {
+      // base-x digits of each exponent (e < r < x^4): GT pows by 4-way
+      // Frobenius splitting on the device, after a GT membership test
+      std::vector<uint64_t> dg(4 * k);
+      for (size_t j = 0; j < k; j++) {
+        uint64_t q[4];
+        memcpy(q, &ex[4 * j], 32);
+        for (int t = 0; t < 4; t++) {
+          unsigned __int128 rem = 0;
+          for (int l = 3; l >= 0; l--) {
+            const unsigned __int128 cur = (rem << 64) | q[l];
+            q[l] = (uint64_t)(cur / params::BLS_X);
+            rem = cur % params::BLS_X;
+          }
+          dg[4 * j + t] = (uint64_t)rem;
+        }
+      }
       hipStream_t s = ctx->stream;
-      DevBuf db, de, dout;
+      DevBuf db, de, dout, dok;
       TPST_HIP(ctx, db.alloc(k * sizeof(Fq12)));
       TPST_HIP(ctx, de.alloc(k * 32));
       TPST_HIP(ctx, dout.alloc(k * sizeof(Fq12)));
+      TPST_HIP(ctx, dok.alloc(k * 4));
       TPST_HIP(ctx, hipMemcpyAsync(db.p, bases.data(), k * sizeof(Fq12), hipMemcpyHostToDevice, s));
-      TPST_HIP(ctx, hipMemcpyAsync(de.p, ex.data(), k * 32, hipMemcpyHostToDevice, s));
-      TPST_HIP(ctx, gt_pow(s, (Fq12*)db.p, de.u(), k, (Fq12*)dout.p));
+      TPST_HIP(ctx, hipMemcpyAsync(de.p, dg.data(), k * 32, hipMemcpyHostToDevice, s));
+      TPST_HIP(ctx, gt_pow_wave(s, (const Fq12*)db.p, (const uint64_t*)de.p, k, (Fq12*)dout.p, dok.u()));
       std::vector<Fq12> pw(k);
+      std::vector<uint32_t> okv(k);
       TPST_HIP(ctx, hipMemcpyAsync(pw.data(), dout.p, k * sizeof(Fq12), hipMemcpyDeviceToHost, s));
+      TPST_HIP(ctx, hipMemcpyAsync(okv.data(), dok.p, k * 4, hipMemcpyDeviceToHost, s));
       TPST_HIP(ctx, hipStreamSynchronize(s));
+      for (uint32_t o : okv)
+        if (!o) return fail(ctx, TPST_E_VERIFY, "comms_t element outside GT");
       for (auto& x : pw) acc = mul(acc, x);
     }
     uint64_t ft[72];

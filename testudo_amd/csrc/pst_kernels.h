@@ -52,7 +52,4 @@ hipError_t xyzz_to_affine_mont(hipStream_t s, const Xyzz<F>* d_in, uint32_t* d_o
 // affine rotation by half: out[j] = in[(j + n/2) % n], `words` u32 per point
 hipError_t affine_rot(hipStream_t s, const uint32_t* d_in, uint32_t* d_out, size_t n, size_t words);
 
-// GT: out[i] = base[i]^(canonical exps[i]) , n independent
-hipError_t gt_pow(hipStream_t s, const Fq12* d_base, const uint32_t* d_exps, size_t n, Fq12* d_out);
-
 }  // namespace tpst

@@ -389,6 +389,7 @@ extern "C" int tpst_r1cs_load(tpst_ctx* ctx, size_t num_cons, size_t num_vars, s
   std::lock_guard<std::mutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   std::unique_ptr<tpst_r1cs> R(new tpst_r1cs());
+  R->owner = ctx;
   R->num_cons = num_cons;
   R->num_vars = num_vars;
   R->num_inputs = num_inputs;
@@ -433,6 +434,7 @@ extern "C" int tpst_r1cs_synthetic(tpst_ctx* ctx, size_t num_cons, size_t num_va
   std::lock_guard<std::mutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   std::unique_ptr<tpst_r1cs> R(new tpst_r1cs());
+  R->owner = ctx;
   R->num_cons = num_cons;
   R->num_vars = num_vars;
   R->num_inputs = num_inputs;
@@ -456,6 +458,46 @@ extern "C" int tpst_r1cs_synthetic(tpst_ctx* ctx, size_t num_cons, size_t num_va
 }
 
 extern "C" void tpst_r1cs_free(tpst_r1cs* r) { delete r; }
+
+// UniPoly::from_evals (unipoly.rs:15-45) as the sum-check rounds use it: n = 3
+// (quad) or 4 (cubic) evaluations at 0..n-1 -> coefficients, constant first
+extern "C" int tpst_unipoly_from_evals(const uint64_t* evals, int n, uint64_t* coeffs) {
+  if (!evals || !coeffs || (n != 3 && n != 4)) return TPST_E_ARG;
+  Fr e[4], cs[4];
+  for (int i = 0; i < n; i++) {
+    if (!fr_ok_host(evals + 4 * i)) return TPST_E_ARG;
+    e[i] = frc(evals + 4 * i);
+  }
+  from_evals(e, n, cs);
+  for (int i = 0; i < n; i++) fro(cs[i], coeffs + 4 * i);
+  return TPST_OK;
+}
+
+// EqPolynomial::evals (dense_mlpoly.rs:231-250) on the device: the MSB-first
+// chi table of r (ell <= 30), the kernel the phase-one tau table uses
+extern "C" int tpst_eq_evals(tpst_ctx* ctx, const uint64_t* r, int ell, uint64_t* out) {
+  if (!ctx || !r || !out || ell < 0 || ell > 30) return fail(ctx, TPST_E_ARG, "eq_evals: bad argument");
+  std::vector<Fr> rm(ell ? ell : 1);
+  for (int j = 0; j < ell; j++) {
+    if (!fr_ok_host(r + 4 * j)) return fail(ctx, TPST_E_ARG, "eq_evals: r_j >= r");
+    rm[j] = frc(r + 4 * j);
+  }
+  const size_t n = (size_t)1 << ell;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  Buf dr, dt;
+  TPST_HIP(ctx, dr.alloc(rm.size() * 32));
+  TPST_HIP(ctx, dt.alloc(n * 32));
+  TPST_HIP(ctx, hipMemcpyAsync(dr.p, rm.data(), rm.size() * 32, hipMemcpyHostToDevice, s));
+  k_eq_evals<<<grid_for(n, 256), 256, 0, s>>>(dr.u(), ell, n, dt.u());
+  TPST_HIP(ctx, hipGetLastError());
+  std::vector<Fr> h(n);
+  TPST_HIP(ctx, hipMemcpyAsync(h.data(), dt.p, n * 32, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipStreamSynchronize(s));
+  for (size_t i = 0; i < n; i++) fro(h[i], out + 4 * i);
+  return TPST_OK;
+}
 
 // one sum-check (K = 4 cubic with additive term, K = 2 quad) over device
 // tables of length 2^rounds; transcript on the host between rounds
@@ -520,6 +562,7 @@ static void fr_copy_out(const Fr& a, uint64_t* o) { fro(a, o); }
 extern "C" int tpst_r1cs_prove(tpst_ctx* ctx, tpst_r1cs* R, const uint64_t* vars, const uint64_t* inputs,
                                tpst_transcript* tr, tpst_r1cs_proof* out) {
   if (!ctx || !R || !vars || (R->num_inputs && !inputs) || !tr || !out) return fail(ctx, TPST_E_ARG, "null argument");
+  if (R->owner != ctx) return fail(ctx, TPST_E_ARG, "instance belongs to another context");
   memset(out, 0, sizeof(*out));
   const int nvar_bits = log2_exact(R->num_vars);
   const int rx_n = log2_exact(R->num_cons), ry_n = nvar_bits + 1;
@@ -636,6 +679,7 @@ extern "C" int tpst_r1cs_prove(tpst_ctx* ctx, tpst_r1cs* R, const uint64_t* vars
 extern "C" int tpst_r1cs_commit(tpst_ctx* ctx, tpst_r1cs* R, const uint8_t* label, size_t label_len,
                                 uint64_t* comm_ops, size_t* ops_rows, uint64_t* comm_mem, size_t* mem_rows) {
   if (!ctx || !R || !ops_rows || !mem_rows || (label_len && !label)) return fail(ctx, TPST_E_ARG, "null argument");
+  if (R->owner != ctx) return fail(ctx, TPST_E_ARG, "instance belongs to another context");
   size_t maxnz = 1;
   for (int m = 0; m < 3; m++) maxnz = R->nnz[m] > maxnz ? R->nnz[m] : maxnz;
   size_t N = 1;

@@ -5,6 +5,7 @@
 
 #include <cstring>
 
+#include "../../include/tpst.h"
 #include "field.h"
 
 namespace tpst {
@@ -51,6 +52,7 @@ inline int log2_exact(size_t n) {
 
 // ================================================================ state ==
 struct tpst_r1cs {
+  const tpst_ctx* owner = nullptr;  // the context whose device holds the tables
   size_t num_cons = 0, num_vars = 0, num_inputs = 0, ncols = 0;
   size_t nnz[3] = {0, 0, 0};
   tpst::Buf rptr[3], ridx[3], rval[3];  // CSR over rows (multiply_vec)

@@ -404,8 +404,9 @@ extern "C" int tpst_de_open_proof(const uint8_t* pst, size_t pst_len, const uint
 // CommitterKey { nv: usize, powers_of_g: Vec<Vec<G1>>, powers_of_h: Vec<Vec<G2>>,
 // g: G1, h: G2 } (ark-poly-commit multilinear_pc data_structures, after trim)
 // from the flat SRS layout of tpst_srs_export
-extern "C" int tpst_ser_committer_key(int nv, const uint64_t* flat, uint8_t* out, size_t cap, size_t* len) {
-  if (!flat || nv < 1 || nv > TPST_MAX_VARS) return TPST_E_ARG;
+extern "C" int tpst_ser_committer_key(int nv, const uint64_t* flat, size_t flat_len, uint8_t* out, size_t cap,
+                                      size_t* len) {
+  if (!flat || nv < 1 || nv > TPST_MAX_VARS || flat_len != tpst_srs_flat_len(nv)) return TPST_E_ARG;
   const uint64_t* g = flat;
   const uint64_t* h = flat + 12;
   std::vector<const uint64_t*> pg(nv), ph(nv);

@@ -104,30 +104,23 @@ def prove(pk: ProvingKey, inst: R1CSInstance, vars_, inputs, r, s) -> Proof:
     return Proof(a, b, c)
 
 
-def _g1_neg(p: np.ndarray) -> np.ndarray:
-    p = np.asarray(p, dtype=np.uint64)
-    y = sum(int(p[6 + i]) << (64 * i) for i in range(6))
-    if y == 0 and not p[:6].any():
-        return p.copy()
-    ny = _P - y
-    out = p.copy()
-    out[6:] = [(ny >> (64 * i)) & (2 ** 64 - 1) for i in range(6)]
-    return out
-
-
 def verify(ctx, vk: VerifyingKey, inputs, proof: Proof) -> bool:
     """Groth16::verify_proof: e(A, B) == e(alpha, beta) e(IC, gamma) e(C, delta)
-    with IC = gamma_abc[0] + sum inputs_i gamma_abc[i + 1]; one device
-    multi-pairing of (A, B), (-alpha, beta), (-IC, gamma), (-C, delta)."""
-    inputs = np.asarray(inputs, dtype=np.uint64).reshape(-1, 4)
-    if len(inputs) + 1 != len(vk.gamma_abc_g1):
+    with IC = gamma_abc[0] + sum inputs_i gamma_abc[i + 1] (tpst_groth16_verify:
+    a device MSM and one device multi-pairing).  Every proof and key element
+    is validated first (canonical, on the curve, in the subgroup; inputs < r),
+    as arkworks' Validate::Yes deserialisation would: a malformed element is
+    an invalid proof (False)."""
+    inputs = np.ascontiguousarray(inputs, dtype=np.uint64).reshape(-1, 4)
+    abc = np.ascontiguousarray(vk.gamma_abc_g1, dtype=np.uint64).reshape(-1, 12)
+    if len(inputs) + 1 != len(abc):
         raise ValueError("wrong number of public inputs")
-    one = np.zeros((1, 4), dtype=np.uint64)
-    one[0, 0] = 1
-    ic = ctx.g1_msm(vk.gamma_abc_g1, np.concatenate([one, inputs]))
-    g1 = np.stack([proof.a, _g1_neg(vk.alpha_g1), _g1_neg(ic), _g1_neg(proof.c)])
-    g2 = np.stack([proof.b, vk.beta_g2, vk.gamma_g2, vk.delta_g2])
-    gt = ctx.multi_pairing(g1, g2)
-    want = np.zeros(72, dtype=np.uint64)
-    want[0] = 1
-    return bool(np.array_equal(gt, want))
+    u = lambda a, n: np.ascontiguousarray(a, dtype=np.uint64).reshape(n)  # noqa: E731
+    rc = ctx.lib.tpst_groth16_verify(ctx.h, ptr(u(vk.alpha_g1, 12)), ptr(u(vk.beta_g2, 24)), ptr(u(vk.gamma_g2, 24)),
+                                     ptr(u(vk.delta_g2, 24)), ptr(abc), len(abc),
+                                     ptr(inputs if len(inputs) else np.zeros((1, 4), dtype=np.uint64)), len(inputs),
+                                     ptr(u(proof.a, 12)), ptr(u(proof.b, 24)), ptr(u(proof.c, 12)))
+    if rc == -5:
+        return False
+    ctx.check(rc, "Groth16::verify")
+    return True

@@ -40,6 +40,33 @@ def transcript_new_from_state2(tr: PoseidonTranscript, fr) -> None:
         raise ValueError("scalar >= r")
 
 
+class UniPoly:
+    """UniPoly::from_evals (unipoly.rs:15-45): the round-polynomial encoding of
+    the sum-checks (host C-ABI, the same routine the device rounds use)."""
+
+    @staticmethod
+    def from_evals(evals) -> np.ndarray:
+        e = _fr(evals)
+        out = np.zeros_like(e)
+        if _lib.load().tpst_unipoly_from_evals(ptr(e), len(e), ptr(out)) != 0:
+            raise ValueError("UniPoly::from_evals takes 3 or 4 evaluations < r")
+        return out
+
+
+class EqPolynomial:
+    """EqPolynomial (dense_mlpoly.rs:221-250): ``evals`` is the MSB-first chi
+    table of r, computed by the device kernel the phase-one sum-check uses."""
+
+    def __init__(self, r):
+        self.r = _fr(r)
+
+    def evals(self, ctx: Context) -> np.ndarray:
+        ell = len(self.r)
+        out = np.zeros((1 << ell, 4), dtype=np.uint64)
+        ctx.check(ctx.lib.tpst_eq_evals(ctx.h, ptr(self.r), ell, ptr(out)), "EqPolynomial::evals")
+        return out
+
+
 class R1CSInstance:
     """Device-resident R1CS instance (A, B, C as CSR + CSC)."""
 

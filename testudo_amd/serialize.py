@@ -104,4 +104,4 @@ def ser_committer_key(nv: int, srs_flat) -> bytes:
     """CommitterKey { nv, powers_of_g, powers_of_h, g, h } of the flat SRS
     (tpst_srs_export layout) -- benches/pst.rs:43-46."""
     flat = np.ascontiguousarray(srs_flat, dtype=np.uint64)
-    return _write(_lib_().tpst_ser_committer_key, nv, _u64p(flat))
+    return _write(_lib_().tpst_ser_committer_key, nv, _u64p(flat), len(flat))

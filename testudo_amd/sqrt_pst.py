@@ -41,6 +41,12 @@ class PoseidonTranscript:
     def append_gt(self, f):
         self.lib.tpst_transcript_append_gt(C.byref(self.t), ptr(_u64(f, (72,))))
 
+    def append_bytes(self, b: bytes):
+        """append_bytes (poseidon_transcript.rs:67-69); ``append`` of a value
+        is this over its Compress::No serialisation."""
+        b = bytes(b)
+        self.lib.tpst_transcript_append_bytes(C.byref(self.t), b, len(b))
+
     def challenge_scalar(self) -> np.ndarray:
         out = np.zeros(4, dtype=np.uint64)
         self.lib.tpst_transcript_challenge(C.byref(self.t), ptr(out))
@@ -85,6 +91,15 @@ def fr_stream(seed: int, n: int, start: int = 0):
     return out, nxt
 
 
+def _nv(evals) -> int:
+    """log2 of the evaluation count; a non-power-of-two vector is an error
+    (the reference's MultilinearExtension always has 2^nv evaluations)."""
+    nv = len(evals).bit_length() - 1
+    if len(evals) == 0 or 1 << nv != len(evals):
+        raise TpstError("evaluation count must be a power of two")
+    return nv
+
+
 class MultilinearPC:
     """The ark-poly-commit fork's MultilinearPC<Bls12_377> calls the reference
     makes, against the SRS loaded in ``ctx``.  Points are
@@ -94,7 +109,7 @@ class MultilinearPC:
     def commit(ctx: Context, evals) -> np.ndarray:
         """sqrt_pst.rs:124 -> g_product (12,)."""
         evals = _u64(evals).reshape(-1, 4)
-        nv = len(evals).bit_length() - 1
+        nv = _nv(evals)
         out = np.zeros(12, dtype=np.uint64)
         ctx.check(ctx.lib.tpst_mlpc_commit(ctx.h, ptr(evals), nv, ptr(out)), "MultilinearPC::commit")
         return out
@@ -103,7 +118,7 @@ class MultilinearPC:
     def commit_g2(ctx: Context, evals) -> np.ndarray:
         """mipp.rs:133 -> h_product (24,)."""
         evals = _u64(evals).reshape(-1, 4)
-        nv = len(evals).bit_length() - 1
+        nv = _nv(evals)
         out = np.zeros(24, dtype=np.uint64)
         ctx.check(ctx.lib.tpst_mlpc_commit_g2(ctx.h, ptr(evals), nv, ptr(out)), "MultilinearPC::commit_g2")
         return out
@@ -112,7 +127,7 @@ class MultilinearPC:
     def open(ctx: Context, evals, point) -> np.ndarray:
         """sqrt_pst.rs:225 -> Proof (nv, 24) G2."""
         evals = _u64(evals).reshape(-1, 4)
-        nv = len(evals).bit_length() - 1
+        nv = _nv(evals)
         point = _u64(point, (nv, 4))
         out = np.zeros((nv, 24), dtype=np.uint64)
         ctx.check(ctx.lib.tpst_mlpc_open(ctx.h, ptr(evals), nv, ptr(point), ptr(out)), "MultilinearPC::open")
@@ -122,7 +137,7 @@ class MultilinearPC:
     def open_g1(ctx: Context, evals, point) -> np.ndarray:
         """mipp.rs:144 -> ProofG1 (nv, 12)."""
         evals = _u64(evals).reshape(-1, 4)
-        nv = len(evals).bit_length() - 1
+        nv = _nv(evals)
         point = _u64(point, (nv, 4))
         out = np.zeros((nv, 12), dtype=np.uint64)
         ctx.check(ctx.lib.tpst_mlpc_open_g1(ctx.h, ptr(evals), nv, ptr(point), ptr(out)), "MultilinearPC::open_g1")
