@@ -457,12 +457,15 @@ def _wire_sizes(ctx, nv, pst_proof, mipp):
 def sharded_leg(ctx, log_n, dist, dev):
     """sqrt-PST commit + open at 2^log_n variables (BASELINE configs[3]).
     N > 1: every rank uploads only its column block of Z and commits its rows
-    AND their share of the IPP's Miller loops (one RCCL all-gather of [row
-    commitments | Miller partial], one final exponentiation on rank 0); the
-    open (transcript-sequential MIPP + PST open) runs on rank
-    0, which also holds the whole Z for it.  N = 1: the plain commit + open."""
+    AND their share of the IPP's Miller loops (one all-gather of [row
+    commitments | Miller partial] device buffers, one final exponentiation on
+    rank 0, read from the gathered buffer); then each rank computes its rows'
+    share of get_q's z_q and of c_u (one all-gather, summed on rank 0 -- the
+    q / eval step that benches/pst.rs runs before the open timer), and rank 0
+    opens from q alone (transcript-sequential MIPP + PST open, SURVEY.md
+    §8(e)).  No rank holds the whole Z.  N = 1: the plain commit + open."""
     from testudo_amd import sqrt_pst as S
-    from testudo_amd.distributed import shard_rows, sharded_commit
+    from testudo_amd.distributed import shard_rows, sharded_commit, sharded_open_inputs
     nv = (log_n + 1) // 2
     t = time.perf_counter()
     S.srs_setup(ctx, nv, SEED + 1)
@@ -472,36 +475,43 @@ def sharded_leg(ctx, log_n, dist, dev):
     rank = dist.get_rank() if dist else 0
     world = dist.get_world_size() if dist else 1
     r0, r1 = shard_rows(1 << (log_n // 2), world, rank)
-    pl = None
-    h2d_full_s = None
-    if rank == 0:  # rank 0 opens, so it holds the whole polynomial
-        t = time.perf_counter()
-        pl = S.Polynomial.from_evaluations(ctx, Z)
-        h2d_full_s = time.perf_counter() - t
-    shard = pl
-    h2d_s = h2d_full_s
-    if dist and rank != 0:  # the rank-local column block only
-        t = time.perf_counter()
+    t = time.perf_counter()
+    if dist:  # the rank-local column block only
         shard = S.Polynomial.from_evaluations_cols(ctx, Z, r0, r1)
-        h2d_s = time.perf_counter() - t
-    if rank == 0:
-        v = pl.eval(pt)
+    else:
+        shard = S.Polynomial.from_evaluations(ctx, Z)
+    h2d_s = time.perf_counter() - t
+    del Z
     reps = 2
-    commits, opens = [], []
+    commits, qs, opens = [], [], []
     for _ in range(reps + 1):
         if dist:
             dist.barrier()
         ctx.synchronize()
         t = time.perf_counter()
         if dist:
-            comms, T = sharded_commit(log_n, shard.commit_rows_partial, lambda m: S.gt_final_exp_product(ctx, m),
-                                      dist, dev)
+            comms, T, own = sharded_commit(log_n, shard.commit_rows_partial_into,
+                                           lambda got: S.gt_final_exp_product_gathered(ctx, got, r1 - r0), dist, dev)
         else:
-            comms, T = pl.commit()
+            comms, T = shard.commit()
         ctx.synchronize()
         if dist:
             dist.barrier()
         commits.append(_max_over_ranks(dist, dev, time.perf_counter() - t))
+        # q (and c_u) before the open timer, as eval does in benches/pst.rs:48-62
+        t = time.perf_counter()
+        if dist:
+            zq, U = sharded_open_inputs(log_n, lambda a, b, out: shard.get_q_partial_into(pt, a, b, out),
+                                        lambda a, b: S.cu_partial(ctx, log_n, pt, a, b, own),
+                                        lambda got: S.fr_sum(ctx, got), lambda sh: S.g1_sum(ctx, sh), dist, dev)
+            pl = S.Polynomial.from_q(ctx, log_n, pt, zq, U) if rank == 0 else None
+        else:
+            pl = shard
+        v = pl.eval(pt) if rank == 0 else None
+        ctx.synchronize()
+        if dist:
+            dist.barrier()
+        qs.append(_max_over_ranks(dist, dev, time.perf_counter() - t))
         if rank == 0:
             t = time.perf_counter()
             U, pst_proof, mipp = pl.open(S.PoseidonTranscript(), comms, pt, T)
@@ -516,12 +526,13 @@ def sharded_leg(ctx, log_n, dist, dev):
     return {"log_n": log_n, "commit_s": round(c, 4), "open_s": round(o, 4), "commit_plus_open_s": round(c + o, 4),
             **_wire_sizes(ctx, nv, pst_proof, mipp),
             "first_call": {"commit_s": round(commits[0], 4), "open_s": round(opens[0], 4)},
+            "q_eval_s": round(min(qs[1:]), 4),
             "ranks": world, "rows_per_rank": r1 - r0, "verified": ok,
-            "h2d_s_rank0_full": round(h2d_full_s, 4), "h2d_s_rank0_shard": round(h2d_s, 4),
-            "srs_setup_s": round(setup_s, 3),
+            "h2d_s_rank0": round(h2d_s, 4), "srs_setup_s": round(setup_s, 3),
             "exchange": ("per-rank column-block upload; %s all_gather of [96-B row commitments | 576-B Miller "
-                         "partial] per rank; final exponentiation + open on rank 0"
-                         % ("RCCL" if dist.get_backend() == "nccl" else "gloo")) if dist else "none"}
+                         "partial] device buffers, FE on rank 0; %s all_gather of [z_q share | c_u share], mod-r / "
+                         "G1 sum on rank 0, open from q on rank 0"
+                         % ((("RCCL" if dist.get_backend() == "nccl" else "gloo"),) * 2)) if dist else "none"}
 
 
 def cpu_leg(ctx, bk, sc, gpu_out, result):

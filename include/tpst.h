@@ -198,6 +198,29 @@ int tpst_poly_ipp(tpst_ctx* ctx, int n, const uint64_t* comms, uint64_t* T);
 int tpst_poly_commit_rows_partial(tpst_ctx* ctx, tpst_poly* p, size_t r0, size_t r1, uint64_t* comms,
                                   uint64_t* miller);
 int tpst_gt_final_exp_product(tpst_ctx* ctx, const uint64_t* partials, size_t k, uint64_t* T);
+/* Device-resident variants for the RCCL path (no host round trip): the share
+ * [comms (R x 12) | Miller partial (72)] written into a device buffer of
+ * R * 96 + 576 bytes; k partials read from device memory `stride_bytes` apart
+ * (an all-gather of those buffers). */
+int tpst_poly_commit_rows_partial_dev(tpst_ctx* ctx, tpst_poly* p, size_t r0, size_t r1, void* d_out);
+int tpst_gt_final_exp_product_dev(tpst_ctx* ctx, const void* d_partials, size_t stride_bytes, size_t k, uint64_t* T);
+
+/* Row-sharded opening (sqrt_pst.rs:81-101, 198).  Rank g
+ * (rows [r0, r1) resident, e.g. a from_evaluations_cols handle) computes its
+ * share of get_q, zq_g[j] = sum_{r0 <= i < r1} Z_i[j] chi_i(b) (2^m_row
+ * canonical Fr), and of c_u = sum_{r0 <= i < r1} chi_i(b) C_i (canonical
+ * affine, from its own row commitments).  The shares are summed on rank 0
+ * (tpst_fr_sum_dev: k device vectors of n canonical Fr, mod r; c_u: a G1 sum),
+ * which opens from an opening-only handle: tpst_poly_from_q_dev (q on the
+ * device, chi(b) from the point, c_u optional -- NULL computes it) serves
+ * tpst_poly_eval and tpst_poly_open without the evaluations. */
+int tpst_poly_get_q_partial(tpst_ctx* ctx, tpst_poly* p, const uint64_t* point, size_t r0, size_t r1, uint64_t* zq);
+int tpst_poly_get_q_partial_dev(tpst_ctx* ctx, tpst_poly* p, const uint64_t* point, size_t r0, size_t r1, void* d_zq);
+int tpst_fr_sum_dev(tpst_ctx* ctx, const void* d_parts, size_t k, size_t n, void* d_out);
+int tpst_poly_cu_partial(tpst_ctx* ctx, int n, const uint64_t* point, size_t r0, size_t r1, const uint64_t* comms,
+                         uint64_t* out);
+int tpst_poly_from_q_dev(tpst_ctx* ctx, int n, const uint64_t* point, const void* d_zq, const uint64_t* U,
+                         tpst_poly** out);
 /* Polynomial::open (sqrt_pst.rs:168-230); the transcript is updated in place.
  * U = MSM(comms, chi(b)) over the caller's comm_list (sqrt_pst.rs:198). */
 int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, const uint64_t* comms,

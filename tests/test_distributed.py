@@ -4,7 +4,8 @@
   C++ oracle standing in for the per-rank GPU compute (row MSMs + unreduced
   Miller-loop partial per rank, one final exponentiation on rank 0) -- the
   gathered commitment list and T must equal the single-process commit bit for
-  bit;
+  bit -- and the sharded opening inputs (C3: per-rank shares of get_q's z_q and
+  of c_u, summed on rank 0) against the single-process q and U;
 * bench.py's timing aggregation (barrier + max over ranks).
 """
 import os
@@ -31,12 +32,15 @@ def _worker(rank, world, port, n, q):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle", "cpu"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle", "py"))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import orc
-        from testudo_amd.distributed import sharded_commit
+        import pst as PY
+        from testudo_amd.distributed import sharded_commit, sharded_open_inputs
+        R_ = PY.R
         nv = (n + 1) // 2
         srs = orc.SRS(nv, 0x7E57D1)
         flat = srs.export()
@@ -52,16 +56,56 @@ def _worker(rank, world, port, n, q):
         odd = n % 2
         hstart = levels[odd][1]
         hvec = flat[hstart:hstart + C * 24].reshape(C, 24)
-        Z, _ = orc.fr_stream(0x7E57D0, 1 << n)
+        Z, k = orc.fr_stream(0x7E57D0, 1 << n)
+        pt, _ = orc.fr_stream(0x7E57D0, n, k)
 
-        def commit_rows_partial(r0, r1):
+        def commit_rows_partial_into(r0, r1, out):
             cm = orc.g1_msm_batch(pg0, Z[r0:].reshape(-1), r1 - r0, 1, C)
-            return cm, orc.miller_product(cm, hvec[r0:r1])
+            ml = orc.miller_product(cm, hvec[r0:r1])
+            out.copy_(torch.from_numpy(np.concatenate([cm.reshape(-1), ml]).view(np.int64)))
 
-        comms, T = sharded_commit(n, commit_rows_partial, orc.gt_final_exp_product, dist, torch.device("cpu"))
+        def finalize(got):
+            Rr = C // world
+            return orc.gt_final_exp_product(got[:, 12 * Rr:].numpy().view(np.uint64))
+
+        comms, T, own = sharded_commit(n, commit_rows_partial_into, finalize, dist, torch.device("cpu"))
+        # C3: shares of z_q and c_u (oracle/py restatement of the per-rank work)
+        Zi = [int(v) for v in (Z[:, 0].astype(object) + (Z[:, 1].astype(object) << 64) +
+                               (Z[:, 2].astype(object) << 128) + (Z[:, 3].astype(object) << 192))]
+        pti = [int(a) + (int(b) << 64) + (int(c) << 128) + (int(d) << 192) for a, b, c, d in pt]
+        m_col, m_row = n // 2, n - n // 2
+        chis = [PY.get_chi_i(pti[m_row:], i) for i in range(C)]
+
+        def fr_np(vals):
+            return np.array([[(v >> (64 * t)) & (2 ** 64 - 1) for t in range(4)] for v in vals], dtype=np.uint64)
+
+        def q_partial_into(r0, r1, out):
+            share = [sum(Zi[(j << m_col) | i] * chis[i] for i in range(r0, r1)) % R_ for j in range(1 << m_row)]
+            out.copy_(torch.from_numpy(fr_np(share).reshape(-1).view(np.int64)))
+
+        def cu_partial(r0, r1):
+            return orc.g1_msm(own, fr_np(chis[r0:r1]))
+
+        def combine_q(got):
+            a = got.numpy().view(np.uint64).reshape(world, -1, 4)
+            tot = [sum(int(a[w, j, 0]) + (int(a[w, j, 1]) << 64) + (int(a[w, j, 2]) << 128) + (int(a[w, j, 3]) << 192)
+                       for w in range(world)) % R_ for j in range(a.shape[1])]
+            return torch.from_numpy(fr_np(tot).reshape(-1).view(np.int64))
+
+        def combine_cu(shares):
+            ones = np.zeros((len(shares), 4), dtype=np.uint64)
+            ones[:, 0] = 1
+            return orc.g1_msm(shares, ones)
+
+        zq, U = sharded_open_inputs(n, q_partial_into, cu_partial, combine_q, combine_cu, dist, torch.device("cpu"))
         if rank == 0:
             c2, T2 = orc.pst_commit(srs, Z, n)
-            q.put((bool(np.array_equal(comms, c2)), bool(np.array_equal(T, T2))))
+            ref = PY.Polynomial(Zi)
+            ref.get_q(pti)
+            pr = orc.pst_open(srs, Z, n, pt, c2)
+            q.put((bool(np.array_equal(comms, c2)), bool(np.array_equal(T, T2)),
+                   bool(np.array_equal(zq.numpy().view(np.uint64).reshape(-1, 4), fr_np(ref.q))),
+                   bool(np.array_equal(U, pr["U"]))))
         else:
             q.put(None)
     finally:
@@ -81,7 +125,7 @@ def test_sharded_commit_gloo_world2(n):
         p.join(timeout=60)
         assert p.exitcode == 0
     res = [r for r in res if r is not None]
-    assert res == [(True, True)]
+    assert res == [(True, True, True, True)]  # comm_list, T, combined z_q, combined c_u
 
 
 def _timing_worker(rank, world, port, q):

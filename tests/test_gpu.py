@@ -360,3 +360,53 @@ def test_column_slice_upload_matches_full_commit(ctx, n, world):
         with pytest.raises(TpstError):
             sl.eval(np.zeros((n, 4), dtype=np.uint64))
     assert np.array_equal(S.gt_final_exp_product(ctx, np.stack(parts)), T)
+
+
+@pytest.mark.parametrize("n,world", [(11, 4), (12, 2)])
+def test_sharded_opening_matches_single_process(ctx, n, world):
+    """Row-sharded opening: every rank's column-slice
+    handle computes its rows' share of get_q's z_q and of c_u; the mod-r sum
+    (tpst_fr_sum_dev) and the G1 sum give q and U; the opening-only handle
+    (tpst_poly_from_q_dev) evaluates and opens to the same bytes as the
+    whole-polynomial handle, and the proof verifies.  The device-buffer
+    variants of the commit share and of the final exponentiation agree with
+    the host ones."""
+    import torch
+    from testudo_amd import sqrt_pst as S
+    nv = (n + 1) // 2
+    S.srs_setup(ctx, nv, 0x7E57D1)
+    Z, k = S.fr_stream(0x7E57D0 + 5 * n, 1 << n)
+    pt, _ = S.fr_stream(0x7E57D0 + 5 * n, n, k)
+    full = S.Polynomial.from_evaluations(ctx, Z)
+    comms, T = full.commit()
+    v = full.eval(pt)
+    U, pst_proof, mipp = full.open(S.PoseidonTranscript(), comms, pt, T)
+    C = 1 << (n // 2)
+    N = 1 << (n - n // 2)
+    R = C // world
+    dev = torch.device("cuda", 0)
+    zq_parts = torch.empty((world, N * 4), dtype=torch.int64, device=dev)
+    cm_parts = torch.empty((world, R * 12 + 72), dtype=torch.int64, device=dev)
+    cu = []
+    for g in range(world):
+        sl = S.Polynomial.from_evaluations_cols(ctx, Z, g * R, (g + 1) * R)
+        sl.get_q_partial_into(pt, g * R, (g + 1) * R, zq_parts[g])
+        host = sl.get_q_partial(pt, g * R, (g + 1) * R)
+        assert np.array_equal(zq_parts[g].cpu().numpy().view(np.uint64).reshape(-1, 4), host)
+        sl.commit_rows_partial_into(g * R, (g + 1) * R, cm_parts[g])
+        c, ml = sl.commit_rows_partial(g * R, (g + 1) * R)
+        got = cm_parts[g].cpu().numpy().view(np.uint64)
+        assert np.array_equal(got[:12 * R].reshape(R, 12), c) and np.array_equal(got[12 * R:], ml)
+        cu.append(S.cu_partial(ctx, n, pt, g * R, (g + 1) * R, c))
+    assert np.array_equal(S.gt_final_exp_product_gathered(ctx, cm_parts, R), T)
+    zq = S.fr_sum(ctx, zq_parts)
+    Uc = S.g1_sum(ctx, np.stack(cu))
+    assert np.array_equal(Uc, U)
+    for Ugiven in (Uc, None):
+        pq = S.Polynomial.from_q(ctx, n, pt, zq, Ugiven)
+        assert np.array_equal(pq.eval(pt), v)
+        U2, pst2, mipp2 = pq.open(S.PoseidonTranscript(), comms, pt, T)
+        assert np.array_equal(U2, U) and np.array_equal(pst2, pst_proof)
+        for f in ("comms_t", "comms_u", "final_a", "final_h", "pst_proof_h"):
+            assert np.array_equal(getattr(mipp2, f), getattr(mipp, f)), f
+    assert S.verify(ctx, S.PoseidonTranscript(), U, pt, v, pst_proof, mipp, T)

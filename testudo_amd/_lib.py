@@ -65,6 +65,13 @@ PROTOTYPES = [
     ("tpst_poly_ipp", C.c_int, [_vp, C.c_int, _u64p, _u64p]),
     ("tpst_poly_commit_rows_partial", C.c_int, [_vp, _vp, _sz, _sz, _u64p, _u64p]),
     ("tpst_gt_final_exp_product", C.c_int, [_vp, _u64p, _sz, _u64p]),
+    ("tpst_poly_commit_rows_partial_dev", C.c_int, [_vp, _vp, _sz, _sz, _vp]),
+    ("tpst_gt_final_exp_product_dev", C.c_int, [_vp, _vp, _sz, _sz, _u64p]),
+    ("tpst_poly_get_q_partial", C.c_int, [_vp, _vp, _u64p, _sz, _sz, _u64p]),
+    ("tpst_poly_get_q_partial_dev", C.c_int, [_vp, _vp, _u64p, _sz, _sz, _vp]),
+    ("tpst_fr_sum_dev", C.c_int, [_vp, _vp, _sz, _sz, _vp]),
+    ("tpst_poly_cu_partial", C.c_int, [_vp, C.c_int, _u64p, _sz, _sz, _u64p, _u64p]),
+    ("tpst_poly_from_q_dev", C.c_int, [_vp, C.c_int, _u64p, _vp, _u64p, C.POINTER(_vp)]),
     ("tpst_poly_open", C.c_int, [_vp, _vp, _vp, _u64p, _u64p, _u64p, _vp]),
     ("tpst_pst_verify", C.c_int, [_vp, _vp, C.c_int, _u64p, _u64p, _u64p, _vp]),
     ("tpst_mlpc_commit", C.c_int, [_vp, _u64p, C.c_int, _u64p]),

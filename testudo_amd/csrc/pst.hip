@@ -42,16 +42,18 @@ hipError_t chi_table(hipStream_t s, const uint32_t* d_b, int m, uint32_t* d_out)
   return hipGetLastError();
 }
 
-// one workgroup per output j: the row Z[j*C .. j*C+C) is contiguous, read coalesced
+// one workgroup per output j: q[j] = sum_{i < nr} Z[j cs + i] chis[i], the run
+// Z[j cs .. j cs + nr) contiguous and read coalesced (the whole polynomial:
+// cs = nr = 2^m_col; a row shard: the shard's block, nr of its rows)
 template <int BS>
-__global__ void __launch_bounds__(BS) k_get_q(const uint32_t* __restrict__ Z, int m_col, const uint32_t* __restrict__ chis,
-                                              uint32_t* __restrict__ q) {
+__global__ void __launch_bounds__(BS) k_get_q(const uint32_t* __restrict__ Z, size_t cs, size_t nr,
+                                              const uint32_t* __restrict__ chis, uint32_t* __restrict__ q,
+                                              int canonical_out) {
   __shared__ Fr sh[BS];
   const size_t j = blockIdx.x;
-  const size_t C = (size_t)1 << m_col;
   Fr acc = Fr::zero();
-  for (size_t i = threadIdx.x; i < C; i += BS) {
-    const Fr z = to_mont(load_f<Fr>(Z + 8 * ((j << m_col) | i)));
+  for (size_t i = threadIdx.x; i < nr; i += BS) {
+    const Fr z = to_mont(load_f<Fr>(Z + 8 * (j * cs + i)));
     acc = add(acc, mul(z, load_f<Fr>(chis + 8 * i)));
   }
   sh[threadIdx.x] = acc;
@@ -60,11 +62,33 @@ __global__ void __launch_bounds__(BS) k_get_q(const uint32_t* __restrict__ Z, in
     if ((int)threadIdx.x < h) sh[threadIdx.x] = add(sh[threadIdx.x], sh[threadIdx.x + h]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) store_f<Fr>(q + 8 * j, sh[0]);
+  if (threadIdx.x == 0) store_f<Fr>(q + 8 * j, canonical_out ? from_mont(sh[0]) : sh[0]);
 }
 
 hipError_t get_q(hipStream_t s, const uint32_t* d_Z, int m_col, int m_row, const uint32_t* d_chis, uint32_t* d_q) {
-  k_get_q<256><<<(unsigned)((size_t)1 << m_row), 256, 0, s>>>(d_Z, m_col, d_chis, d_q);
+  const size_t C = (size_t)1 << m_col;
+  k_get_q<256><<<(unsigned)((size_t)1 << m_row), 256, 0, s>>>(d_Z, C, C, d_chis, d_q, 0);
+  return hipGetLastError();
+}
+
+hipError_t get_q_rows(hipStream_t s, const uint32_t* d_Z, size_t cs, size_t nr, int m_row, const uint32_t* d_chis,
+                      uint32_t* d_q_canonical) {
+  k_get_q<256><<<(unsigned)((size_t)1 << m_row), 256, 0, s>>>(d_Z, cs, nr, d_chis, d_q_canonical, 1);
+  return hipGetLastError();
+}
+
+// out[j] = sum_t parts[t n + j] (mod r), canonical in and out
+__global__ void k_fr_sum_parts(const uint32_t* __restrict__ parts, size_t k, size_t n, uint32_t* __restrict__ out) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  Fr acc = Fr::zero();
+  for (size_t t = 0; t < k; t++) acc = add(acc, load_f<Fr>(parts + 8 * (t * n + j)));
+  store_f<Fr>(out + 8 * j, acc);
+}
+
+hipError_t fr_sum_parts(hipStream_t s, const uint32_t* d_parts, size_t k, size_t n, uint32_t* d_out) {
+  if (!n) return hipSuccess;
+  k_fr_sum_parts<<<grid_for(n, 256), 256, 0, s>>>(d_parts, k, n, d_out);
   return hipGetLastError();
 }
 

@@ -389,6 +389,11 @@ struct tpst_poly {
   size_t col0 = 0, ncols = 0;
   DevBuf q, chis;                 // Montgomery
   bool has_q = false;
+  // opening-only handle (row-sharded commit): q combined from
+  // the ranks' shares, no evaluations resident; optionally c_u combined too
+  bool q_only = false;
+  bool has_u = false;
+  uint64_t U[12] = {};
 };
 
 static int srs_fbt(tpst_ctx* ctx, SrsState* st, int odd);
@@ -744,8 +749,15 @@ static int poly_rows_view(tpst_ctx* ctx, const tpst_poly* p, size_t r0, size_t r
 }
 
 static int poly_need_full(tpst_ctx* ctx, const tpst_poly* p) {
+  if (p->q_only) return fail(ctx, TPST_E_STATE, "operation needs the evaluations (this handle holds q only)");
   return p->ncols ? fail(ctx, TPST_E_STATE, "operation needs the whole polynomial (this handle holds a column slice)")
                   : TPST_OK;
+}
+
+// eval / open need q and chi(b): a whole polynomial computes them, an
+// opening-only handle carries them
+static int poly_need_q_source(tpst_ctx* ctx, const tpst_poly* p) {
+  return p->q_only ? TPST_OK : poly_need_full(ctx, p);
 }
 
 extern "C" int tpst_poly_from_evaluations_dev(tpst_ctx* ctx, const void* d_Z, int n, tpst_poly** out) {
@@ -782,7 +794,7 @@ static int poly_get_q(tpst_ctx* ctx, tpst_poly* p, const uint64_t* point) {
 extern "C" int tpst_poly_eval(tpst_ctx* ctx, tpst_poly* p, const uint64_t* point, uint64_t* out_v) {
   if (!ctx || !p || !point || !out_v) return fail(ctx, TPST_E_ARG, "null argument");
   std::lock_guard<std::mutex> lk(ctx->mu);
-  if (int rc = poly_need_full(ctx, p)) return rc;
+  if (int rc = poly_need_q_source(ctx, p)) return rc;
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   if (!p->has_q) {
     int rc = poly_get_q(ctx, p, point);
@@ -921,9 +933,9 @@ extern "C" int tpst_poly_ipp(tpst_ctx* ctx, int n, const uint64_t* comms, uint64
 // prod_{r0 <= i < r1} ml(C_i, h_i) before final exponentiation (canonical
 // Fq12, 72 u64).  Rank 0 finishes T = FE(prod over ranks) with
 // tpst_gt_final_exp_product, so no rank runs more than its share of Miller loops.
-extern "C" int tpst_poly_commit_rows_partial(tpst_ctx* ctx, tpst_poly* p, size_t r0, size_t r1, uint64_t* comms,
-                                             uint64_t* miller) {
-  if (!ctx || !p || !comms || !miller || r1 < r0) return fail(ctx, TPST_E_ARG, "bad argument");
+static int commit_rows_partial(tpst_ctx* ctx, tpst_poly* p, size_t r0, size_t r1, uint64_t* comms, uint64_t* miller,
+                               void* d_out) {
+  if (!ctx || !p || ((!comms || !miller) && !d_out) || r1 < r0) return fail(ctx, TPST_E_ARG, "bad argument");
   std::lock_guard<std::mutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   SrsState* st = srs_of(ctx);
@@ -935,8 +947,13 @@ extern "C" int tpst_poly_commit_rows_partial(tpst_ctx* ctx, tpst_poly* p, size_t
   const size_t R = r1 - r0;
   hipStream_t s = ctx->stream;
   if (R == 0) {  // empty share: comms untouched, partial = 1
-    memset(miller, 0, 576);
-    miller[0] = 1;
+    uint64_t one[72] = {1};
+    if (d_out) {
+      TPST_HIP(ctx, hipMemcpyAsync(d_out, one, 576, hipMemcpyHostToDevice, s));
+      TPST_HIP(ctx, hipStreamSynchronize(s));
+    } else {
+      memcpy(miller, one, 576);
+    }
     return TPST_OK;
   }
   DevBuf rows, cm, out, hsub, tt;
@@ -957,15 +974,30 @@ extern "C" int tpst_poly_commit_rows_partial(tpst_ctx* ctx, tpst_poly* p, size_t
   TPST_HIP(ctx, multi_pairing_prepared(ctx->arena, s, cm.u(), h, lc, 1, R, (Fq12*)tt.p, false));
   TPST_HIP(ctx, affine_from_mont<Fq>(s, cm.u(), out.u(), R));
   TPST_HIP(ctx, fq12_from_mont(s, (Fq12*)tt.p, out.u() + 24 * R, 1));
-  TPST_HIP(ctx, hipMemcpyAsync(comms, out.p, R * 96, hipMemcpyDeviceToHost, s));
-  TPST_HIP(ctx, hipMemcpyAsync(miller, out.u() + 24 * R, 576, hipMemcpyDeviceToHost, s));
+  if (d_out) {  // [comms | partial] straight into the caller's (all-gather) buffer
+    TPST_HIP(ctx, hipMemcpyAsync(d_out, out.p, R * 96 + 576, hipMemcpyDeviceToDevice, s));
+  } else {
+    TPST_HIP(ctx, hipMemcpyAsync(comms, out.p, R * 96, hipMemcpyDeviceToHost, s));
+    TPST_HIP(ctx, hipMemcpyAsync(miller, out.u() + 24 * R, 576, hipMemcpyDeviceToHost, s));
+  }
   TPST_HIP(ctx, hipStreamSynchronize(s));
   return TPST_OK;
 }
 
-// T = FE(prod_k partials[k]) for k Miller-loop partials (canonical Fq12 each)
-extern "C" int tpst_gt_final_exp_product(tpst_ctx* ctx, const uint64_t* partials, size_t k, uint64_t* T) {
-  if (!ctx || (!partials && k) || !T) return fail(ctx, TPST_E_ARG, "null argument");
+extern "C" int tpst_poly_commit_rows_partial(tpst_ctx* ctx, tpst_poly* p, size_t r0, size_t r1, uint64_t* comms,
+                                             uint64_t* miller) {
+  return commit_rows_partial(ctx, p, r0, r1, comms, miller, nullptr);
+}
+
+extern "C" int tpst_poly_commit_rows_partial_dev(tpst_ctx* ctx, tpst_poly* p, size_t r0, size_t r1, void* d_out) {
+  return commit_rows_partial(ctx, p, r0, r1, nullptr, nullptr, d_out);
+}
+
+// T = FE(prod_k partials[k]) for k Miller-loop partials (canonical Fq12 each;
+// host, or device with a byte stride between consecutive partials)
+static int final_exp_product(tpst_ctx* ctx, const uint64_t* partials, const void* d_partials, size_t stride,
+                             size_t k, uint64_t* T) {
+  if (!ctx || (!partials && !d_partials && k) || !T) return fail(ctx, TPST_E_ARG, "null argument");
   std::lock_guard<std::mutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
@@ -974,7 +1006,10 @@ extern "C" int tpst_gt_final_exp_product(tpst_ctx* ctx, const uint64_t* partials
   TPST_HIP(ctx, up.alloc(kk * sizeof(Fq12)));
   TPST_HIP(ctx, out.alloc(sizeof(Fq12) + 576));
   if (k) {
-    TPST_HIP(ctx, hipMemcpyAsync(up.p, partials, k * 576, hipMemcpyHostToDevice, s));
+    if (d_partials)
+      TPST_HIP(ctx, hipMemcpy2DAsync(up.p, 576, d_partials, stride, 576, k, hipMemcpyDeviceToDevice, s));
+    else
+      TPST_HIP(ctx, hipMemcpyAsync(up.p, partials, k * 576, hipMemcpyHostToDevice, s));
     TPST_HIP(ctx, points_to_mont<Fq>(s, up.u(), up.u(), 6 * k));  // 12 Fq = 6 "points"
   }
   ctx->arena.reset();
@@ -983,6 +1018,143 @@ extern "C" int tpst_gt_final_exp_product(tpst_ctx* ctx, const uint64_t* partials
   TPST_HIP(ctx, fq12_from_mont(s, (Fq12*)out.p, out.u() + sizeof(Fq12) / 4, 1));
   TPST_HIP(ctx, hipMemcpyAsync(T, out.u() + sizeof(Fq12) / 4, 576, hipMemcpyDeviceToHost, s));
   TPST_HIP(ctx, hipStreamSynchronize(s));
+  return TPST_OK;
+}
+
+extern "C" int tpst_gt_final_exp_product(tpst_ctx* ctx, const uint64_t* partials, size_t k, uint64_t* T) {
+  return final_exp_product(ctx, partials, nullptr, 0, k, T);
+}
+
+extern "C" int tpst_gt_final_exp_product_dev(tpst_ctx* ctx, const void* d_partials, size_t stride_bytes, size_t k,
+                                             uint64_t* T) {
+  if (stride_bytes < 576) return fail(ctx, TPST_E_ARG, "stride below one Fq12");
+  return final_exp_product(ctx, nullptr, d_partials, stride_bytes, k, T);
+}
+
+// ------------------------------------------------ row-sharded opening -----
+// rank g holds rows [r0, r1) of the strided view (a
+// column-slice handle), so it computes its share of get_q's mat-vec
+//   zq_g[j] = sum_{r0 <= i < r1} Z_i[j] chi_i(b)            (sqrt_pst.rs:92-95)
+// and of c_u = MSM(comm_list, chi(b))                      (sqrt_pst.rs:198);
+// the shares are gathered as bytes (RCCL has no mod-r or elliptic-curve
+// reduction) and summed on rank 0, which then opens from q alone.
+static int chi_b_table(tpst_ctx* ctx, int m_col, int m_row, const uint64_t* point, DevBuf& chis) {
+  hipStream_t s = ctx->stream;
+  DevBuf b;
+  TPST_HIP(ctx, b.alloc((size_t)(m_col ? m_col : 1) * 32));
+  if (m_col) {
+    TPST_HIP(ctx, hipMemcpyAsync(b.p, point + 4 * m_row, m_col * 32, hipMemcpyHostToDevice, s));
+    TPST_HIP(ctx, fr_to_mont(s, b.u(), b.u(), m_col));
+  }
+  TPST_HIP(ctx, chis.alloc(((size_t)1 << m_col) * 32));
+  TPST_HIP(ctx, chi_table(s, b.u(), m_col, chis.u()));
+  return hipStreamSynchronize(s) == hipSuccess ? TPST_OK : fail(ctx, TPST_E_HIP, "chi table");
+}
+
+static int poly_q_partial(tpst_ctx* ctx, tpst_poly* p, const uint64_t* point, size_t r0, size_t r1, void* d_out,
+                          uint64_t* h_out) {
+  if (!ctx || !p || !point || (!d_out && !h_out) || r1 < r0) return fail(ctx, TPST_E_ARG, "bad argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  if (p->q_only) return fail(ctx, TPST_E_STATE, "opening-only handle holds no evaluations");
+  for (int i = 0; i < p->n; i++)
+    if (!fr_ok(point + 4 * i)) return fail(ctx, TPST_E_ARG, "point coordinate >= r");
+  const uint32_t* zb;
+  size_t cs;
+  if (int rc = poly_rows_view(ctx, p, r0, r1, &zb, &cs)) return rc;
+  DevBuf chis, tmp;
+  if (int rc = chi_b_table(ctx, p->m_col, p->m_row, point, chis)) return rc;
+  hipStream_t s = ctx->stream;
+  const size_t N = (size_t)1 << p->m_row;
+  uint32_t* dst = (uint32_t*)d_out;
+  if (!dst) {
+    TPST_HIP(ctx, tmp.alloc(N * 32));
+    dst = tmp.u();
+  }
+  if (r1 > r0) {
+    TPST_HIP(ctx, get_q_rows(s, zb, cs, r1 - r0, p->m_row, chis.u() + 8 * r0, dst));
+  } else {
+    TPST_HIP(ctx, hipMemsetAsync(dst, 0, N * 32, s));
+  }
+  if (h_out) TPST_HIP(ctx, hipMemcpyAsync(h_out, dst, N * 32, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipStreamSynchronize(s));
+  return TPST_OK;
+}
+
+extern "C" int tpst_poly_get_q_partial(tpst_ctx* ctx, tpst_poly* p, const uint64_t* point, size_t r0, size_t r1,
+                                       uint64_t* zq) {
+  return poly_q_partial(ctx, p, point, r0, r1, nullptr, zq);
+}
+
+extern "C" int tpst_poly_get_q_partial_dev(tpst_ctx* ctx, tpst_poly* p, const uint64_t* point, size_t r0, size_t r1,
+                                           void* d_zq) {
+  return poly_q_partial(ctx, p, point, r0, r1, d_zq, nullptr);
+}
+
+extern "C" int tpst_fr_sum_dev(tpst_ctx* ctx, const void* d_parts, size_t k, size_t n, void* d_out) {
+  if (!ctx || (n && (!d_parts || !d_out))) return fail(ctx, TPST_E_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  TPST_HIP(ctx, fr_sum_parts(ctx->stream, (const uint32_t*)d_parts, k, n, (uint32_t*)d_out));
+  TPST_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return TPST_OK;
+}
+
+// c_u's share: sum_{r0 <= i < r1} chi_i(b) C_i over this rank's row commitments
+extern "C" int tpst_poly_cu_partial(tpst_ctx* ctx, int n, const uint64_t* point, size_t r0, size_t r1,
+                                    const uint64_t* comms, uint64_t* out) {
+  if (!ctx || !point || (!comms && r1 > r0) || !out || r1 < r0) return fail(ctx, TPST_E_ARG, "bad argument");
+  int m_col, m_row, odd;
+  if (poly_dims(n, m_col, m_row, odd)) return fail(ctx, TPST_E_ARG, "bad num_vars");
+  if (r1 > ((size_t)1 << m_col)) return fail(ctx, TPST_E_ARG, "row range out of bounds");
+  for (int i = 0; i < n; i++)
+    if (!fr_ok(point + 4 * i)) return fail(ctx, TPST_E_ARG, "point coordinate >= r");
+  std::vector<uint64_t> sc((r1 - r0) * 4 + 4);
+  {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    TPST_HIP(ctx, hipSetDevice(ctx->device));
+    DevBuf chis;
+    if (int rc = chi_b_table(ctx, m_col, m_row, point, chis)) return rc;
+    if (r1 > r0) {
+      TPST_HIP(ctx, fr_from_mont(ctx->stream, chis.u() + 8 * r0, chis.u() + 8 * r0, r1 - r0));
+      TPST_HIP(ctx, hipMemcpyAsync(sc.data(), chis.u() + 8 * r0, (r1 - r0) * 32, hipMemcpyDeviceToHost, ctx->stream));
+      TPST_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
+  }
+  if (r1 == r0) {
+    memset(out, 0, 96);
+    return TPST_OK;
+  }
+  return tpst_g1_msm(ctx, comms, r1 - r0, sc.data(), r1 - r0, out);
+}
+
+// opening-only Polynomial from the combined q (2^m_row canonical Fr, device)
+// and, optionally, the combined c_u (canonical affine; NULL = the opening
+// computes U = MSM(comm_list, chi(b)) itself)
+extern "C" int tpst_poly_from_q_dev(tpst_ctx* ctx, int n, const uint64_t* point, const void* d_zq,
+                                    const uint64_t* U, tpst_poly** out) {
+  if (!ctx || !point || !d_zq || !out) return fail(ctx, TPST_E_ARG, "null argument");
+  auto p = std::make_unique<tpst_poly>();
+  if (poly_dims(n, p->m_col, p->m_row, p->odd)) return fail(ctx, TPST_E_ARG, "bad num_vars");
+  for (int i = 0; i < n; i++)
+    if (!fr_ok(point + 4 * i)) return fail(ctx, TPST_E_ARG, "point coordinate >= r");
+  if (U && !point_valid<Fq>(U)) return fail(ctx, TPST_E_ARG, "c_u is not a valid G1 point");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  p->ctx = ctx;
+  p->n = n;
+  p->q_only = true;
+  if (int rc = chi_b_table(ctx, p->m_col, p->m_row, point, p->chis)) return rc;
+  const size_t N = (size_t)1 << p->m_row;
+  TPST_HIP(ctx, p->q.alloc(N * 32));
+  TPST_HIP(ctx, fr_to_mont(ctx->stream, (const uint32_t*)d_zq, p->q.u(), N));
+  TPST_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  p->has_q = true;
+  if (U) {
+    memcpy(p->U, U, 96);
+    p->has_u = true;
+  }
+  *out = p.release();
   return TPST_OK;
 }
 
@@ -1118,7 +1290,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   (void)T;  // the reference passes T but the prover does not use it (mipp.rs:38)
   if (!ctx || !p || !tr || !comms || !point || !proof) return fail(ctx, TPST_E_ARG, "null argument");
   std::lock_guard<std::mutex> lk(ctx->mu);
-  if (int rc = poly_need_full(ctx, p)) return rc;
+  if (int rc = poly_need_q_source(ctx, p)) return rc;
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   SrsState* st = srs_of(ctx);
   if (!st) return fail(ctx, TPST_E_STATE, "no SRS loaded");
@@ -1218,9 +1390,13 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   // ---- stream C (round 0): the fold table over comm_list
   TPST_HIP(ctx, fbt_build<Fq>(arC, sC, A.u(), C, st->t_A.u()));
   TPST_HIP(ctx, hipEventRecord(ev[EV_TABLE], sC));
-  // ---- stream B: U = MSM(comm_list, chi(b)) on that table
+  // ---- stream B: U = MSM(comm_list, chi(b)) on that table (or the c_u the
+  // ranks combined, for an opening-only handle)
   TPST_HIP(ctx, hipStreamWaitEvent(sB, ev[EV_TABLE], 0));
-  {
+  if (p->has_u) {
+    memcpy(pin + dn_U, p->U, 96);
+    TPST_HIP(ctx, hipEventRecord(ev[EV_U], sB));
+  } else {
     FbGroups g;
     g.members = C;
     g.L = g.D = C;

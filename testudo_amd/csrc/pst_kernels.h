@@ -17,6 +17,11 @@ hipError_t chi_table(hipStream_t s, const uint32_t* d_b, int m, uint32_t* d_out)
 
 // q[j] = sum_i Z[(j << m_col) | i] * chis[i]  (sqrt_pst.rs:93-96); Z canonical, chis/q Montgomery
 hipError_t get_q(hipStream_t s, const uint32_t* d_Z, int m_col, int m_row, const uint32_t* d_chis, uint32_t* d_q);
+// a row shard's share of q: out[j] = sum_{i < nr} Z[j cs + i] chis[i] (canonical out)
+hipError_t get_q_rows(hipStream_t s, const uint32_t* d_Z, size_t cs, size_t nr, int m_row, const uint32_t* d_chis,
+                      uint32_t* d_q_canonical);
+// the combine of the shares: out = sum of k canonical Fr vectors of length n, mod r
+hipError_t fr_sum_parts(hipStream_t s, const uint32_t* d_parts, size_t k, size_t n, uint32_t* d_out);
 
 // v = sum_j x[j] * y[j] (Montgomery), one value
 hipError_t fr_dot(hipStream_t s, const uint32_t* d_x, const uint32_t* d_y, size_t n, uint32_t* d_v);

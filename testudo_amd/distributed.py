@@ -1,4 +1,4 @@
-"""Row-sharded sqrt-PST commit across ranks.
+"""Row-sharded sqrt-PST commit and opening inputs across ranks.
 
 One process per GPU (torch.distributed; backend "nccl" = RCCL over xGMI on
 MI355X, "gloo" on CPU for tests).  The 2^m_col row MSMs of
@@ -6,19 +6,30 @@ MI355X, "gloo" on CPU for tests).  The 2^m_col row MSMs of
 [g*R, (g+1)*R), R = 2^m_col / world -- a contiguous block of *columns* of Z,
 which the K1 kernel reads through the strided view with no data movement.
 
-Exchange: every rank also runs the Miller loops of its own rows' pairs
-(C_i, h_i) and keeps their product f_g unreduced, so the IPP
-T = prod e(C_i, h_i) (sqrt_pst.rs:128-143) is split by rows too.  One RCCL
+Commit exchange (C1/C2): every rank also runs the Miller loops of its own rows'
+pairs (C_i, h_i) and keeps their product f_g unreduced, so the IPP
+T = prod e(C_i, h_i) (sqrt_pst.rs:128-143) is split by rows too.  One
 all-gather moves each rank's [row commitments (96 B each) | f_g (576 B)] as
-raw bytes (RCCL has no elliptic-curve or GT reduction op, so nothing is
-reduced in flight); rank 0 multiplies the world's f_g and runs the single
-final exponentiation, then broadcasts T (576 B).  The per-rank compute and
-the finalisation are injected, so the orchestration is testable on CPU with
-the C++ oracle standing in for the GPU (tests/test_distributed.py).
+raw bytes, device tensor to device tensor (RCCL has no elliptic-curve or GT
+reduction op, so nothing is reduced in flight); rank 0 multiplies the world's
+f_g and runs the single final exponentiation straight from the gathered
+device buffer, then broadcasts T (576 B).
+
+Opening exchange (C3): get_q's mat-vec z_q[j] = sum_i Z_i[j] chi_i(b)
+(sqrt_pst.rs:92-95) and c_u = sum_i chi_i(b) C_i (sqrt_pst.rs:198) are sums
+over rows, so each rank computes its rows' share of both; one all-gather of
+[z_q share (2^m_row Fr) | c_u share (G1)] and a mod-r / G1 sum on rank 0 give
+q and U, and rank 0 opens from q alone (no rank holds the whole Z).  The MIPP
+rounds, the PST proof of q and the final folds are transcript-sequential and
+KB-sized: they stay on rank 0.
+
+The per-rank compute and the combines are injected, so the orchestration is
+testable on CPU with the C++ oracle standing in for the GPU
+(tests/test_distributed.py).
 """
 from __future__ import annotations
 
-from typing import Callable, Tuple
+from typing import Callable, Optional, Tuple
 
 import numpy as np
 
@@ -30,30 +41,71 @@ def shard_rows(n_rows: int, world: int, rank: int) -> Tuple[int, int]:
     return rank * per, (rank + 1) * per
 
 
-def sharded_commit(n: int, commit_rows_partial: Callable[[int, int], Tuple[np.ndarray, np.ndarray]],
-                   finalize: Callable[[np.ndarray], np.ndarray], dist, device) -> Tuple[np.ndarray, np.ndarray]:
-    """Returns (comm_list (2^m_col, 12) uint64, T (72,) uint64) on every rank.
+def _device(dist, device):
+    return "cpu" if dist.get_backend() == "gloo" else device  # gloo moves host tensors only
 
-    commit_rows_partial(r0, r1) -> (comms (r1-r0, 12), miller partial (72,));
-    finalize(partials (world, 72)) -> T, run on rank 0 only."""
+
+def _all_gather(dist, t):
+    """(world, *t.shape) tensor on t's device: one all-gather of equal-size shares."""
     import torch
-    if dist.get_backend() == "gloo":  # gloo gathers host tensors only
-        device = "cpu"
-    world = dist.get_world_size()
-    rank = dist.get_rank()
-    m_col = n // 2
-    r0, r1 = shard_rows(1 << m_col, world, rank)
-    comms, ml = commit_rows_partial(r0, r1)
-    local = np.concatenate([np.ascontiguousarray(comms, dtype=np.uint64).reshape(-1),
-                            np.ascontiguousarray(ml, dtype=np.uint64).reshape(72)])
-    t = torch.from_numpy(local.view(np.int64).copy()).to(device)
-    parts = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(parts, t)  # C1: row commitments + Miller partials, bytes only
-    got = torch.stack(parts).cpu().numpy().view(np.uint64)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return torch.stack(parts)
+
+
+def sharded_commit(n: int, commit_rows_partial_into: Callable, finalize: Callable, dist,
+                   device) -> Tuple[Optional[np.ndarray], np.ndarray, np.ndarray]:
+    """Row-sharded Polynomial::commit.
+
+    commit_rows_partial_into(r0, r1, out) fills the int64 tensor ``out`` (on
+    the rank's device, R * 12 + 72 words) with [row commitments (R, 12) |
+    unreduced Miller partial (72)] as canonical u64 limbs;
+    finalize(gathered) -> T (72,) uint64 runs on rank 0 over the gathered
+    (world, R * 12 + 72) device tensor.
+
+    Returns (comm_list (2^m_col, 12) uint64 on rank 0 else None, T (72,) on
+    every rank, this rank's own row commitments (R, 12))."""
+    import torch
+    dev = _device(dist, device)
+    world, rank = dist.get_world_size(), dist.get_rank()
+    r0, r1 = shard_rows(1 << (n // 2), world, rank)
     R = r1 - r0
-    comm_list = got[:, :12 * R].reshape(-1, 12).copy()
-    T = torch.zeros(72, dtype=torch.int64, device=device)
+    buf = torch.empty(R * 12 + 72, dtype=torch.int64, device=dev)
+    commit_rows_partial_into(r0, r1, buf)
+    got = _all_gather(dist, buf)  # C1 + C2: bytes only
+    own = buf[:12 * R].cpu().numpy().view(np.uint64).reshape(R, 12).copy()
+    T = torch.zeros(72, dtype=torch.int64, device=dev)
+    comm_list = None
     if rank == 0:
-        T.copy_(torch.from_numpy(np.ascontiguousarray(finalize(got[:, 12 * R:]), dtype=np.uint64).view(np.int64)))
+        comm_list = got[:, :12 * R].cpu().numpy().view(np.uint64).reshape(-1, 12).copy()
+        T.copy_(torch.from_numpy(np.ascontiguousarray(finalize(got), dtype=np.uint64).view(np.int64)))
     dist.broadcast(T, src=0)
-    return comm_list, T.cpu().numpy().view(np.uint64).copy()
+    return comm_list, T.cpu().numpy().view(np.uint64).copy(), own
+
+
+def sharded_open_inputs(n: int, q_partial_into: Callable, cu_partial: Callable, combine_q: Callable,
+                        combine_cu: Callable, dist, device):
+    """C3: this rank's rows' share of z_q and of c_u, one all-gather, the
+    combine on rank 0.
+
+    q_partial_into(r0, r1, out) fills the int64 tensor ``out`` (2^m_row * 4
+    words) with the share of z_q (canonical Fr); cu_partial(r0, r1) -> (12,)
+    uint64 canonical affine share of c_u; combine_q(gathered (world, N * 4)
+    tensor) -> z_q as an int64 tensor on the rank's device; combine_cu(shares
+    (world, 12) uint64) -> U (12,).  Returns (z_q, U) on rank 0, (None, None)
+    elsewhere."""
+    import torch
+    dev = _device(dist, device)
+    world, rank = dist.get_world_size(), dist.get_rank()
+    r0, r1 = shard_rows(1 << (n // 2), world, rank)
+    N = 1 << (n - n // 2)
+    buf = torch.empty(N * 4 + 12, dtype=torch.int64, device=dev)
+    q_partial_into(r0, r1, buf[:N * 4])
+    cu = np.ascontiguousarray(cu_partial(r0, r1), dtype=np.uint64).reshape(12)
+    buf[N * 4:].copy_(torch.from_numpy(cu.view(np.int64)))
+    got = _all_gather(dist, buf)
+    if rank != 0:
+        return None, None
+    zq = combine_q(got[:, :N * 4].contiguous())
+    U = combine_cu(got[:, N * 4:].cpu().numpy().view(np.uint64).copy())
+    return zq, np.ascontiguousarray(U, dtype=np.uint64).reshape(12)

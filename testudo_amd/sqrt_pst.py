@@ -249,6 +249,54 @@ class Polynomial:
                        "commit_rows_partial")
         return out, ml
 
+    def commit_rows_partial_into(self, r0: int, r1: int, out) -> None:
+        """commit_rows_partial written into the int64 tensor ``out`` (R * 12 +
+        72 words, [comms | Miller partial]): straight from device memory when
+        ``out`` is a GPU tensor (the RCCL all-gather buffer), else via host."""
+        if out.is_cuda:
+            self.ctx.check(self.ctx.lib.tpst_poly_commit_rows_partial_dev(self.ctx.h, self.h, r0, r1,
+                                                                          C.c_void_p(out.data_ptr())),
+                           "commit_rows_partial_dev")
+            return
+        import torch
+        cm, ml = self.commit_rows_partial(r0, r1)
+        out.copy_(torch.from_numpy(np.concatenate([cm.reshape(-1), ml]).view(np.int64)))
+
+    def get_q_partial(self, point, r0: int, r1: int) -> np.ndarray:
+        """Rows [r0, r1)'s share of get_q (sqrt_pst.rs:92-95): (2^m_row, 4) canonical Fr."""
+        point = _u64(point, (self.n, 4))
+        out = np.zeros((1 << self.m_row, 4), dtype=np.uint64)
+        self.ctx.check(self.ctx.lib.tpst_poly_get_q_partial(self.ctx.h, self.h, ptr(point), r0, r1, ptr(out)),
+                       "get_q_partial")
+        return out
+
+    def get_q_partial_into(self, point, r0: int, r1: int, out) -> None:
+        """get_q_partial into the int64 tensor ``out`` (device-side when it is a GPU tensor)."""
+        if out.is_cuda:
+            point = _u64(point, (self.n, 4))
+            self.ctx.check(self.ctx.lib.tpst_poly_get_q_partial_dev(self.ctx.h, self.h, ptr(point), r0, r1,
+                                                                    C.c_void_p(out.data_ptr())),
+                           "get_q_partial_dev")
+            return
+        import torch
+        out.copy_(torch.from_numpy(self.get_q_partial(point, r0, r1).reshape(-1).view(np.int64)))
+
+    @classmethod
+    def from_q(cls, ctx: Context, n: int, point, zq, U=None) -> "Polynomial":
+        """Opening-only Polynomial from the combined q (an int64 tensor of 2^m_row
+        canonical Fr, moved to the device if needed) and optionally the combined
+        c_u: serves eval and open; no evaluations resident."""
+        import torch
+        point = _u64(point, (n, 4))
+        if not zq.is_cuda:
+            zq = zq.to(torch.device("cuda", ctx.device))
+        zq = zq.contiguous()
+        Up = ptr(_u64(U, (12,))) if U is not None else None
+        h = C.c_void_p()
+        ctx.check(ctx.lib.tpst_poly_from_q_dev(ctx.h, n, ptr(point), C.c_void_p(zq.data_ptr()), Up, C.byref(h)),
+                  "from_q")
+        return cls(ctx, h, n, keep=zq)
+
     def commit_dev(self, d_comms: int, d_T: int):
         self.ctx.check(self.ctx.lib.tpst_poly_commit_dev(self.ctx.h, self.h, C.c_void_p(d_comms),
                                                          C.c_void_p(d_T)), "commit_dev")
@@ -292,6 +340,51 @@ def ipp(ctx: Context, n: int, comms) -> np.ndarray:
     T = np.zeros(72, dtype=np.uint64)
     ctx.check(ctx.lib.tpst_poly_ipp(ctx.h, n, ptr(_u64(comms, (-1, 12))), ptr(T)), "ipp")
     return T
+
+
+def gt_final_exp_product_gathered(ctx: Context, gathered, R: int) -> np.ndarray:
+    """T = FE(prod of the Miller partials) of an all-gathered (world, R * 12 +
+    72) int64 tensor of commit_rows_partial shares, read in place on the device."""
+    import torch
+    if not gathered.is_cuda:
+        gathered = gathered.to(torch.device("cuda", ctx.device))
+    gathered = gathered.contiguous()
+    k, w = gathered.shape
+    T = np.zeros(72, dtype=np.uint64)
+    ctx.check(ctx.lib.tpst_gt_final_exp_product_dev(ctx.h, C.c_void_p(gathered.data_ptr() + 96 * R), 8 * w, k,
+                                                    ptr(T)), "gt_final_exp_product_dev")
+    return T
+
+
+def fr_sum(ctx: Context, gathered):
+    """Mod-r sum of the rows of a (k, n * 4) int64 tensor of canonical Fr (the C3
+    combine): an (n * 4,) int64 tensor on the context's device."""
+    import torch
+    if not gathered.is_cuda:
+        gathered = gathered.to(torch.device("cuda", ctx.device))
+    gathered = gathered.contiguous()
+    k, w = gathered.shape
+    out = torch.empty(w, dtype=torch.int64, device=gathered.device)
+    ctx.check(ctx.lib.tpst_fr_sum_dev(ctx.h, C.c_void_p(gathered.data_ptr()), k, w // 4, C.c_void_p(out.data_ptr())),
+              "fr_sum_dev")
+    return out
+
+
+def cu_partial(ctx: Context, n: int, point, r0: int, r1: int, comms_rows) -> np.ndarray:
+    """Rows [r0, r1)'s share of c_u = MSM(comm_list, chi(b)) (sqrt_pst.rs:198), (12,)."""
+    point = _u64(point, (n, 4))
+    comms_rows = _u64(comms_rows, (r1 - r0, 12)) if r1 > r0 else np.zeros((1, 12), dtype=np.uint64)
+    out = np.zeros(12, dtype=np.uint64)
+    ctx.check(ctx.lib.tpst_poly_cu_partial(ctx.h, n, ptr(point), r0, r1, ptr(comms_rows), ptr(out)), "cu_partial")
+    return out
+
+
+def g1_sum(ctx: Context, points) -> np.ndarray:
+    """Sum of canonical affine G1 points (the c_u combine): an MSM with unit scalars."""
+    points = _u64(points).reshape(-1, 12)
+    ones = np.zeros((len(points), 4), dtype=np.uint64)
+    ones[:, 0] = 1
+    return ctx.g1_msm(points, ones)
 
 
 def gt_final_exp_product(ctx: Context, partials) -> np.ndarray:
