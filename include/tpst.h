@@ -124,6 +124,11 @@ int tpst_g2_msm_fixed(tpst_ctx* ctx, const uint64_t* bases, size_t n, const uint
  * prod_i e(g1[i], g2[i]) after final exponentiation (ark-ec
  * Pairing::multi_pairing(...).0; sqrt_pst.rs:143, mipp.rs:397). */
 int tpst_multi_pairing(tpst_ctx* ctx, const uint64_t* g1, const uint64_t* g2, size_t n, uint64_t* out_gt);
+/* Valid::check of a canonical affine point (ark-serialize Validate::Yes):
+ * coordinates < p, on the curve, in the r-torsion subgroup (infinity = all
+ * zero is valid).  TPST_OK or TPST_E_VERIFY; host only, no context. */
+int tpst_g1_check(const uint64_t* p);
+int tpst_g2_check(const uint64_t* p);
 
 
 /* ---- sqrt-PST protocol ----------------------------------------------------

@@ -40,6 +40,8 @@ PROTOTYPES = [
     ("tpst_g1_msm_fixed", C.c_int, [_vp, _u64p, _sz, _u64p, _sz, _sz, _u64p]),
     ("tpst_g2_msm_fixed", C.c_int, [_vp, _u64p, _sz, _u64p, _sz, _sz, _u64p]),
     ("tpst_multi_pairing", C.c_int, [_vp, _u64p, _u64p, _sz, _u64p]),
+    ("tpst_g1_check", C.c_int, [_u64p]),
+    ("tpst_g2_check", C.c_int, [_u64p]),
     ("tpst_g1_mul_generator", C.c_int, [_vp, _u64p, _sz, _u64p]),
     ("tpst_g2_mul_generator", C.c_int, [_vp, _u64p, _sz, _u64p]),
     ("tpst_g1_mul_generator_dev", C.c_int, [_vp, _vp, _sz, _vp]),

@@ -13,6 +13,7 @@
 #include "../../include/tpst.h"
 #include "ctx.h"
 #include "fbt.h"
+#include "host_curve.h"
 #include "device_util.h"
 #include "pst_kernels.h"
 
@@ -321,18 +322,11 @@ bool all_zero(const uint64_t* a, int n) {
     if (a[i]) return false;
   return true;
 }
-// canonical coordinates, on the curve, and r * P == O (prime-order subgroup)
+// canonical coordinates, on the curve, and r * P == O (prime-order subgroup),
+// on 64-bit host arithmetic (host_curve.h)
 template <class F>
 bool point_valid(const uint64_t* p) {
-  constexpr int NQ = sizeof(F) / sizeof(Fq);  // Fq coordinates per F
-  for (int k = 0; k < 2 * NQ; k++)
-    if (!fq_ok(p + 6 * k)) return false;
-  if (all_zero(p, 12 * NQ)) return true;  // infinity
-  Affine<F> a;
-  Fq* c = reinterpret_cast<Fq*>(&a);
-  for (int k = 0; k < 2 * NQ; k++) c[k] = fq_canon(p + 6 * k);
-  if (!on_curve(a)) return false;
-  return is_inf(scalar_mul(a, params::FR_P, 253));
+  return host::point_in_subgroup<F>(p);
 }
 bool gt_ok(const uint64_t* f) {
   for (int k = 0; k < 12; k++)
@@ -603,6 +597,11 @@ extern "C" int tpst_srs_export(tpst_ctx* ctx, uint64_t* flat) {
   memcpy(flat, st->flat.data(), st->flat.size() * 8);
   return TPST_OK;
 }
+
+// Valid::check of an affine point (what Validate::Yes deserialisation runs):
+// canonical coordinates, on the curve, in the r-torsion subgroup.  Host only.
+extern "C" int tpst_g1_check(const uint64_t* p) { return p && point_valid<Fq>(p) ? TPST_OK : TPST_E_VERIFY; }
+extern "C" int tpst_g2_check(const uint64_t* p) { return p && point_valid<Fq2>(p) ? TPST_OK : TPST_E_VERIFY; }
 
 // internal (groth16.hip): the same element validation as the PST verifier
 bool tpst_internal_g1_valid(const uint64_t* p) { return point_valid<Fq>(p); }
@@ -1620,51 +1619,12 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
 }
 
 // -------------------------------------------------------------- verify ---
-// small helpers on host-side canonical points via device MSMs
-template <class F>
-static int small_msm(tpst_ctx* ctx, const std::vector<uint64_t>& pts_canon, const std::vector<uint64_t>& sc,
-                     uint64_t* out) {
-  constexpr size_t PW = 2 * Words<F>::n;
-  const size_t n = sc.size() / 4;
-  hipStream_t s = ctx->stream;
-  DevBuf b, bm, d_s, r, o;
-  TPST_HIP(ctx, b.alloc(n * PW * 4));
-  TPST_HIP(ctx, bm.alloc(n * PW * 4));
-  TPST_HIP(ctx, d_s.alloc(n * 32));
-  TPST_HIP(ctx, r.alloc(sizeof(Xyzz<F>)));
-  TPST_HIP(ctx, o.alloc(PW * 4));
-  TPST_HIP(ctx, hipMemcpyAsync(b.p, pts_canon.data(), n * PW * 4, hipMemcpyHostToDevice, s));
-  TPST_HIP(ctx, hipMemcpyAsync(d_s.p, sc.data(), n * 32, hipMemcpyHostToDevice, s));
-  TPST_HIP(ctx, points_to_mont<F>(s, b.u(), bm.u(), n));
-  TPST_HIP(ctx, msm_var<F>(ctx->arena, s, bm.u(), d_s.u(), n, (Xyzz<F>*)r.p));
-  TPST_HIP(ctx, xyzz_to_affine_canonical<F>(s, (Xyzz<F>*)r.p, o.u(), 1));
-  TPST_HIP(ctx, hipMemcpyAsync(out, o.p, PW * 4, hipMemcpyDeviceToHost, s));
-  TPST_HIP(ctx, hipStreamSynchronize(s));
-  return TPST_OK;
-}
-
-static int pairing_product(tpst_ctx* ctx, const std::vector<uint64_t>& g1, const std::vector<uint64_t>& g2,
-                           uint64_t* out_gt) {
-  const size_t n = g1.size() / 12;
-  hipStream_t s = ctx->stream;
-  DevBuf a, am, b, bm, f, o;
-  TPST_HIP(ctx, a.alloc(n * 96));
-  TPST_HIP(ctx, am.alloc(n * 96));
-  TPST_HIP(ctx, b.alloc(n * 192));
-  TPST_HIP(ctx, bm.alloc(n * 192));
-  TPST_HIP(ctx, f.alloc(sizeof(Fq12)));
-  TPST_HIP(ctx, o.alloc(576));
-  TPST_HIP(ctx, hipMemcpyAsync(a.p, g1.data(), n * 96, hipMemcpyHostToDevice, s));
-  TPST_HIP(ctx, hipMemcpyAsync(b.p, g2.data(), n * 192, hipMemcpyHostToDevice, s));
-  TPST_HIP(ctx, points_to_mont<Fq>(s, a.u(), am.u(), n));
-  TPST_HIP(ctx, points_to_mont<Fq2>(s, b.u(), bm.u(), n));
-  TPST_HIP(ctx, multi_pairing(ctx->arena, s, am.u(), bm.u(), 1, n, (Fq12*)f.p));
-  TPST_HIP(ctx, fq12_from_mont(s, (Fq12*)f.p, o.u(), 1));
-  TPST_HIP(ctx, hipMemcpyAsync(out_gt, o.p, 576, hipMemcpyDeviceToHost, s));
-  TPST_HIP(ctx, hipStreamSynchronize(s));
-  return TPST_OK;
-}
-
+// The verifier is a handful of short serial chains (two-term scalar
+// combinations, subgroup checks) plus three pairing products and the GT
+// exponentiations: the chains run on host threads (host_curve.h, ~30 ns per
+// Fq product against ~1.6 us on a lone GPU lane), the pairing products in ONE
+// device launch (groups padded with infinity pairs), the GT powers on a side
+// stream (pairing.hip k_gt_pow_wave).
 static bool gt_is_one(const uint64_t* gt) {
   if (gt[0] != 1) return false;
   for (int i = 1; i < 72; i++)
@@ -1674,6 +1634,41 @@ static bool gt_is_one(const uint64_t* gt) {
 
 static void push(std::vector<uint64_t>& v, const uint64_t* p, size_t n) { v.insert(v.end(), p, p + n); }
 
+// pairs of one pairing-product check (canonical affine G1 12 u64, G2 24 u64)
+struct PairSet {
+  std::vector<uint64_t> g1, g2;
+  size_t n() const { return g1.size() / 12; }
+};
+
+// prod_{pairs in group g} e(P, Q) for every group, one multi-pairing launch
+// (groups padded to a common length with infinity pairs, which contribute 1)
+static int pairing_groups(tpst_ctx* ctx, const std::vector<const PairSet*>& sets, std::vector<uint64_t>& gts) {
+  const size_t G = sets.size();
+  size_t n = 1;
+  for (const PairSet* p : sets) n = std::max(n, p->n());
+  std::vector<uint64_t> g1(G * n * 12, 0), g2(G * n * 24, 0);
+  for (size_t g = 0; g < G; g++) {
+    std::copy(sets[g]->g1.begin(), sets[g]->g1.end(), g1.begin() + g * n * 12);
+    std::copy(sets[g]->g2.begin(), sets[g]->g2.end(), g2.begin() + g * n * 24);
+  }
+  hipStream_t s = ctx->stream;
+  DevBuf a, b, f, o;
+  TPST_HIP(ctx, a.alloc(G * n * 96));
+  TPST_HIP(ctx, b.alloc(G * n * 192));
+  TPST_HIP(ctx, f.alloc(G * sizeof(Fq12)));
+  TPST_HIP(ctx, o.alloc(G * 576));
+  TPST_HIP(ctx, hipMemcpyAsync(a.p, g1.data(), G * n * 96, hipMemcpyHostToDevice, s));
+  TPST_HIP(ctx, hipMemcpyAsync(b.p, g2.data(), G * n * 192, hipMemcpyHostToDevice, s));
+  TPST_HIP(ctx, points_to_mont<Fq>(s, a.u(), a.u(), G * n));
+  TPST_HIP(ctx, points_to_mont<Fq2>(s, b.u(), b.u(), G * n));
+  TPST_HIP(ctx, multi_pairing(ctx->arena, s, a.u(), b.u(), G, n, (Fq12*)f.p));
+  TPST_HIP(ctx, fq12_from_mont(s, (Fq12*)f.p, o.u(), G));
+  gts.assign(G * 72, 0);
+  TPST_HIP(ctx, hipMemcpyAsync(gts.data(), o.p, G * 576, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipStreamSynchronize(s));
+  return TPST_OK;
+}
+
 // MultilinearPC::check (circuit_verifier.rs:245-314): for k points pt (LSB-first,
 // canonical Fr) and k G2 proofs,
 //   e(C - g^v, h) * prod_i e(g^{pt_i} - g_mask[nv - k + i], pi_i) == 1.
@@ -1681,78 +1676,64 @@ static void push(std::vector<uint64_t>& v, const uint64_t* p, size_t n) { v.inse
 // the trapdoor coordinates t[ck.nv - k ..], hence the mask offset (the same
 // offset check_2 applies to h_mask, circuit_verifier.rs:214); the reference
 // only checks full-level polynomials (sqrt_pst.rs:261), where it is 0.
-static int mlpc_check_impl(tpst_ctx* ctx, SrsState* st, int k, const uint64_t* comm, const uint64_t* pt,
-                           const uint64_t* v, const uint64_t* proofs) {
+static void mlpc_check_pairs(const SrsState* st, int k, const uint64_t* comm, const uint64_t* pt, const uint64_t* v,
+                             const uint64_t* proofs, PairSet& ps) {
   const uint64_t* flat = st->flat.data();
   const uint64_t* g = flat;
   const uint64_t* h = flat + 12;
   const uint64_t* gmask = flat + tpst_srs_flat_len(st->nv) - 36 * st->nv;
-  const uint64_t one[4] = {1, 0, 0, 0};
-  uint64_t minus1[4], negv[4];
-  fr_out(sub(Fr::zero(), Fr::one()), minus1);
+  uint64_t negv[4];
   fr_out(sub(Fr::zero(), fr_canon(v)), negv);
-  std::vector<uint64_t> g1s, g2s, pts, sc;
-  uint64_t q[12];
-  int rc;
-  push(pts, comm, 12);
-  push(sc, one, 4);
-  push(pts, g, 12);
-  push(sc, negv, 4);
-  if ((rc = small_msm<Fq>(ctx, pts, sc, q))) return rc;
-  push(g1s, q, 12);
-  push(g2s, h, 24);
-  for (int i = 0; i < k; i++) {
-    pts.clear();
-    sc.clear();
-    push(pts, g, 12);
-    push(sc, pt + 4 * i, 4);
-    push(pts, gmask + 12 * (st->nv - k + i), 12);
-    push(sc, minus1, 4);
-    if ((rc = small_msm<Fq>(ctx, pts, sc, q))) return rc;
-    push(g1s, q, 12);
-    push(g2s, proofs + 24 * i, 24);
-  }
-  uint64_t gt[72];
-  if ((rc = pairing_product(ctx, g1s, g2s, gt))) return rc;
-  return gt_is_one(gt) ? TPST_OK : TPST_E_VERIFY;
+  ps.g1.assign((size_t)(k + 1) * 12, 0);
+  ps.g2.clear();
+  push(ps.g2, h, 24);
+  for (int i = 0; i < k; i++) push(ps.g2, proofs + 24 * i, 24);
+  host::parallel_for((size_t)k + 1, [&](size_t i) {
+    if (i == 0)
+      host::mul_add<Fq>(g, negv, comm, 1, &ps.g1[0]);  // C - g^v
+    else
+      host::mul_add<Fq>(g, pt + 4 * (i - 1), gmask + 12 * (st->nv - k + i - 1), -1, &ps.g1[12 * i]);
+  });
 }
 
 // check_2 (circuit_verifier.rs:175-243; mipp.rs:307): G2 commitment C_h, k G1
 // proofs,  e(g, C_h - h^v) * prod_i e(pi_i, h^{pt_i} - h_mask[nv - k + i]) == 1
-static int mlpc_check2_impl(tpst_ctx* ctx, SrsState* st, int k, const uint64_t* comm_h, const uint64_t* pt,
-                            const uint64_t* v, const uint64_t* proofs) {
+static void mlpc_check2_pairs(const SrsState* st, int k, const uint64_t* comm_h, const uint64_t* pt,
+                              const uint64_t* v, const uint64_t* proofs, PairSet& ps) {
   const uint64_t* flat = st->flat.data();
   const uint64_t* g = flat;
   const uint64_t* h = flat + 12;
   const uint64_t* hmask = flat + tpst_srs_flat_len(st->nv) - 24 * st->nv;
-  const uint64_t one[4] = {1, 0, 0, 0};
-  uint64_t minus1[4], negv[4];
-  fr_out(sub(Fr::zero(), Fr::one()), minus1);
+  uint64_t negv[4];
   fr_out(sub(Fr::zero(), fr_canon(v)), negv);
-  std::vector<uint64_t> g1s, g2s, pts, sc;
-  uint64_t q[24];
-  int rc;
-  push(pts, comm_h, 24);
-  push(sc, one, 4);
-  push(pts, h, 24);
-  push(sc, negv, 4);
-  if ((rc = small_msm<Fq2>(ctx, pts, sc, q))) return rc;
-  push(g1s, g, 12);
-  push(g2s, q, 24);
-  for (int i = 0; i < k; i++) {
-    pts.clear();
-    sc.clear();
-    push(pts, h, 24);
-    push(sc, pt + 4 * i, 4);
-    push(pts, hmask + 24 * (st->nv - k + i), 24);
-    push(sc, minus1, 4);
-    if ((rc = small_msm<Fq2>(ctx, pts, sc, q))) return rc;
-    push(g1s, proofs + 12 * i, 12);
-    push(g2s, q, 24);
-  }
-  uint64_t gt[72];
-  if ((rc = pairing_product(ctx, g1s, g2s, gt))) return rc;
-  return gt_is_one(gt) ? TPST_OK : TPST_E_VERIFY;
+  ps.g1.clear();
+  push(ps.g1, g, 12);
+  for (int i = 0; i < k; i++) push(ps.g1, proofs + 12 * i, 12);
+  ps.g2.assign((size_t)(k + 1) * 24, 0);
+  host::parallel_for((size_t)k + 1, [&](size_t i) {
+    if (i == 0)
+      host::mul_add<Fq2>(h, negv, comm_h, 1, &ps.g2[0]);  // C_h - h^v
+    else
+      host::mul_add<Fq2>(h, pt + 4 * (i - 1), hmask + 24 * (st->nv - k + i - 1), -1, &ps.g2[24 * i]);
+  });
+}
+
+static int mlpc_check_impl(tpst_ctx* ctx, SrsState* st, int k, const uint64_t* comm, const uint64_t* pt,
+                           const uint64_t* v, const uint64_t* proofs) {
+  PairSet ps;
+  mlpc_check_pairs(st, k, comm, pt, v, proofs, ps);
+  std::vector<uint64_t> gt;
+  if (int rc = pairing_groups(ctx, {&ps}, gt)) return rc;
+  return gt_is_one(gt.data()) ? TPST_OK : TPST_E_VERIFY;
+}
+
+static int mlpc_check2_impl(tpst_ctx* ctx, SrsState* st, int k, const uint64_t* comm_h, const uint64_t* pt,
+                            const uint64_t* v, const uint64_t* proofs) {
+  PairSet ps;
+  mlpc_check2_pairs(st, k, comm_h, pt, v, proofs, ps);
+  std::vector<uint64_t> gt;
+  if (int rc = pairing_groups(ctx, {&ps}, gt)) return rc;
+  return gt_is_one(gt.data()) ? TPST_OK : TPST_E_VERIFY;
 }
 
 // ------------------------------------------------- MultilinearPC calls ---
@@ -1879,24 +1860,32 @@ extern "C" int tpst_mlpc_check_2(tpst_ctx* ctx, int nv, const uint64_t* comm_h, 
 // Every proof element is validated before the transcript absorbs it (a
 // non-canonical encoding of a point would otherwise change the Fiat-Shamir
 // challenges without changing the point): Fq limbs < p, points on the curve
-// and in the r-torsion, GT coefficients < p, scalars < r.
+// and in the r-torsion (host threads), GT coefficients < p (GT membership of
+// comms_t is tested on the device with its exponentiation), scalars < r.
 static bool proof_valid(const tpst_open_proof* pr, int n, const uint64_t* point, const uint64_t* v,
                         const uint64_t* T) {
   for (int i = 0; i < n; i++)
     if (!fr_ok(point + 4 * i)) return false;
-  if (!fr_ok(v) || !gt_ok(T) || !point_valid<Fq>(pr->U) || !point_valid<Fq>(pr->final_a) ||
-      !point_valid<Fq2>(pr->final_h))
-    return false;
+  if (!fr_ok(v) || !gt_ok(T)) return false;
+  for (int i = 0; i < pr->m_col; i++)
+    if (!gt_ok(pr->comms_t[i][0]) || !gt_ok(pr->comms_t[i][1])) return false;
+  std::vector<const uint64_t*> g1 = {pr->U, pr->final_a}, g2 = {pr->final_h};
   for (int i = 0; i < pr->m_col; i++) {
-    if (!point_valid<Fq>(pr->comms_u[i][0]) || !point_valid<Fq>(pr->comms_u[i][1]) || !gt_ok(pr->comms_t[i][0]) ||
-        !gt_ok(pr->comms_t[i][1]) || !point_valid<Fq>(pr->pst_proof_h[i]))
-      return false;
+    g1.push_back(pr->comms_u[i][0]);
+    g1.push_back(pr->comms_u[i][1]);
+    g1.push_back(pr->pst_proof_h[i]);
   }
-  for (int i = 0; i < pr->m_row; i++)
-    if (!point_valid<Fq2>(pr->pst_proof[i])) return false;
-  return true;
+  for (int i = 0; i < pr->m_row; i++) g2.push_back(pr->pst_proof[i]);
+  std::atomic<bool> ok(true);
+  host::parallel_for(g1.size() + g2.size(), [&](size_t t) {
+    if (!ok.load(std::memory_order_relaxed)) return;
+    const bool good = t < g2.size() ? point_valid<Fq2>(g2[t]) : point_valid<Fq>(g1[t - g2.size()]);
+    if (!good) ok.store(false);
+  });
+  return ok.load();
 }
 
+// Polynomial::verify (sqrt_pst.rs:232-264) with MippProof::verify (mipp.rs:182-320)
 extern "C" int tpst_pst_verify(tpst_ctx* ctx, tpst_transcript* tr, int n, const uint64_t* point, const uint64_t* v,
                                const uint64_t* T, const tpst_open_proof* proof) {
   if (!ctx || !tr || !point || !v || !T || !proof) return fail(ctx, TPST_E_ARG, "null argument");
@@ -1916,7 +1905,6 @@ extern "C" int tpst_pst_verify(tpst_ctx* ctx, tpst_transcript* tr, int n, const 
   sp.absorb_bytes(b, 96);
   std::vector<Fr> xs(m), xs_inv(m);
   Fr final_y = Fr::one();
-  std::vector<uint64_t> exps;  // canonical exponents for the GT pows
   for (int i = 0; i < m; i++) {  // mipp.rs:207-227
     g1_bytes(proof->comms_u[i][0], b);
     sp.absorb_bytes(b, 96);
@@ -1944,31 +1932,17 @@ extern "C" int tpst_pst_verify(tpst_ctx* ctx, tpst_transcript* tr, int n, const 
     fr_out(x, c.data());
     return c;
   };
-  auto negc = [](const Fr& x) { return sub(Fr::zero(), x); };
-  int rc;
-  // U check: uc = U + sum(c_inv u_l + c u_r) == final_y * final_a
-  {
-    std::vector<uint64_t> pts, sc;
-    push(pts, proof->U, 12);
-    push(sc, canon4(Fr::one()).data(), 4);
-    for (int i = 0; i < m; i++) {
-      push(pts, proof->comms_u[i][0], 12);
-      push(sc, canon4(xs_inv[i]).data(), 4);
-      push(pts, proof->comms_u[i][1], 12);
-      push(sc, canon4(xs[i]).data(), 4);
-    }
-    push(pts, proof->final_a, 12);
-    push(sc, canon4(negc(final_y)).data(), 4);
-    uint64_t res[12];
-    if ((rc = small_msm<Fq>(ctx, pts, sc, res))) return rc;
-    for (int i = 0; i < 12; i++)
-      if (res[i]) return TPST_E_VERIFY;
-  }
-  // T check: T * prod t_l^{c_inv} t_r^{c} == e(final_a, final_h)
-  {
-    const size_t k = 2 * m;
+  // T check, device side first (side stream): t_l^{c_inv}, t_r^{c} for every
+  // round after a GT membership test of each (mipp.rs:263-283)
+  const size_t k = 2 * (size_t)m;
+  if (int rc = open_streams(ctx, 8, 0)) return rc;
+  hipStream_t s2 = ctx->side[0];
+  DevBuf db, de, dout, dok;
+  std::vector<Fq12> pw(k);
+  std::vector<uint32_t> okv(k);
+  if (k) {
     std::vector<uint32_t> bases;
-    std::vector<uint64_t> ex;
+    std::vector<uint64_t> dg(4 * k);
     for (int i = 0; i < m; i++) {
       for (int j = 0; j < 2; j++) {
         Fq12 f;
@@ -1976,73 +1950,82 @@ extern "C" int tpst_pst_verify(tpst_ctx* ctx, tpst_transcript* tr, int n, const 
         for (int q = 0; q < 12; q++) c[q] = fq_canon(proof->comms_t[i][j] + 6 * q);
         const uint32_t* fw = reinterpret_cast<const uint32_t*>(&f);
         bases.insert(bases.end(), fw, fw + sizeof(Fq12) / 4);
-        push(ex, canon4(j == 0 ? xs_inv[i] : xs[i]).data(), 4);
-      }
-    }
-    Fq12 acc;
-    {
-      Fq* c = reinterpret_cast<Fq*>(&acc);
-      for (int q = 0; q < 12; q++) c[q] = fq_canon(T + 6 * q);
-    }
-    if (k) {
-      // base-x digits of each exponent (e < r < x^4): GT pows by 4-way
-      // Frobenius splitting on the device, after a GT membership test
-      std::vector<uint64_t> dg(4 * k);
-      for (size_t j = 0; j < k; j++) {
-        uint64_t q[4];
-        memcpy(q, &ex[4 * j], 32);
+        // base-x digits of the exponent (e < r < x^4)
+        uint64_t q4[4];
+        fr_out(j == 0 ? xs_inv[i] : xs[i], q4);
         for (int t = 0; t < 4; t++) {
           unsigned __int128 rem = 0;
           for (int l = 3; l >= 0; l--) {
-            const unsigned __int128 cur = (rem << 64) | q[l];
-            q[l] = (uint64_t)(cur / params::BLS_X);
+            const unsigned __int128 cur = (rem << 64) | q4[l];
+            q4[l] = (uint64_t)(cur / params::BLS_X);
             rem = cur % params::BLS_X;
           }
-          dg[4 * j + t] = (uint64_t)rem;
+          dg[4 * (2 * i + j) + t] = (uint64_t)rem;
         }
       }
-      hipStream_t s = ctx->stream;
-      DevBuf db, de, dout, dok;
-      TPST_HIP(ctx, db.alloc(k * sizeof(Fq12)));
-      TPST_HIP(ctx, de.alloc(k * 32));
-      TPST_HIP(ctx, dout.alloc(k * sizeof(Fq12)));
-      TPST_HIP(ctx, dok.alloc(k * 4));
-      TPST_HIP(ctx, hipMemcpyAsync(db.p, bases.data(), k * sizeof(Fq12), hipMemcpyHostToDevice, s));
-      TPST_HIP(ctx, hipMemcpyAsync(de.p, dg.data(), k * 32, hipMemcpyHostToDevice, s));
-      TPST_HIP(ctx, gt_pow_wave(s, (const Fq12*)db.p, (const uint64_t*)de.p, k, (Fq12*)dout.p, dok.u()));
-      std::vector<Fq12> pw(k);
-      std::vector<uint32_t> okv(k);
-      TPST_HIP(ctx, hipMemcpyAsync(pw.data(), dout.p, k * sizeof(Fq12), hipMemcpyDeviceToHost, s));
-      TPST_HIP(ctx, hipMemcpyAsync(okv.data(), dok.p, k * 4, hipMemcpyDeviceToHost, s));
-      TPST_HIP(ctx, hipStreamSynchronize(s));
-      for (uint32_t o : okv)
-        if (!o) return fail(ctx, TPST_E_VERIFY, "comms_t element outside GT");
-      for (auto& x : pw) acc = mul(acc, x);
     }
-    uint64_t ft[72];
-    std::vector<uint64_t> a1(proof->final_a, proof->final_a + 12), a2(proof->final_h, proof->final_h + 24);
-    if ((rc = pairing_product(ctx, a1, a2, ft))) return rc;
+    TPST_HIP(ctx, db.alloc(k * sizeof(Fq12)));
+    TPST_HIP(ctx, de.alloc(k * 32));
+    TPST_HIP(ctx, dout.alloc(k * sizeof(Fq12)));
+    TPST_HIP(ctx, dok.alloc(k * 4));
+    TPST_HIP(ctx, hipMemcpyAsync(db.p, bases.data(), k * sizeof(Fq12), hipMemcpyHostToDevice, s2));
+    TPST_HIP(ctx, hipMemcpyAsync(de.p, dg.data(), k * 32, hipMemcpyHostToDevice, s2));
+    TPST_HIP(ctx, gt_pow_wave(s2, (const Fq12*)db.p, (const uint64_t*)de.p, k, (Fq12*)dout.p, dok.u()));
+    TPST_HIP(ctx, hipMemcpyAsync(pw.data(), dout.p, k * sizeof(Fq12), hipMemcpyDeviceToHost, s2));
+    TPST_HIP(ctx, hipMemcpyAsync(okv.data(), dok.p, k * 4, hipMemcpyDeviceToHost, s2));
+  }
+  // host threads meanwhile: the U check's terms and the check / check_2 pairs
+  // U check: uc = U + sum(c_inv u_l + c u_r) == final_y * final_a (mipp.rs:239-251)
+  std::vector<Xyzz<host::HFq>> terms(2 * (size_t)m + 1);
+  std::vector<std::vector<uint64_t>> tsc(2 * (size_t)m + 1);
+  for (int i = 0; i < m; i++) {
+    tsc[2 * i] = canon4(xs_inv[i]);
+    tsc[2 * i + 1] = canon4(xs[i]);
+  }
+  tsc[2 * m] = canon4(sub(Fr::zero(), final_y));
+  PairSet chk2, chk;
+  {
+    std::vector<uint64_t> rsc(4 * (size_t)m);
+    for (int i = 0; i < m; i++) fr_out(rs[i], &rsc[4 * i]);
+    uint64_t vhc[4];
+    fr_out(vh, vhc);
+    std::vector<uint64_t> arev(4 * (size_t)m_row);
+    for (int i = 0; i < m_row; i++) memcpy(&arev[4 * i], point + 4 * (m_row - 1 - i), 32);
+    host::parallel_for(terms.size(), [&](size_t t) {
+      const uint64_t* P = t == 2 * (size_t)m ? proof->final_a : proof->comms_u[t / 2][t % 2];
+      terms[t] = scalar_mul(host::aff_in<host::HFq>(P), reinterpret_cast<const uint32_t*>(tsc[t].data()), 253);
+    });
+    mlpc_check2_pairs(st, m, proof->final_h, rsc.data(), vhc, &proof->pst_proof_h[0][0], chk2);  // mipp.rs:307
+    mlpc_check_pairs(st, m_row, proof->U, arev.data(), v, &proof->pst_proof[0][0], chk);         // sqrt_pst.rs:261
+  }
+  Xyzz<host::HFq> uc = to_xyzz(host::aff_in<host::HFq>(proof->U));
+  for (auto& t : terms) uc = add(uc, t);
+  if (!is_inf(uc)) return TPST_E_VERIFY;
+  // the three pairing products in one launch: e(final_a, final_h), check_2, check
+  PairSet fin;
+  push(fin.g1, proof->final_a, 12);
+  push(fin.g2, proof->final_h, 24);
+  std::vector<uint64_t> gts;
+  if (int rc = pairing_groups(ctx, {&fin, &chk2, &chk}, gts)) return rc;
+  TPST_HIP(ctx, hipStreamSynchronize(s2));
+  for (uint32_t o : okv)
+    if (!o) return fail(ctx, TPST_E_VERIFY, "comms_t element outside GT");
+  // T * prod t_l^{c_inv} t_r^{c} == e(final_a, final_h)
+  Fq12 acc;
+  {
+    Fq* c = reinterpret_cast<Fq*>(&acc);
+    for (int q = 0; q < 12; q++) c[q] = fq_canon(T + 6 * q);
+  }
+  for (auto& x : pw) acc = mul(acc, x);
+  {
     const Fq* c = reinterpret_cast<const Fq*>(&acc);
     for (int q = 0; q < 12; q++) {
       uint64_t lim[6];
       fq_out(c[q], lim);
-      if (memcmp(lim, ft + 6 * q, 48) != 0) return TPST_E_VERIFY;
+      if (memcmp(lim, gts.data() + 6 * q, 48) != 0) return TPST_E_VERIFY;
     }
   }
-  // check_2 (mipp.rs:307) of final_h at rs with value vh
-  {
-    std::vector<uint64_t> rsc(4 * m);
-    for (int i = 0; i < m; i++) fr_out(rs[i], &rsc[4 * i]);
-    uint64_t vhc[4];
-    fr_out(vh, vhc);
-    if ((rc = mlpc_check2_impl(ctx, st, m, proof->final_h, rsc.data(), vhc, &proof->pst_proof_h[0][0]))) return rc;
-  }
-  // MultilinearPC::check of U at a_rev (sqrt_pst.rs:261)
-  {
-    std::vector<uint64_t> arev(4 * m_row);
-    for (int i = 0; i < m_row; i++) memcpy(&arev[4 * i], point + 4 * (m_row - 1 - i), 32);
-    if ((rc = mlpc_check_impl(ctx, st, m_row, proof->U, arev.data(), v, &proof->pst_proof[0][0]))) return rc;
-  }
+  if (!gt_is_one(gts.data() + 72) || !gt_is_one(gts.data() + 144)) return TPST_E_VERIFY;
   sp.store(tr);
   return TPST_OK;
 }
