@@ -110,15 +110,24 @@ __device__ int fe_exp_by_x(const wave::Eng& e, const wave::lds_t* prog, int src,
 
 // f (register F) -> f^(3(p^12-1)/r); returns the result register.  Same chain
 // as final_exponentiation() in pairing.h (eprint 2020/875).
-__device__ int fe_final_exp(const wave::Eng& e, const wave::lds_t* prog, int F, int regs, int I) {
+// ninv: the inverse of f's Fq-norm N(f) computed elsewhere in the workgroup
+// (k_chain_final's second wave), or nullptr to invert N(f) here on lane 0;
+// with ninv the function contains one __syncthreads (the hand-over).
+__device__ int fe_final_exp(const wave::Eng& e, const wave::lds_t* prog, int F, int regs, int I,
+                            const Fq* ninv = nullptr) {
   const int lane = threadIdx.x & 63;
 #define R(i) (regs + 12 * (i))
-  // f^-1 through the tower norms, one Fq inversion on lane 0
+  // f^-1 through the tower norms and one Fq inversion
   wave::run(e, prog + FE_SET.off[FE_INV1 + 0], F, 0, I + 0);        // t = c0^2 - v c1^2
   wave::run(e, prog + FE_SET.off[FE_INV1 + 1], I + 0, 0, I + 6);    // Fq6 adjugate c'
   wave::run(e, prog + FE_SET.off[FE_INV1 + 2], I + 6, I + 0, I + 12);  // Fq6 norm t'
   wave::run(e, prog + FE_SET.off[FE_INV1 + 3], I + 12, 0, I + 14);  // Fq2 norm n
-  if (lane == 0) wave::put_slot(e.lds, I + 15, inv(wave::get_slot(e.lds, I + 14)));
+  if (ninv) {
+    __syncthreads();
+    if (lane == 0) wave::put_slot(e.lds, I + 15, *ninv);
+  } else if (lane == 0) {
+    wave::put_slot(e.lds, I + 15, inv(wave::get_slot(e.lds, I + 14)));
+  }
   wave::wave_sync();
   wave::run(e, prog + FE_SET.off[FE_INV1 + 4], I + 12, I + 15, I + 16);  // t'^-1
   wave::run(e, prog + FE_SET.off[FE_INV1 + 5], I + 6, I + 16, I + 18);   // t^-1
@@ -323,14 +332,18 @@ __device__ __forceinline__ int dbl_idx(int b) {
 // one wave per (group, block): MB = prod_{b in block} M_b^(2^(b - lo))
 constexpr int BW = 4;
 constexpr int BW_SLOTS = 64 + 36;
-constexpr int BW_OPS[] = {wave::OP_F12_MUL, wave::OP_F12_SQR};
-constexpr wave::OpSet<2> BW_SET(BW_OPS);
+constexpr int BW_OPS[] = {wave::OP_F12_MUL, wave::OP_F12_SQR, wave::OP_INV1, wave::OP_INV2, wave::OP_INV3,
+                          wave::OP_INV4};
+constexpr wave::OpSet<6> BW_SET(BW_OPS);
 constexpr int BW_PROG = BW_SET.words;
 constexpr size_t BW_LDS = (size_t)(BW_PROG + (wave::N_CONSTS + BW * BW_SLOTS) * wave::SLOT) * 4;
 static_assert(BW_LDS <= 65536, "block-multiplier kernel LDS");
 
+// and MBn[o] = N(MB[o]), the Fq-norm of the block multiplier (the tower norms
+// of the final exponentiation's inversion, fe_final_exp), so that the chain
+// kernel can invert N(f) = prod_j N(MB_j)^(2^(LB j)) off its critical path
 __global__ void __launch_bounds__(64 * BW) k_miller_blocks(const Fq12* __restrict__ M, size_t groups,
-                                                           Fq12* __restrict__ MB) {
+                                                           Fq12* __restrict__ MB, Fq* __restrict__ MBn) {
   extern __shared__ uint4 smem4[];
   wave::lds_t* prog = (wave::lds_t*)(smem4);
   wave::lds_t* vals = prog + BW_PROG;
@@ -366,21 +379,48 @@ __global__ void __launch_bounds__(64 * BW) k_miller_blocks(const Fq12* __restric
     }
   }
   wave::store_f12(vals, acc, MB + o);
+  if (MBn) {
+    const int I = base + 76;  // in_r / tmp are free now: 15 slots of norm temporaries
+    wave::run(e, prog + BW_SET.off[2], acc, 0, I + 0);
+    wave::run(e, prog + BW_SET.off[3], I + 0, 0, I + 6);
+    wave::run(e, prog + BW_SET.off[4], I + 6, I + 0, I + 12);
+    wave::run(e, prog + BW_SET.off[5], I + 12, 0, I + 14);
+    if ((threadIdx.x & 63) == 0) MBn[o] = wave::get_slot(vals, I + 14);
+  }
 }
 
 // one wave per group: F = MB_top, F = F^(2^LB) MB_j, then (optionally) the
-// final exponentiation
+// final exponentiation.  A second wave meanwhile runs the same Horner on the
+// blocks' Fq-norms and inverts the result -- N(F)^-1, the one Fq inversion of
+// the final exponentiation (~0.18 ms on a lone lane) -- so the first wave
+// finds it ready instead of waiting for it.
 constexpr size_t CH_LDS = (size_t)(FW_PROG + (wave::N_CONSTS + FW_SLOTS + FE_SLOTS) * wave::SLOT) * 4;
 static_assert(CH_LDS <= 65536, "chain kernel LDS");
 
-__global__ void __launch_bounds__(64) k_chain_final(const Fq12* __restrict__ MB, Fq12* __restrict__ out, int do_final) {
+__global__ void __launch_bounds__(128) k_chain_final(const Fq12* __restrict__ MB, const Fq* __restrict__ MBn,
+                                                     Fq12* __restrict__ out, int do_final) {
   extern __shared__ uint4 smem4[];
+  __shared__ Fq ninv_sh;
   wave::lds_t* prog = (wave::lds_t*)(smem4);
   wave::lds_t* vals = prog + FW_PROG;
   wave::load_set(prog, FE_SET);
   wave::load_consts(vals, 0);
   __syncthreads();
   const size_t g = blockIdx.x;
+  if (threadIdx.x >= 64) {  // norm wave
+    if (!do_final) return;
+    if (threadIdx.x == 64) {
+      const Fq* nb = MBn + g * NBLK;
+      Fq n = nb[NBLK - 1];
+      for (int blk = NBLK - 2; blk >= 0; blk--) {
+        for (int i = 0; i < LB; i++) n = sqr(n);
+        n = mul(n, nb[blk]);
+      }
+      ninv_sh = inv(n);
+    }
+    __syncthreads();  // hand-over: pairs with the one inside fe_final_exp
+    return;
+  }
   const int base = wave::N_CONSTS;
   const wave::Eng e{vals, base, 0};
   int acc = base + 64, in_r = base + 76, tmp = base + 88;
@@ -404,7 +444,7 @@ __global__ void __launch_bounds__(64) k_chain_final(const Fq12* __restrict__ MB,
     return;
   }
   const int fe = wave::N_CONSTS + FW_SLOTS;
-  const int r = fe_final_exp(e, prog, acc, fe, fe + 120);
+  const int r = fe_final_exp(e, prog, acc, fe, fe + 120, &ninv_sh);
   wave::store_f12(vals, r, out + g);
 }
 
@@ -420,7 +460,7 @@ static size_t line_tree_len(size_t n) {  // tree levels over n pairs, chunk TREE
 size_t multi_pairing_scratch(size_t groups, size_t n) {
   const size_t G = groups * N_LINE_COEFFS;
   return Arena::need(G * (n ? n : 1), sizeof(Fq12)) + Arena::need(G * (line_tree_len(n) + 1), sizeof(Fq12)) +
-         Arena::need(groups * NBLK, sizeof(Fq12)) + 4096 + 256 * 16;
+         Arena::need(groups * NBLK, sizeof(Fq12)) + Arena::need(groups * NBLK, sizeof(Fq)) + 4096 + 256 * 16;
 }
 
 hipError_t multi_pairing_prepared(Arena& ar, hipStream_t s, const uint32_t* d_g1, const uint32_t* d_g2,
@@ -446,9 +486,10 @@ hipError_t multi_pairing_prepared(Arena& ar, hipStream_t s, const uint32_t* d_g1
     n = nout;
   }
   Fq12* MB = ar.take<Fq12>(groups * NBLK);
-  k_miller_blocks<<<grid_for(groups * NBLK, BW), 64 * BW, BW_LDS, s>>>(lines, groups, MB);
+  Fq* MBn = final_exp ? ar.take<Fq>(groups * NBLK) : nullptr;
+  k_miller_blocks<<<grid_for(groups * NBLK, BW), 64 * BW, BW_LDS, s>>>(lines, groups, MB, MBn);
   TPST_TRY(hipGetLastError());
-  k_chain_final<<<(unsigned)groups, 64, CH_LDS, s>>>(MB, d_out, final_exp ? 1 : 0);
+  k_chain_final<<<(unsigned)groups, 128, CH_LDS, s>>>(MB, MBn, d_out, final_exp ? 1 : 0);
   return hipGetLastError();
 }
 
