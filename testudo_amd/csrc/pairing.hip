@@ -463,20 +463,10 @@ size_t multi_pairing_scratch(size_t groups, size_t n) {
          Arena::need(groups * NBLK, sizeof(Fq12)) + Arena::need(groups * NBLK, sizeof(Fq)) + 4096 + 256 * 16;
 }
 
-hipError_t multi_pairing_prepared(Arena& ar, hipStream_t s, const uint32_t* d_g1, const uint32_t* d_g2,
-                                  const LineCoeff* d_coeffs, size_t groups, size_t n, Fq12* d_out, bool final_exp,
-                                  size_t map_s, size_t rot_L) {
-  if (!groups) return hipSuccess;
+// tree products of the lines, block multipliers, Horner chain (+ final exp)
+static hipError_t pairing_from_lines(Arena& ar, hipStream_t s, Fq12* lines, size_t groups, size_t n, Fq12* d_out,
+                                     bool final_exp) {
   const size_t G = groups * N_LINE_COEFFS;
-  Fq12* lines = ar.take<Fq12>(G * (n ? n : 1));
-  if (n) {
-    k_line_eval<<<grid_for(G * n, 64), 64, 0, s>>>(d_coeffs, d_g1, rot_L, d_g2, groups, n, map_s, lines);
-    TPST_TRY(hipGetLastError());
-  } else {
-    k_set_one<<<grid_for(G, 64), 64, 0, s>>>(lines, G);
-    TPST_TRY(hipGetLastError());
-    n = 1;
-  }
   while (n > 1) {
     const size_t nout = (n + TREE_CHUNK - 1) / TREE_CHUNK;
     Fq12* nxt = ar.take<Fq12>(G * nout);
@@ -491,6 +481,87 @@ hipError_t multi_pairing_prepared(Arena& ar, hipStream_t s, const uint32_t* d_g1
   TPST_TRY(hipGetLastError());
   k_chain_final<<<(unsigned)groups, 128, CH_LDS, s>>>(MB, MBn, d_out, final_exp ? 1 : 0);
   return hipGetLastError();
+}
+
+hipError_t multi_pairing_prepared(Arena& ar, hipStream_t s, const uint32_t* d_g1, const uint32_t* d_g2,
+                                  const LineCoeff* d_coeffs, size_t groups, size_t n, Fq12* d_out, bool final_exp,
+                                  size_t map_s, size_t rot_L) {
+  if (!groups) return hipSuccess;
+  const size_t G = groups * N_LINE_COEFFS;
+  Fq12* lines = ar.take<Fq12>(G * (n ? n : 1));
+  if (n) {
+    k_line_eval<<<grid_for(G * n, 64), 64, 0, s>>>(d_coeffs, d_g1, rot_L, d_g2, groups, n, map_s, lines);
+    TPST_TRY(hipGetLastError());
+  } else {
+    k_set_one<<<grid_for(G, 64), 64, 0, s>>>(lines, G);
+    TPST_TRY(hipGetLastError());
+    n = 1;
+  }
+  return pairing_from_lines(ar, s, lines, groups, n, d_out, final_exp);
+}
+
+// ---- MIPP look-ahead (pst_api.hip tpst_poly_open) --------------------------
+// The 8 pairing products of round-r vectors (a, h; len, s = len/2, s' = s/2)
+// whose combination with round r's challenge gives round r+1's cross terms:
+//   group  0 A0 (i, i+s')   1 A3 (i+s, i+s+s')   2 A1 (i, i+s+s')   3 A2 (i+s, i+s')
+//          4 B0 (i+s', i)   5 B3 (i+s+s', i+s)   6 B1 (i+s', i+s)   7 B2 (i+s+s', i)
+// (G1 index, G2 index) for i < s'.  x2: h = h_prev_L + c' h_prev_R is not
+// prepared; each pair (p, q) becomes (X[p], hprev[q]) and (X[len + p],
+// hprev[q + len]) with X = a || c' a (XYZZ, the MIPP fold's two sets).
+__constant__ uint32_t LA_P[8] = {0, 2, 0, 2, 1, 3, 1, 3};  // G1 offset in units of s'
+__constant__ uint32_t LA_Q[8] = {1, 3, 3, 1, 0, 2, 2, 0};  // G2 offset in units of s'
+
+__global__ void __launch_bounds__(64) k_line_eval_la(const LineCoeff* __restrict__ coeffs, size_t ncol,
+                                                     const uint32_t* __restrict__ g1, int xyzz,
+                                                     const uint32_t* __restrict__ g2, size_t sp, size_t len, int x2,
+                                                     Fq12* __restrict__ out) {
+  const size_t n = sp * (x2 ? 2 : 1);
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 8 * N_LINE_COEFFS * n) return;
+  const size_t k = t % n, gi = t / n, idx = gi % N_LINE_COEFFS, g = gi / N_LINE_COEFFS;
+  const size_t i = k % sp, half = k / sp;
+  const size_t p = LA_P[g] * sp + i + (half ? len : 0);
+  const size_t q = LA_Q[g] * sp + i + (half ? len : 0);
+  Fq12 r = Fq12::one();
+  if (!is_inf(load_affine<Fq2>(g2, q))) {
+    Fq px, py, lam;
+    bool inf;
+    if (xyzz) {
+      const Xyzz<Fq> P = load_xyzz(reinterpret_cast<const Xyzz<Fq>*>(g1), p);
+      inf = is_inf(P);
+      px = mul(P.X, P.ZZZ);
+      py = mul(P.Y, P.ZZ);
+      lam = mul(P.ZZ, P.ZZZ);
+    } else {
+      const G1A P = load_affine<Fq>(g1, p);
+      inf = is_inf(P);
+      px = P.x;
+      py = P.y;
+    }
+    if (!inf) {
+      const LineCoeff c = coeffs[idx * ncol + q];
+      r = Fq12{{mul_fq(c.c0, py), Fq2::zero(), Fq2::zero()},
+               {mul_fq(c.c1, px), xyzz ? mul_fq(c.c2, lam) : c.c2, Fq2::zero()}};
+    }
+  }
+  out[t] = r;
+}
+
+size_t mipp_lookahead_scratch(size_t sp, bool x2) {
+  const size_t n = sp * (x2 ? 2 : 1);
+  return Arena::need(8 * N_LINE_COEFFS * n, sizeof(Fq12)) + multi_pairing_scratch(8, n);
+}
+
+hipError_t mipp_lookahead(Arena& ar, hipStream_t s, const LineCoeff* d_coeffs, size_t ncol, const uint32_t* d_g2,
+                          const uint32_t* d_g1, bool xyzz, size_t len, bool x2, Fq12* d_out8) {
+  const size_t sp = len / 4;
+  if (!sp) return hipErrorInvalidValue;
+  const size_t n = sp * (x2 ? 2 : 1);
+  Fq12* lines = ar.take<Fq12>(8 * N_LINE_COEFFS * n);
+  k_line_eval_la<<<grid_for(8 * N_LINE_COEFFS * n, 64), 64, 0, s>>>(d_coeffs, ncol, d_g1, xyzz ? 1 : 0, d_g2, sp,
+                                                                      len, x2 ? 1 : 0, lines);
+  TPST_TRY(hipGetLastError());
+  return pairing_from_lines(ar, s, lines, 8, n, d_out8, true);
 }
 
 hipError_t gt_product_final(Arena& ar, hipStream_t s, const Fq12* d_partials, size_t groups, size_t n, Fq12* d_out) {
@@ -535,34 +606,44 @@ __device__ bool regs_equal(const wave::lds_t* lds, int a, int b) {
   return __all(same ? 1 : 0) != 0;
 }
 
+// mipp: the opening's look-ahead combination (pst_api.hip): wave i raises
+// base[MIPP_POW_SEL[i]] in place (out == base), no membership test (the bases
+// are final-exponentiation outputs)
+__constant__ uint32_t MIPP_POW_SEL[4] = {2, 3, 6, 7};
+
 __global__ void __launch_bounds__(64) k_gt_pow_wave(const Fq12* __restrict__ base, const uint64_t* __restrict__ digits,
-                                                    size_t n, Fq12* __restrict__ out, uint32_t* __restrict__ ok) {
+                                                    size_t n, Fq12* __restrict__ out, uint32_t* __restrict__ ok,
+                                                    int mipp) {
   extern __shared__ uint4 smem4[];
   wave::lds_t* prog = (wave::lds_t*)(smem4);
   wave::lds_t* vals = prog + FW_PROG;
   wave::load_set(prog, FE_SET);
   wave::load_consts(vals, 0);
   __syncthreads();
-  const size_t i = blockIdx.x;
-  if (i >= n) return;
+  if (blockIdx.x >= n) return;
+  const size_t i = mipp ? MIPP_POW_SEL[blockIdx.x] : blockIdx.x;
+  const uint64_t* d = digits + 4 * blockIdx.x;
   const wave::Eng e{vals, wave::N_CONSTS, 0};
 #define R(k) (wave::N_CONSTS + 64 + 12 * (k))
   const int ACC = R(16), TMP = R(17), X1 = R(18), X2 = R(19);
   const wave::lds_t* P = prog;
   wave::load_f12(vals, R(1), base + i);
-  // cyclotomic subgroup: f^(p^4) f == f^(p^2)
-  wave::run(e, P + FE_SET.off[FE_FROB2], R(1), 0, X1);
-  wave::run(e, P + FE_SET.off[FE_FROB2], X1, 0, X2);
-  wave::run(e, P + FE_SET.off[FE_MUL], X2, R(1), R(0));
-  bool good = regs_equal(vals, R(0), X1);
+  const bool check = ok != nullptr;
+  bool good = true;
+  if (check) {  // cyclotomic subgroup: f^(p^4) f == f^(p^2)
+    wave::run(e, P + FE_SET.off[FE_FROB2], R(1), 0, X1);
+    wave::run(e, P + FE_SET.off[FE_FROB2], X1, 0, X2);
+    wave::run(e, P + FE_SET.off[FE_MUL], X2, R(1), R(0));
+    good = regs_equal(vals, R(0), X1);
+  }
   // GT: f^p == f^x
   wave::run(e, P + FE_SET.off[FE_FROB1], R(1), 0, R(2));
-  if (good) {
+  if (check && good) {
     const int fx = fe_exp_by_x(e, P, R(1), X1, X2);
     good = regs_equal(vals, fx, R(2));
   }
   const int lane = threadIdx.x & 63;
-  if (lane == 0) ok[i] = good ? 1u : 0u;
+  if (check && lane == 0) ok[i] = good ? 1u : 0u;
   if (!good) return;
   // subset table T[m] = prod_{bit j of m} f^(p^j)
   wave::run(e, P + FE_SET.off[FE_FROB2], R(1), 0, R(4));
@@ -572,7 +653,6 @@ __global__ void __launch_bounds__(64) k_gt_pow_wave(const Fq12* __restrict__ bas
     const int hi = 1 << (31 - __builtin_clz(m));
     wave::run(e, P + FE_SET.off[FE_MUL], R(m - hi), R(hi), R(m));
   }
-  const uint64_t* d = digits + 4 * i;
   int acc = -1;
   for (int b = 63; b >= 0; b--) {
     if (acc >= 0) {
@@ -602,7 +682,14 @@ __global__ void __launch_bounds__(64) k_gt_pow_wave(const Fq12* __restrict__ bas
 hipError_t gt_pow_wave(hipStream_t s, const Fq12* d_base, const uint64_t* d_digits, size_t n, Fq12* d_out,
                        uint32_t* d_ok) {
   if (!n) return hipSuccess;
-  k_gt_pow_wave<<<(unsigned)n, 64, GP_LDS, s>>>(d_base, d_digits, n, d_out, d_ok);
+  k_gt_pow_wave<<<(unsigned)n, 64, GP_LDS, s>>>(d_base, d_digits, n, d_out, d_ok, 0);
+  return hipGetLastError();
+}
+
+hipError_t mipp_combine(hipStream_t s, Fq12* d_la8, const uint64_t* d_digits, Fq12* d_out2) {
+  k_gt_pow_wave<<<4, 64, GP_LDS, s>>>(d_la8, d_digits, 4, d_la8, nullptr, 1);
+  TPST_TRY(hipGetLastError());
+  k_f12_chunk_prod<<<1, 64 * RW, RW_LDS, s>>>(d_la8, 2, 4, 1, d_out2, 4);
   return hipGetLastError();
 }
 

@@ -48,6 +48,19 @@ hipError_t multi_pairing(Arena& ar, hipStream_t s, const uint32_t* d_g1, const u
 hipError_t gt_pow_wave(hipStream_t s, const Fq12* d_base, const uint64_t* d_digits, size_t n, Fq12* d_out,
                        uint32_t* d_ok);
 
+// MIPP look-ahead (tpst_poly_open): the 8 pairing products of round-r vectors
+// (pairing.hip, groups A0 A3 A1 A2 B0 B3 B1 B2) into d_out8 (Montgomery);
+// d_g1 affine (xyzz = false) or the fold's XYZZ sets a || c' a (xyzz = true,
+// with x2 = true: pairs against the previous round's prepared h, row length
+// ncol = 2 len).  Scratch: mipp_lookahead_scratch(len / 4, x2).
+size_t mipp_lookahead_scratch(size_t sp, bool x2);
+hipError_t mipp_lookahead(Arena& ar, hipStream_t s, const LineCoeff* d_coeffs, size_t ncol, const uint32_t* d_g2,
+                          const uint32_t* d_g1, bool xyzz, size_t len, bool x2, Fq12* d_out8);
+// round r+1's cross terms from the look-ahead products and c = c_r:
+// t_l = A0 A3 A1^(c^-1) A2^c, t_r = B0 B3 B1^(c^-1) B2^c.  d_digits: base-x
+// digits of (c^-1, c, c^-1, c) (4 x 4 u64); d_la8 is overwritten.
+hipError_t mipp_combine(hipStream_t s, Fq12* d_la8, const uint64_t* d_digits, Fq12* d_out2);
+
 hipError_t fq12_from_mont(hipStream_t s, const Fq12* d_in, uint32_t* d_out, size_t n);
 
 }  // namespace tpst

@@ -306,6 +306,21 @@ void g1_bytes(const uint64_t* p, uint8_t* b) {  // ark serialize Compress::No
 // host Fr helpers
 Fr fr_inv(const Fr& a) { return inv(a); }
 
+// base-x digits of a canonical Fr e (e < r < x^4): e = sum_j out[j] x^j, for
+// the GT exponentiations by Frobenius splitting (pairing.hip k_gt_pow_wave)
+void base_x_digits(const uint64_t* e, uint64_t* out) {
+  uint64_t q[4] = {e[0], e[1], e[2], e[3]};
+  for (int t = 0; t < 4; t++) {
+    unsigned __int128 rem = 0;
+    for (int l = 3; l >= 0; l--) {
+      const unsigned __int128 cur = (rem << 64) | q[l];
+      q[l] = (uint64_t)(cur / params::BLS_X);
+      rem = cur % params::BLS_X;
+    }
+    out[t] = (uint64_t)rem;
+  }
+}
+
 // ---- proof-element validation (the reference's elements are typed arkworks
 // values, validated when deserialized; here they arrive as raw limbs) ----
 bool limbs_lt(const uint64_t* a, const uint32_t* mod32, int n64) {
@@ -1246,7 +1261,7 @@ static int pst_open_fbt(tpst_ctx* ctx, SrsState* st, const uint32_t* table, int 
 static int open_streams(tpst_ctx* ctx, size_t n_events, size_t pinned_bytes) {
   int least = 0, greatest = 0;
   TPST_HIP(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
-  for (int i = 0; i < 2; i++)
+  for (int i = 0; i < 3; i++)
     if (!ctx->side[i]) TPST_HIP(ctx, hipStreamCreateWithPriority(&ctx->side[i], hipStreamNonBlocking, least));
   while (ctx->events.size() < n_events) {
     hipEvent_t e;
@@ -1267,21 +1282,32 @@ static int open_streams(tpst_ctx* ctx, size_t n_events, size_t pinned_bytes) {
 //
 // Critical path = the transcript: each MIPP round's challenge needs that
 // round's comms_u and comms_t, and the next round's folds need the challenge.
-// Per round r (len = C >> r, s = len / 2) the work is spread over 3 streams
-// (one hardware queue each; A at the highest priority):
-//   A (critical): a^(r) and c'a^(r) as ONE grouped table MSM over the original
-//     row commitments (two scalar sets W, c' W: a^(r)_i = sum_t W_t a_{i+t len},
-//     c' = the previous challenge inverse), then t_l, t_r against the PREVIOUS
-//     round's prepared h by bilinearity:
+// Per round r (len = C >> r, s = len / 2, s' = s / 2) the work is spread
+// over 4 streams (one hardware queue each; A at the highest priority):
+//   A (critical): t^(r) = (t_l, t_r).  Round 0 pairs the row commitments
+//     directly.  From round 1 on, t^(r) comes out of the LOOK-AHEAD of round
+//     r-1 (stream D): with a' = a_L + c a_R, h' = h_L + c^-1 h_R (mipp.rs:101-
+//     120) bilinearity splits round r's cross products into eight pairing
+//     products of round r-1's vectors that do not involve c = c_{r-1},
+//       t_l = A0 A3 A1^(c^-1) A2^c,  t_r = B0 B3 B1^(c^-1) B2^c
+//     (pairing.hip, mipp_lookahead), so once c is known the critical path is
+//     four GT exponentiations (base-x Frobenius splitting, ~0.7 ms) and two
+//     products instead of fold + Miller loops + final exponentiations
+//     (~3.3 ms); comms_t -> host.
+//   D: the look-ahead of round r for round r+1: a^(r) and c'a^(r) as ONE
+//     grouped table MSM over the original row commitments (scalar sets W,
+//     c'W: a^(r)_i = sum_t W_t a_{i+t len}, c' = the previous challenge
+//     inverse), then the 8 products against the PREVIOUS round's prepared h:
 //       e(a_i, h^(r)_k) = e(a_i, h^(r-1)_k) e(c' a_i, h^(r-1)_{k+len})
-//     -> Miller loops + the two final exponentiations; comms_t -> host.
+//     -> Miller loops + 8 final exponentiations, overlapping round r's own
+//     transcript work.
 //   B: y fold (compress_field, mipp.rs:124-136) and the cross MSMs u_l, u_r
 //     (mipp.rs:66-75) -> canonical -> host; in round 0 first U =
 //     MSM(comm_list, chi(b)) (sqrt_pst.rs:198) and after it the PST proof of
 //     q (sqrt_pst.rs:218-225), which needs nothing from the MIPP.
 //   C: in round 0 the fold table over comm_list (fbt.h); then h^(r) =
 //     sum_t Wi_t h_{i + t len} (table MSM over powers_of_h) -> affine ->
-//     G2Prepared, consumed by round r+1 (G2 preparation off the critical path).
+//     G2Prepared, consumed by the look-ahead of round r+1.
 // The host waits only for the round's comms (pinned staging), absorbs them
 // (mipp.rs:97-101) and squeezes the challenge; no stream is drained mid-open.
 extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, const uint64_t* comms,
@@ -1316,30 +1342,32 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   // ---- host staging layout (bytes): per-round uploads, final upload, downloads
   std::vector<size_t> up_off(m + 2);
   size_t off = 0;
-  for (int r = 0; r < m; r++) {  // W | c'W | Wi | c' (Fr)
+  for (int r = 0; r < m; r++) {  // W | c'W | Wi | c' (Fr) | base-x digits of (c^-1, c, c^-1, c)
     up_off[r] = off;
-    off += (3 * ((size_t)1 << r) + 1) * 32;
+    off += (3 * ((size_t)1 << r) + 1) * 32 + 128;
   }
   up_off[m] = off;  // final: W | Wi | evals | rs (Fr), a_rev (canonical Fr)
   off += (3 * C + m + k) * 32;
   const size_t up_bytes = off;
   const size_t dn_U = up_bytes, dn_round = dn_U + 96, dn_final = dn_round + (size_t)m * (192 + 1152);
   const size_t dn_bytes = 96 + (size_t)m * (192 + 1152) + 96 + 192 + (size_t)m * 96 + (size_t)k * 192;
-  const size_t n_ev = 8 + 4 * (size_t)m;
+  const size_t n_ev = 8 + 5 * (size_t)m;
   if (int rc = open_streams(ctx, n_ev, up_bytes + dn_bytes)) return rc;
   uint8_t* pin = (uint8_t*)ctx->pinned;
-  hipStream_t sA = ctx->stream, sB = ctx->side[0], sC = ctx->side[1];
-  Arena &arA = ctx->arena, &arB = ctx->arena_side[0], &arC = ctx->arena_side[1];
+  hipStream_t sA = ctx->stream, sB = ctx->side[0], sC = ctx->side[1], sD = ctx->side[2];
+  Arena &arA = ctx->arena, &arB = ctx->arena_side[0], &arC = ctx->arena_side[1], &arD = ctx->arena_side[2];
   hipEvent_t* ev = ctx->events.data();
   enum { EV_PRE, EV_TABLE, EV_U, EV_FINAL_UP, EV_B_DONE, EV_C_DONE, EV_D_DONE, EV_A_DONE };
-  auto ev_up = [&](int r) { return ev[8 + 4 * r]; };
-  auto ev_a = [&](int r) { return ev[8 + 4 * r + 1]; };
-  auto ev_b = [&](int r) { return ev[8 + 4 * r + 2]; };
-  auto ev_c = [&](int r) { return ev[8 + 4 * r + 3]; };
+  auto ev_up = [&](int r) { return ev[8 + 5 * r]; };
+  auto ev_a = [&](int r) { return ev[8 + 5 * r + 1]; };
+  auto ev_b = [&](int r) { return ev[8 + 5 * r + 2]; };
+  auto ev_c = [&](int r) { return ev[8 + 5 * r + 3]; };
+  auto ev_la = [&](int r) { return ev[8 + 5 * r + 4]; };
 
   // ---- device buffers (allocated before any stream runs: no hipFree mid-open)
   const size_t Ch = C > 1 ? C / 2 : 1;
-  DevBuf up, A, P, Y, chiC, ScA, ScB, ScC, xa, xb, xd, xh, xp, Hb[2], Lb[2], gts, canA, canB, canC, canD, pstA, pstB;
+  DevBuf up, A, P, Y, chiC, ScA, ScB, ScC, ScD, xa, xb, xd, xh, xp, xl, LAo[2], Hb[2], Lb[2], gts, canA, canB, canC,
+      canD, pstA, pstB;
   TPST_HIP(ctx, up.alloc(up_bytes));
   TPST_HIP(ctx, A.alloc(C * 96));
   TPST_HIP(ctx, P.alloc(C * 96));
@@ -1358,6 +1386,9 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     TPST_HIP(ctx, Lb[i].alloc(Ch * N_LINE_COEFFS * sizeof(LineCoeff)));
   }
   TPST_HIP(ctx, gts.alloc(2 * sizeof(Fq12)));
+  TPST_HIP(ctx, ScD.alloc(2 * C * 32));
+  TPST_HIP(ctx, xl.alloc(C * sizeof(Xyzz<Fq>)));
+  for (int i = 0; i < 2; i++) TPST_HIP(ctx, LAo[i].alloc(8 * sizeof(Fq12)));
   TPST_HIP(ctx, canA.alloc(2 * 576));
   TPST_HIP(ctx, canB.alloc(2 * 96));
   TPST_HIP(ctx, canC.alloc((size_t)(m + 1) * 192));
@@ -1384,7 +1415,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   TPST_HIP(ctx, hipMemcpyAsync(Y.p, p->chis.p, C * 32, hipMemcpyDeviceToDevice, sA));
   TPST_HIP(ctx, fr_from_mont(sA, p->chis.u(), chiC.u(), C));
   TPST_HIP(ctx, hipEventRecord(ev[EV_PRE], sA));
-  for (hipStream_t s2 : {sB, sC}) TPST_HIP(ctx, hipStreamWaitEvent(s2, ev[EV_PRE], 0));
+  for (hipStream_t s2 : {sB, sC, sD}) TPST_HIP(ctx, hipStreamWaitEvent(s2, ev[EV_PRE], 0));
 
   // ---- stream C (round 0): the fold table over comm_list
   TPST_HIP(ctx, fbt_build<Fq>(arC, sC, A.u(), C, st->t_A.u()));
@@ -1423,6 +1454,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   // a^(r)_i = sum_t W[t] a_{i + t len}, h^(r)_i = sum_t Wi[t] h_{i + t len}
   std::vector<Fr> W(1, Fr::one()), Wi(1, Fr::one()), xs_inv;
   Fr cprev = Fr::one();
+  uint64_t la_digits[16] = {};
   bool have_U = false;
   for (int r = 0; r < m; r++) {  // mipp.rs:58-120
     const size_t len = C >> r, s = len / 2, nW = (size_t)1 << r;
@@ -1435,48 +1467,60 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
       memcpy(stg + 32 * (2 * nW + t), Wi[t].v, 32);
     }
     memcpy(stg + 32 * 3 * nW, cprev.v, 32);
+    memcpy(stg + 32 * (3 * nW + 1), la_digits, 128);
     uint32_t* dW = dup(up_off[r]);
     uint32_t* dcW = dW + 8 * nW;
     uint32_t* dWi = dW + 16 * nW;
     uint32_t* dcp = dW + 24 * nW;
-    TPST_HIP(ctx, hipMemcpyAsync(dW, stg, (3 * nW + 1) * 32, hipMemcpyHostToDevice, sA));
+    const uint64_t* ddig = (const uint64_t*)(dW + 8 * (3 * nW + 1));
+    TPST_HIP(ctx, hipMemcpyAsync(dW, stg, (3 * nW + 1) * 32 + 128, hipMemcpyHostToDevice, sA));
     TPST_HIP(ctx, hipEventRecord(ev_up(r), sA));
 
-    // -- A: G1 side of t_l / t_r, Miller loops, final exponentiations
-    const uint32_t* g2 = H0;
-    const LineCoeff* lines = L0;
-    size_t H = 1;
-    if (r == 0) {
+    // -- A: t_l / t_r of this round
+    if (r == 0) {  // direct: the rotated comm_list (affine) against h^(0)
       TPST_HIP(ctx, affine_rot(sA, A.u(), P.u(), C, 24));
-    } else {
-      TPST_HIP(ctx, hipStreamWaitEvent(sA, ev[EV_TABLE], 0));
-      TPST_HIP(ctx, mipp_scalars(sA, dW, nullptr, len, 0, C, ScA.u()));
-      TPST_HIP(ctx, mipp_scalars(sA, dcW, nullptr, len, 0, C, ScA.u() + 8 * C));
-      FbGroups g;
-      g.groups = len;
-      g.members = C / len;
-      g.L = len;
-      g.D = 1;
-      g.sets = 2;
-      g.set_stride = C;
-      TPST_HIP(ctx, fbt_msm<Fq>(arA, sA, tA, ScA.u(), g, (Xyzz<Fq>*)xa.p));
-      H = 2;
-      if (r >= 2) {  // h^(r-1), prepared by stream C during round r-1
-        TPST_HIP(ctx, hipStreamWaitEvent(sA, ev_c(r - 1), 0));
-        g2 = Hb[(r - 1) & 1].u();
-        lines = (const LineCoeff*)Lb[(r - 1) & 1].p;
-      }
+      arA.reset();
+      TPST_HIP(ctx, arA.reserve(multi_pairing_scratch(2, s)));
+      TPST_HIP(ctx, multi_pairing_prepared(arA, sA, P.u(), H0, L0, 2, s, (Fq12*)gts.p, true, s, 0));
+    } else {  // round r-1's look-ahead products, combined with c_{r-1}
+      TPST_HIP(ctx, hipStreamWaitEvent(sA, ev_la(r - 1), 0));
+      TPST_HIP(ctx, mipp_combine(sA, (Fq12*)LAo[(r - 1) & 1].p, ddig, (Fq12*)gts.p));
     }
-    // G1 side: round 0 the rotated comm_list (affine); later rounds the XYZZ
-    // folds, rotated and line-scaled inside the pairing (no inversion)
-    arA.reset();
-    TPST_HIP(ctx, arA.reserve(multi_pairing_scratch(2, H * s)));
-    TPST_HIP(ctx, multi_pairing_prepared(arA, sA, r == 0 ? P.u() : xa.u(), g2, lines, 2, H * s, (Fq12*)gts.p, true,
-                                         s, r == 0 ? 0 : len));
     TPST_HIP(ctx, fq12_from_mont(sA, (Fq12*)gts.p, canA.u(), 2));
     uint8_t* dn_r = pin + dn_round + (size_t)r * (192 + 1152);
     TPST_HIP(ctx, hipMemcpyAsync(dn_r + 192, canA.p, 1152, hipMemcpyDeviceToHost, sA));
     TPST_HIP(ctx, hipEventRecord(ev_a(r), sA));
+
+    // -- D: look-ahead products of this round's vectors for round r+1
+    if (len >= 4) {
+      TPST_HIP(ctx, hipStreamWaitEvent(sD, ev_up(r), 0));
+      arD.reset();
+      TPST_HIP(ctx, arD.reserve(mipp_lookahead_scratch(len / 4, r > 0) + 4096));
+      if (r == 0) {  // a^(0) = comm_list (affine), h^(0) prepared
+        TPST_HIP(ctx, mipp_lookahead(arD, sD, L0, C, H0, A.u(), false, len, false, (Fq12*)LAo[0].p));
+      } else {
+        TPST_HIP(ctx, hipStreamWaitEvent(sD, ev[EV_TABLE], 0));
+        TPST_HIP(ctx, mipp_scalars(sD, dW, nullptr, len, 0, C, ScD.u()));
+        TPST_HIP(ctx, mipp_scalars(sD, dcW, nullptr, len, 0, C, ScD.u() + 8 * C));
+        FbGroups g;
+        g.groups = len;
+        g.members = C / len;
+        g.L = len;
+        g.D = 1;
+        g.sets = 2;
+        g.set_stride = C;
+        TPST_HIP(ctx, fbt_msm<Fq>(arD, sD, tA, ScD.u(), g, (Xyzz<Fq>*)xl.p));
+        const uint32_t* hp = H0;  // h^(r-1): h^(0) itself, or prepared by stream C in round r-1
+        const LineCoeff* lp = L0;
+        if (r >= 2) {
+          TPST_HIP(ctx, hipStreamWaitEvent(sD, ev_c(r - 1), 0));
+          hp = Hb[(r - 1) & 1].u();
+          lp = (const LineCoeff*)Lb[(r - 1) & 1].p;
+        }
+        TPST_HIP(ctx, mipp_lookahead(arD, sD, lp, 2 * len, hp, xl.u(), true, len, true, (Fq12*)LAo[r & 1].p));
+      }
+      TPST_HIP(ctx, hipEventRecord(ev_la(r), sD));
+    }
 
     // -- B: y fold by the previous challenge, cross MSMs u_l / u_r
     // (u_l = a[:s]^y[s:], u_r = a[s:]^y[:s], on the comm_list table)
@@ -1550,6 +1594,15 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     Wi.swap(Wi2);
     xs_inv.push_back(c_inv);
     cprev = c_inv;
+    // base-x digits of (c^-1, c, c^-1, c) for the next round's combination
+    {
+      uint64_t ci[4], cc[4];
+      fr_out(c_inv, ci);
+      fr_out(c, cc);
+      base_x_digits(ci, la_digits);
+      base_x_digits(cc, la_digits + 4);
+      memcpy(la_digits + 8, la_digits, 64);
+    }
   }
   if (!have_U) {
     TPST_HIP(ctx, hipEventSynchronize(ev[EV_U]));
@@ -1609,7 +1662,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
                                  sB));
   }
   TPST_HIP(ctx, hipEventRecord(ev[EV_B_DONE], sB));
-  for (hipStream_t s2 : {sA, sB, sC}) TPST_HIP(ctx, hipStreamSynchronize(s2));
+  for (hipStream_t s2 : {sA, sB, sC, sD}) TPST_HIP(ctx, hipStreamSynchronize(s2));
   memcpy(proof->final_a, pin + dn_final, 96);
   memcpy(proof->final_h, pin + dn_final + 96, 192);
   if (m > 0) memcpy(proof->pst_proof_h, pin + dn_final + 96 + 192, (size_t)m * 96);
@@ -1950,18 +2003,9 @@ extern "C" int tpst_pst_verify(tpst_ctx* ctx, tpst_transcript* tr, int n, const 
         for (int q = 0; q < 12; q++) c[q] = fq_canon(proof->comms_t[i][j] + 6 * q);
         const uint32_t* fw = reinterpret_cast<const uint32_t*>(&f);
         bases.insert(bases.end(), fw, fw + sizeof(Fq12) / 4);
-        // base-x digits of the exponent (e < r < x^4)
-        uint64_t q4[4];
-        fr_out(j == 0 ? xs_inv[i] : xs[i], q4);
-        for (int t = 0; t < 4; t++) {
-          unsigned __int128 rem = 0;
-          for (int l = 3; l >= 0; l--) {
-            const unsigned __int128 cur = (rem << 64) | q4[l];
-            q4[l] = (uint64_t)(cur / params::BLS_X);
-            rem = cur % params::BLS_X;
-          }
-          dg[4 * (2 * i + j) + t] = (uint64_t)rem;
-        }
+        uint64_t e4[4];  // base-x digits of the exponent (e < r < x^4)
+        fr_out(j == 0 ? xs_inv[i] : xs[i], e4);
+        base_x_digits(e4, &dg[4 * (2 * i + j)]);
       }
     }
     TPST_HIP(ctx, db.alloc(k * sizeof(Fq12)));

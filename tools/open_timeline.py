@@ -17,7 +17,7 @@ commits = [i for i, e in enumerate(ev) if "k_batch_sort" in e[2]]
 i0 = commits[-1]
 # the open starts at the first kernel after the commit's final exponentiation
 j = i0
-while j < len(ev) and "k_final_wave" not in ev[j][2]:
+while j < len(ev) and "k_final_wave" not in ev[j][2] and "k_chain_final" not in ev[j][2]:
     j += 1
 seg = ev[j + 1:]
 t0 = seg[0][0]
