@@ -505,23 +505,24 @@ hipError_t multi_pairing_prepared(Arena& ar, hipStream_t s, const uint32_t* d_g1
 // whose combination with round r's challenge gives round r+1's cross terms:
 //   group  0 A0 (i, i+s')   1 A3 (i+s, i+s+s')   2 A1 (i, i+s+s')   3 A2 (i+s, i+s')
 //          4 B0 (i+s', i)   5 B3 (i+s+s', i+s)   6 B1 (i+s', i+s)   7 B2 (i+s+s', i)
-// (G1 index, G2 index) for i < s'.  x2: h = h_prev_L + c' h_prev_R is not
-// prepared; each pair (p, q) becomes (X[p], hprev[q]) and (X[len + p],
-// hprev[q + len]) with X = a || c' a (XYZZ, the MIPP fold's two sets).
+// (G1 index, G2 index) for i < s'.  E > 1: h is not prepared but an earlier
+// round's h_prev is (row length E len), h_q = sum_j f_j h_prev[q + j len];
+// each pair (p, q) becomes the E pairs (X[p + j len], h_prev[q + j len]) with
+// X = the E fold sets f_j a (XYZZ).
 __constant__ uint32_t LA_P[8] = {0, 2, 0, 2, 1, 3, 1, 3};  // G1 offset in units of s'
 __constant__ uint32_t LA_Q[8] = {1, 3, 3, 1, 0, 2, 2, 0};  // G2 offset in units of s'
 
 __global__ void __launch_bounds__(64) k_line_eval_la(const LineCoeff* __restrict__ coeffs, size_t ncol,
                                                      const uint32_t* __restrict__ g1, int xyzz,
-                                                     const uint32_t* __restrict__ g2, size_t sp, size_t len, int x2,
+                                                     const uint32_t* __restrict__ g2, size_t sp, size_t len, int E,
                                                      Fq12* __restrict__ out) {
-  const size_t n = sp * (x2 ? 2 : 1);
+  const size_t n = sp * (size_t)E;
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= 8 * N_LINE_COEFFS * n) return;
   const size_t k = t % n, gi = t / n, idx = gi % N_LINE_COEFFS, g = gi / N_LINE_COEFFS;
-  const size_t i = k % sp, half = k / sp;
-  const size_t p = LA_P[g] * sp + i + (half ? len : 0);
-  const size_t q = LA_Q[g] * sp + i + (half ? len : 0);
+  const size_t i = k % sp, j = k / sp;
+  const size_t p = LA_P[g] * sp + i + j * len;
+  const size_t q = LA_Q[g] * sp + i + j * len;
   Fq12 r = Fq12::one();
   if (!is_inf(load_affine<Fq2>(g2, q))) {
     Fq px, py, lam;
@@ -547,19 +548,19 @@ __global__ void __launch_bounds__(64) k_line_eval_la(const LineCoeff* __restrict
   out[t] = r;
 }
 
-size_t mipp_lookahead_scratch(size_t sp, bool x2) {
-  const size_t n = sp * (x2 ? 2 : 1);
+size_t mipp_lookahead_scratch(size_t sp, int E) {
+  const size_t n = sp * (size_t)E;
   return Arena::need(8 * N_LINE_COEFFS * n, sizeof(Fq12)) + multi_pairing_scratch(8, n);
 }
 
 hipError_t mipp_lookahead(Arena& ar, hipStream_t s, const LineCoeff* d_coeffs, size_t ncol, const uint32_t* d_g2,
-                          const uint32_t* d_g1, bool xyzz, size_t len, bool x2, Fq12* d_out8) {
+                          const uint32_t* d_g1, bool xyzz, size_t len, int E, Fq12* d_out8) {
   const size_t sp = len / 4;
-  if (!sp) return hipErrorInvalidValue;
-  const size_t n = sp * (x2 ? 2 : 1);
+  if (!sp || (E != 1 && E != 2 && E != 4) || ncol < (size_t)E * len) return hipErrorInvalidValue;
+  const size_t n = sp * (size_t)E;
   Fq12* lines = ar.take<Fq12>(8 * N_LINE_COEFFS * n);
   k_line_eval_la<<<grid_for(8 * N_LINE_COEFFS * n, 64), 64, 0, s>>>(d_coeffs, ncol, d_g1, xyzz ? 1 : 0, d_g2, sp,
-                                                                      len, x2 ? 1 : 0, lines);
+                                                                      len, E, lines);
   TPST_TRY(hipGetLastError());
   return pairing_from_lines(ar, s, lines, 8, n, d_out8, true);
 }

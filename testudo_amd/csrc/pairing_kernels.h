@@ -50,12 +50,12 @@ hipError_t gt_pow_wave(hipStream_t s, const Fq12* d_base, const uint64_t* d_digi
 
 // MIPP look-ahead (tpst_poly_open): the 8 pairing products of round-r vectors
 // (pairing.hip, groups A0 A3 A1 A2 B0 B3 B1 B2) into d_out8 (Montgomery);
-// d_g1 affine (xyzz = false) or the fold's XYZZ sets a || c' a (xyzz = true,
-// with x2 = true: pairs against the previous round's prepared h, row length
-// ncol = 2 len).  Scratch: mipp_lookahead_scratch(len / 4, x2).
-size_t mipp_lookahead_scratch(size_t sp, bool x2);
+// d_g1 affine (xyzz = false, E = 1) or the fold's E XYZZ sets f_j a (xyzz =
+// true), paired against an earlier round's prepared h of row length
+// ncol = E len (E = 1, 2, 4).  Scratch: mipp_lookahead_scratch(len / 4, E).
+size_t mipp_lookahead_scratch(size_t sp, int E);
 hipError_t mipp_lookahead(Arena& ar, hipStream_t s, const LineCoeff* d_coeffs, size_t ncol, const uint32_t* d_g2,
-                          const uint32_t* d_g1, bool xyzz, size_t len, bool x2, Fq12* d_out8);
+                          const uint32_t* d_g1, bool xyzz, size_t len, int E, Fq12* d_out8);
 // round r+1's cross terms from the look-ahead products and c = c_r:
 // t_l = A0 A3 A1^(c^-1) A2^c, t_r = B0 B3 B1^(c^-1) B2^c.  d_digits: base-x
 // digits of (c^-1, c, c^-1, c) (4 x 4 u64); d_la8 is overwritten.

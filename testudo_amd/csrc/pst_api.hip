@@ -1342,9 +1342,9 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   // ---- host staging layout (bytes): per-round uploads, final upload, downloads
   std::vector<size_t> up_off(m + 2);
   size_t off = 0;
-  for (int r = 0; r < m; r++) {  // W | c'W | Wi | c' (Fr) | base-x digits of (c^-1, c, c^-1, c)
+  for (int r = 0; r < m; r++) {  // W | c'W | Wi | c' | f2 W | f3 W (Fr) | base-x digits of (c^-1, c, c^-1, c)
     up_off[r] = off;
-    off += (3 * ((size_t)1 << r) + 1) * 32 + 128;
+    off += (5 * ((size_t)1 << r) + 1) * 32 + 128;
   }
   up_off[m] = off;  // final: W | Wi | evals | rs (Fr), a_rev (canonical Fr)
   off += (3 * C + m + k) * 32;
@@ -1354,8 +1354,13 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   const size_t n_ev = 8 + 5 * (size_t)m;
   if (int rc = open_streams(ctx, n_ev, up_bytes + dn_bytes)) return rc;
   uint8_t* pin = (uint8_t*)ctx->pinned;
-  hipStream_t sA = ctx->stream, sB = ctx->side[0], sC = ctx->side[1], sD = ctx->side[2];
-  Arena &arA = ctx->arena, &arB = ctx->arena_side[0], &arC = ctx->arena_side[1], &arD = ctx->arena_side[2];
+  // four hardware queues: A (critical), B (cross terms, then the h folds of
+  // "C"), and two look-ahead streams for alternating rounds -- consecutive
+  // look-aheads overlap, each taking longer than a round
+  hipStream_t sA = ctx->stream, sB = ctx->side[0], sC = ctx->side[0];
+  hipStream_t sLA[2] = {ctx->side[1], ctx->side[2]};
+  Arena &arA = ctx->arena, &arB = ctx->arena_side[0], &arC = ctx->arena2;
+  Arena* arLA[2] = {&ctx->arena_side[1], &ctx->arena_side[2]};
   hipEvent_t* ev = ctx->events.data();
   enum { EV_PRE, EV_TABLE, EV_U, EV_FINAL_UP, EV_B_DONE, EV_C_DONE, EV_D_DONE, EV_A_DONE };
   auto ev_up = [&](int r) { return ev[8 + 5 * r]; };
@@ -1366,8 +1371,8 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
 
   // ---- device buffers (allocated before any stream runs: no hipFree mid-open)
   const size_t Ch = C > 1 ? C / 2 : 1;
-  DevBuf up, A, P, Y, chiC, ScA, ScB, ScC, ScD, xa, xb, xd, xh, xp, xl, LAo[2], Hb[2], Lb[2], gts, canA, canB, canC,
-      canD, pstA, pstB;
+  DevBuf up, A, P, Y, chiC, ScA, ScB, ScC, ScD[2], xa, xb, xd, xh, xp, xl[2], LAo[2], Hb[4], Lb[4], gts, canA, canB,
+      canC, canD, pstA, pstB;
   TPST_HIP(ctx, up.alloc(up_bytes));
   TPST_HIP(ctx, A.alloc(C * 96));
   TPST_HIP(ctx, P.alloc(C * 96));
@@ -1381,14 +1386,16 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   TPST_HIP(ctx, xd.alloc((k + 1) * sizeof(Xyzz<Fq2>)));
   TPST_HIP(ctx, xh.alloc(C * sizeof(Xyzz<Fq2>)));
   TPST_HIP(ctx, xp.alloc(((size_t)m + 1) * sizeof(Xyzz<Fq>)));
-  for (int i = 0; i < 2; i++) {
+  for (int i = 0; i < 4; i++) {
     TPST_HIP(ctx, Hb[i].alloc(Ch * 192));
     TPST_HIP(ctx, Lb[i].alloc(Ch * N_LINE_COEFFS * sizeof(LineCoeff)));
   }
   TPST_HIP(ctx, gts.alloc(2 * sizeof(Fq12)));
-  TPST_HIP(ctx, ScD.alloc(2 * C * 32));
-  TPST_HIP(ctx, xl.alloc(C * sizeof(Xyzz<Fq>)));
-  for (int i = 0; i < 2; i++) TPST_HIP(ctx, LAo[i].alloc(8 * sizeof(Fq12)));
+  for (int i = 0; i < 2; i++) {
+    TPST_HIP(ctx, ScD[i].alloc(4 * C * 32));
+    TPST_HIP(ctx, xl[i].alloc(C * sizeof(Xyzz<Fq>)));
+    TPST_HIP(ctx, LAo[i].alloc(8 * sizeof(Fq12)));
+  }
   TPST_HIP(ctx, canA.alloc(2 * 576));
   TPST_HIP(ctx, canB.alloc(2 * 96));
   TPST_HIP(ctx, canC.alloc((size_t)(m + 1) * 192));
@@ -1415,22 +1422,22 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   TPST_HIP(ctx, hipMemcpyAsync(Y.p, p->chis.p, C * 32, hipMemcpyDeviceToDevice, sA));
   TPST_HIP(ctx, fr_from_mont(sA, p->chis.u(), chiC.u(), C));
   TPST_HIP(ctx, hipEventRecord(ev[EV_PRE], sA));
-  for (hipStream_t s2 : {sB, sC, sD}) TPST_HIP(ctx, hipStreamWaitEvent(s2, ev[EV_PRE], 0));
+  for (hipStream_t s2 : {sB, sLA[0], sLA[1]}) TPST_HIP(ctx, hipStreamWaitEvent(s2, ev[EV_PRE], 0));
 
-  // ---- stream C (round 0): the fold table over comm_list
-  TPST_HIP(ctx, fbt_build<Fq>(arC, sC, A.u(), C, st->t_A.u()));
-  TPST_HIP(ctx, hipEventRecord(ev[EV_TABLE], sC));
-  // ---- stream B: U = MSM(comm_list, chi(b)) on that table (or the c_u the
-  // ranks combined, for an opening-only handle)
-  TPST_HIP(ctx, hipStreamWaitEvent(sB, ev[EV_TABLE], 0));
+  // ---- look-ahead stream 1 (idle until round 1): the fold table over comm_list
+  TPST_HIP(ctx, fbt_build<Fq>(*arLA[1], sLA[1], A.u(), C, st->t_A.u()));
+  TPST_HIP(ctx, hipEventRecord(ev[EV_TABLE], sLA[1]));
+  // ---- stream B: U = MSM(comm_list, chi(b)) on that table, or the c_u the
+  // ranks combined for an opening-only handle
   if (p->has_u) {
     memcpy(pin + dn_U, p->U, 96);
     TPST_HIP(ctx, hipEventRecord(ev[EV_U], sB));
   } else {
-    FbGroups g;
-    g.members = C;
-    g.L = g.D = C;
-    TPST_HIP(ctx, fbt_msm<Fq>(arB, sB, tA, chiC.u(), g, (Xyzz<Fq>*)xd.p));
+    TPST_HIP(ctx, hipStreamWaitEvent(sB, ev[EV_TABLE], 0));
+    FbGroups gu;
+    gu.members = C;
+    gu.L = gu.D = C;
+    TPST_HIP(ctx, fbt_msm<Fq>(arB, sB, tA, chiC.u(), gu, (Xyzz<Fq>*)xd.p));
     TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(sB, (Xyzz<Fq>*)xd.p, canD.u(), 1));
     TPST_HIP(ctx, hipMemcpyAsync(pin + dn_U, canD.p, 96, hipMemcpyDeviceToHost, sB));
     TPST_HIP(ctx, hipEventRecord(ev[EV_U], sB));
@@ -1460,20 +1467,26 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     const size_t len = C >> r, s = len / 2, nW = (size_t)1 << r;
     // stage W | c'W | Wi | c' and upload once (stream A); B and C wait on it
     uint8_t* stg = pin + up_off[r];
+    // look-ahead fold factors for h^(r) over h^(r-2): f2 = c'_{r-2}, f3 = c'_{r-1} c'_{r-2}
+    const Fr f2 = r >= 2 ? xs_inv[r - 2] : Fr::one(), f3 = mul(cprev, f2);
     for (size_t t = 0; t < nW; t++) {
-      const Fr cw = mul(W[t], cprev);
+      const Fr cw = mul(W[t], cprev), w2 = mul(W[t], f2), w3 = mul(W[t], f3);
       memcpy(stg + 32 * t, W[t].v, 32);
       memcpy(stg + 32 * (nW + t), cw.v, 32);
       memcpy(stg + 32 * (2 * nW + t), Wi[t].v, 32);
+      memcpy(stg + 32 * (3 * nW + 1 + t), w2.v, 32);
+      memcpy(stg + 32 * (4 * nW + 1 + t), w3.v, 32);
     }
     memcpy(stg + 32 * 3 * nW, cprev.v, 32);
-    memcpy(stg + 32 * (3 * nW + 1), la_digits, 128);
+    memcpy(stg + 32 * (5 * nW + 1), la_digits, 128);
     uint32_t* dW = dup(up_off[r]);
     uint32_t* dcW = dW + 8 * nW;
     uint32_t* dWi = dW + 16 * nW;
     uint32_t* dcp = dW + 24 * nW;
-    const uint64_t* ddig = (const uint64_t*)(dW + 8 * (3 * nW + 1));
-    TPST_HIP(ctx, hipMemcpyAsync(dW, stg, (3 * nW + 1) * 32 + 128, hipMemcpyHostToDevice, sA));
+    uint32_t* dW2 = dW + 8 * (3 * nW + 1);
+    uint32_t* dW3 = dW + 8 * (4 * nW + 1);
+    const uint64_t* ddig = (const uint64_t*)(dW + 8 * (5 * nW + 1));
+    TPST_HIP(ctx, hipMemcpyAsync(dW, stg, (5 * nW + 1) * 32 + 128, hipMemcpyHostToDevice, sA));
     TPST_HIP(ctx, hipEventRecord(ev_up(r), sA));
 
     // -- A: t_l / t_r of this round
@@ -1493,31 +1506,38 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
 
     // -- D: look-ahead products of this round's vectors for round r+1
     if (len >= 4) {
+      hipStream_t sD = sLA[r & 1];
+      Arena& arD = *arLA[r & 1];
       TPST_HIP(ctx, hipStreamWaitEvent(sD, ev_up(r), 0));
       arD.reset();
-      TPST_HIP(ctx, arD.reserve(mipp_lookahead_scratch(len / 4, r > 0) + 4096));
+      const int E = r == 0 ? 1 : r == 1 ? 2 : 4;  // h^(r) over h^(0) / h^(0) / h^(r-2)
+      TPST_HIP(ctx, arD.reserve(mipp_lookahead_scratch(len / 4, E) + 4096));
       if (r == 0) {  // a^(0) = comm_list (affine), h^(0) prepared
-        TPST_HIP(ctx, mipp_lookahead(arD, sD, L0, C, H0, A.u(), false, len, false, (Fq12*)LAo[0].p));
+        TPST_HIP(ctx, mipp_lookahead(arD, sD, L0, C, H0, A.u(), false, len, 1, (Fq12*)LAo[0].p));
       } else {
+        // E fold sets f_j a^(r) (f = 1, c'_{r-1}, c'_{r-2}, c'_{r-1} c'_{r-2}):
+        // h^(r)_q = sum_j f_j h^(r-E/2 ...)[q + j len]
         TPST_HIP(ctx, hipStreamWaitEvent(sD, ev[EV_TABLE], 0));
-        TPST_HIP(ctx, mipp_scalars(sD, dW, nullptr, len, 0, C, ScD.u()));
-        TPST_HIP(ctx, mipp_scalars(sD, dcW, nullptr, len, 0, C, ScD.u() + 8 * C));
+        uint32_t* sc = ScD[r & 1].u();
+        const uint32_t* wsets[4] = {dW, dcW, dW2, dW3};
+        for (int j = 0; j < E; j++) TPST_HIP(ctx, mipp_scalars(sD, wsets[j], nullptr, len, 0, C, sc + 8 * C * j));
         FbGroups g;
         g.groups = len;
         g.members = C / len;
         g.L = len;
         g.D = 1;
-        g.sets = 2;
+        g.sets = (size_t)E;
         g.set_stride = C;
-        TPST_HIP(ctx, fbt_msm<Fq>(arD, sD, tA, ScD.u(), g, (Xyzz<Fq>*)xl.p));
-        const uint32_t* hp = H0;  // h^(r-1): h^(0) itself, or prepared by stream C in round r-1
+        TPST_HIP(ctx, fbt_msm<Fq>(arD, sD, tA, sc, g, (Xyzz<Fq>*)xl[r & 1].p));
+        const uint32_t* hp = H0;  // h^(0), or h^(r-2) prepared by stream C in round r-2
         const LineCoeff* lp = L0;
-        if (r >= 2) {
-          TPST_HIP(ctx, hipStreamWaitEvent(sD, ev_c(r - 1), 0));
-          hp = Hb[(r - 1) & 1].u();
-          lp = (const LineCoeff*)Lb[(r - 1) & 1].p;
+        if (r >= 3) {
+          TPST_HIP(ctx, hipStreamWaitEvent(sD, ev_c(r - 2), 0));
+          hp = Hb[(r - 2) % 4].u();
+          lp = (const LineCoeff*)Lb[(r - 2) % 4].p;
         }
-        TPST_HIP(ctx, mipp_lookahead(arD, sD, lp, 2 * len, hp, xl.u(), true, len, true, (Fq12*)LAo[r & 1].p));
+        TPST_HIP(ctx, mipp_lookahead(arD, sD, lp, (size_t)E * len, hp, xl[r & 1].u(), true, len, E,
+                                     (Fq12*)LAo[r & 1].p));
       }
       TPST_HIP(ctx, hipEventRecord(ev_la(r), sD));
     }
@@ -1526,8 +1546,9 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     // (u_l = a[:s]^y[s:], u_r = a[s:]^y[:s], on the comm_list table)
     TPST_HIP(ctx, hipStreamWaitEvent(sB, ev_up(r), 0));
     if (r > 0) TPST_HIP(ctx, compress_fr(sB, Y.u(), len, dcp));  // y_l + c' y_r (mipp.rs:124-136)
+    TPST_HIP(ctx, mipp_scalars(sB, dW, Y.u(), len, s, C, ScB.u()));
     {
-      TPST_HIP(ctx, mipp_scalars(sB, dW, Y.u(), len, s, C, ScB.u()));
+      TPST_HIP(ctx, hipStreamWaitEvent(sB, ev[EV_TABLE], 0));
       FbGroups g;
       g.groups = 2;
       g.members = C / len * s;
@@ -1542,8 +1563,9 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
       if (int rc = pst_q()) return rc;
 
     // -- C: h^(r) for round r+1 (r >= 1; round 1 pairs against h^(0) itself)
-    if (r >= 1 && r + 1 < m) {
+    if (r >= 1 && r + 4 <= m) {  // h^(r) for the look-ahead of round r+2
       TPST_HIP(ctx, hipStreamWaitEvent(sC, ev_up(r), 0));
+      if (r - 2 >= 3) TPST_HIP(ctx, hipStreamWaitEvent(sC, ev_la(r - 2), 0));  // the last reader of slot r % 4
       TPST_HIP(ctx, mipp_scalars(sC, dWi, nullptr, len, 0, C, ScC.u()));
       FbGroups g;
       g.groups = len;
@@ -1551,8 +1573,8 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
       g.L = len;
       g.D = 1;
       TPST_HIP(ctx, fbt_msm<Fq2>(arC, sC, tH, ScC.u(), g, (Xyzz<Fq2>*)xh.p));
-      TPST_HIP(ctx, xyzz_to_affine_mont<Fq2>(sC, (Xyzz<Fq2>*)xh.p, Hb[r & 1].u(), len));
-      TPST_HIP(ctx, g2_prepare_batch(sC, Hb[r & 1].u(), len, (LineCoeff*)Lb[r & 1].p));
+      TPST_HIP(ctx, xyzz_to_affine_mont<Fq2>(sC, (Xyzz<Fq2>*)xh.p, Hb[r % 4].u(), len));
+      TPST_HIP(ctx, g2_prepare_batch(sC, Hb[r % 4].u(), len, (LineCoeff*)Lb[r % 4].p));
       TPST_HIP(ctx, hipEventRecord(ev_c(r), sC));
     }
 
@@ -1662,7 +1684,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
                                  sB));
   }
   TPST_HIP(ctx, hipEventRecord(ev[EV_B_DONE], sB));
-  for (hipStream_t s2 : {sA, sB, sC, sD}) TPST_HIP(ctx, hipStreamSynchronize(s2));
+  for (hipStream_t s2 : {sA, sB, sLA[0], sLA[1]}) TPST_HIP(ctx, hipStreamSynchronize(s2));
   memcpy(proof->final_a, pin + dn_final, 96);
   memcpy(proof->final_h, pin + dn_final + 96, 192);
   if (m > 0) memcpy(proof->pst_proof_h, pin + dn_final + 96 + 192, (size_t)m * 96);
