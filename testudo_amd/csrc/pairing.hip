@@ -556,7 +556,7 @@ size_t mipp_lookahead_scratch(size_t sp, int E) {
 hipError_t mipp_lookahead(Arena& ar, hipStream_t s, const LineCoeff* d_coeffs, size_t ncol, const uint32_t* d_g2,
                           const uint32_t* d_g1, bool xyzz, size_t len, int E, Fq12* d_out8) {
   const size_t sp = len / 4;
-  if (!sp || (E != 1 && E != 2 && E != 4) || ncol < (size_t)E * len) return hipErrorInvalidValue;
+  if (!sp || E < 1 || E > 8 || (E & (E - 1)) || ncol < (size_t)E * len) return hipErrorInvalidValue;
   const size_t n = sp * (size_t)E;
   Fq12* lines = ar.take<Fq12>(8 * N_LINE_COEFFS * n);
   k_line_eval_la<<<grid_for(8 * N_LINE_COEFFS * n, 64), 64, 0, s>>>(d_coeffs, ncol, d_g1, xyzz ? 1 : 0, d_g2, sp,

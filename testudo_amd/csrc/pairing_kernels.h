@@ -52,7 +52,7 @@ hipError_t gt_pow_wave(hipStream_t s, const Fq12* d_base, const uint64_t* d_digi
 // (pairing.hip, groups A0 A3 A1 A2 B0 B3 B1 B2) into d_out8 (Montgomery);
 // d_g1 affine (xyzz = false, E = 1) or the fold's E XYZZ sets f_j a (xyzz =
 // true), paired against an earlier round's prepared h of row length
-// ncol = E len (E = 1, 2, 4).  Scratch: mipp_lookahead_scratch(len / 4, E).
+// ncol = E len (E = 1, 2, 4, 8).  Scratch: mipp_lookahead_scratch(len / 4, E).
 size_t mipp_lookahead_scratch(size_t sp, int E);
 hipError_t mipp_lookahead(Arena& ar, hipStream_t s, const LineCoeff* d_coeffs, size_t ncol, const uint32_t* d_g2,
                           const uint32_t* d_g1, bool xyzz, size_t len, int E, Fq12* d_out8);

@@ -1342,9 +1342,9 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   // ---- host staging layout (bytes): per-round uploads, final upload, downloads
   std::vector<size_t> up_off(m + 2);
   size_t off = 0;
-  for (int r = 0; r < m; r++) {  // W | c'W | Wi | c' | f2 W | f3 W (Fr) | base-x digits of (c^-1, c, c^-1, c)
+  for (int r = 0; r < m; r++) {  // f_j W (j < 8, f_0 = 1) | Wi | c' (Fr) | base-x digits of (c^-1, c, c^-1, c)
     up_off[r] = off;
-    off += (5 * ((size_t)1 << r) + 1) * 32 + 128;
+    off += (9 * ((size_t)1 << r) + 1) * 32 + 128;
   }
   up_off[m] = off;  // final: W | Wi | evals | rs (Fr), a_rev (canonical Fr)
   off += (3 * C + m + k) * 32;
@@ -1356,7 +1356,11 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   uint8_t* pin = (uint8_t*)ctx->pinned;
   // four hardware queues: A (critical), B (cross terms, then the h folds of
   // "C"), and two look-ahead streams for alternating rounds -- consecutive
-  // look-aheads overlap, each taking longer than a round
+  // look-aheads overlap, each taking longer than a round.  h is prepared
+  // (G2 line coefficients, a ~2 ms chain) only at odd rounds: look-ahead r
+  // pairs E = 2^(r - s) fold sets of a^(r) against the prepared h^(s),
+  // s = r - 2 (r odd) or r - 3 (r even), s = 0 for r <= 2, so stream B
+  // carries one preparation per two rounds
   hipStream_t sA = ctx->stream, sB = ctx->side[0], sC = ctx->side[0];
   hipStream_t sLA[2] = {ctx->side[1], ctx->side[2]};
   Arena &arA = ctx->arena, &arB = ctx->arena_side[0], &arC = ctx->arena2;
@@ -1368,10 +1372,12 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   auto ev_b = [&](int r) { return ev[8 + 5 * r + 2]; };
   auto ev_c = [&](int r) { return ev[8 + 5 * r + 3]; };
   auto ev_la = [&](int r) { return ev[8 + 5 * r + 4]; };
+  // the prepared h the look-ahead of round r pairs against (see above)
+  auto la_src = [](int r) { return r <= 2 ? 0 : (r & 1) ? r - 2 : r - 3; };
 
   // ---- device buffers (allocated before any stream runs: no hipFree mid-open)
   const size_t Ch = C > 1 ? C / 2 : 1;
-  DevBuf up, A, P, Y, chiC, ScA, ScB, ScC, ScD[2], xa, xb, xd, xh, xp, xl[2], LAo[2], Hb[4], Lb[4], gts, canA, canB,
+  DevBuf up, A, P, Y, chiC, ScA, ScB, ScC, ScD[2], xa, xb, xd, xh, xp, xl[2], LAo[2], Hb[2], Lb[2], gts, canA, canB,
       canC, canD, pstA, pstB;
   TPST_HIP(ctx, up.alloc(up_bytes));
   TPST_HIP(ctx, A.alloc(C * 96));
@@ -1386,13 +1392,13 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   TPST_HIP(ctx, xd.alloc((k + 1) * sizeof(Xyzz<Fq2>)));
   TPST_HIP(ctx, xh.alloc(C * sizeof(Xyzz<Fq2>)));
   TPST_HIP(ctx, xp.alloc(((size_t)m + 1) * sizeof(Xyzz<Fq>)));
-  for (int i = 0; i < 4; i++) {
+  for (int i = 0; i < 2; i++) {
     TPST_HIP(ctx, Hb[i].alloc(Ch * 192));
     TPST_HIP(ctx, Lb[i].alloc(Ch * N_LINE_COEFFS * sizeof(LineCoeff)));
   }
   TPST_HIP(ctx, gts.alloc(2 * sizeof(Fq12)));
   for (int i = 0; i < 2; i++) {
-    TPST_HIP(ctx, ScD[i].alloc(4 * C * 32));
+    TPST_HIP(ctx, ScD[i].alloc(8 * C * 32));
     TPST_HIP(ctx, xl[i].alloc(C * sizeof(Xyzz<Fq>)));
     TPST_HIP(ctx, LAo[i].alloc(8 * sizeof(Fq12)));
   }
@@ -1467,26 +1473,30 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     const size_t len = C >> r, s = len / 2, nW = (size_t)1 << r;
     // stage W | c'W | Wi | c' and upload once (stream A); B and C wait on it
     uint8_t* stg = pin + up_off[r];
-    // look-ahead fold factors for h^(r) over h^(r-2): f2 = c'_{r-2}, f3 = c'_{r-1} c'_{r-2}
-    const Fr f2 = r >= 2 ? xs_inv[r - 2] : Fr::one(), f3 = mul(cprev, f2);
-    for (size_t t = 0; t < nW; t++) {
-      const Fr cw = mul(W[t], cprev), w2 = mul(W[t], f2), w3 = mul(W[t], f3);
-      memcpy(stg + 32 * t, W[t].v, 32);
-      memcpy(stg + 32 * (nW + t), cw.v, 32);
-      memcpy(stg + 32 * (2 * nW + t), Wi[t].v, 32);
-      memcpy(stg + 32 * (3 * nW + 1 + t), w2.v, 32);
-      memcpy(stg + 32 * (4 * nW + 1 + t), w3.v, 32);
+    // look-ahead fold factors of h^(r) over h^(s), s = la_src(r): f_j = product
+    // of c'_{r-1-b} over the set bits b of j (offset j len of h^(s)'s row)
+    const int E = r == 0 ? 1 : 1 << (r - la_src(r));
+    Fr f[8];
+    f[0] = Fr::one();
+    for (int j = 1; j < E; j++) {
+      const int b = 31 - __builtin_clz((unsigned)j);
+      f[j] = mul(f[j ^ (1 << b)], xs_inv[r - 1 - b]);
     }
-    memcpy(stg + 32 * 3 * nW, cprev.v, 32);
-    memcpy(stg + 32 * (5 * nW + 1), la_digits, 128);
+    for (size_t t = 0; t < nW; t++) {
+      memcpy(stg + 32 * t, W[t].v, 32);
+      for (int j = 1; j < E; j++) {
+        const Fr fw = mul(W[t], f[j]);
+        memcpy(stg + 32 * (j * nW + t), fw.v, 32);
+      }
+      memcpy(stg + 32 * (8 * nW + t), Wi[t].v, 32);
+    }
+    memcpy(stg + 32 * 9 * nW, cprev.v, 32);
+    memcpy(stg + 32 * (9 * nW + 1), la_digits, 128);
     uint32_t* dW = dup(up_off[r]);
-    uint32_t* dcW = dW + 8 * nW;
-    uint32_t* dWi = dW + 16 * nW;
-    uint32_t* dcp = dW + 24 * nW;
-    uint32_t* dW2 = dW + 8 * (3 * nW + 1);
-    uint32_t* dW3 = dW + 8 * (4 * nW + 1);
-    const uint64_t* ddig = (const uint64_t*)(dW + 8 * (5 * nW + 1));
-    TPST_HIP(ctx, hipMemcpyAsync(dW, stg, (5 * nW + 1) * 32 + 128, hipMemcpyHostToDevice, sA));
+    uint32_t* dWi = dW + 64 * nW;
+    uint32_t* dcp = dW + 72 * nW;
+    const uint64_t* ddig = (const uint64_t*)(dW + 8 * (9 * nW + 1));
+    TPST_HIP(ctx, hipMemcpyAsync(dW, stg, (9 * nW + 1) * 32 + 128, hipMemcpyHostToDevice, sA));
     TPST_HIP(ctx, hipEventRecord(ev_up(r), sA));
 
     // -- A: t_l / t_r of this round
@@ -1510,17 +1520,15 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
       Arena& arD = *arLA[r & 1];
       TPST_HIP(ctx, hipStreamWaitEvent(sD, ev_up(r), 0));
       arD.reset();
-      const int E = r == 0 ? 1 : r == 1 ? 2 : 4;  // h^(r) over h^(0) / h^(0) / h^(r-2)
       TPST_HIP(ctx, arD.reserve(mipp_lookahead_scratch(len / 4, E) + 4096));
       if (r == 0) {  // a^(0) = comm_list (affine), h^(0) prepared
         TPST_HIP(ctx, mipp_lookahead(arD, sD, L0, C, H0, A.u(), false, len, 1, (Fq12*)LAo[0].p));
       } else {
-        // E fold sets f_j a^(r) (f = 1, c'_{r-1}, c'_{r-2}, c'_{r-1} c'_{r-2}):
-        // h^(r)_q = sum_j f_j h^(r-E/2 ...)[q + j len]
+        // E fold sets f_j a^(r): h^(r)_q = sum_j f_j h^(s)[q + j len]
         TPST_HIP(ctx, hipStreamWaitEvent(sD, ev[EV_TABLE], 0));
         uint32_t* sc = ScD[r & 1].u();
-        const uint32_t* wsets[4] = {dW, dcW, dW2, dW3};
-        for (int j = 0; j < E; j++) TPST_HIP(ctx, mipp_scalars(sD, wsets[j], nullptr, len, 0, C, sc + 8 * C * j));
+        for (int j = 0; j < E; j++)
+          TPST_HIP(ctx, mipp_scalars(sD, dW + 8 * nW * j, nullptr, len, 0, C, sc + 8 * C * j));
         FbGroups g;
         g.groups = len;
         g.members = C / len;
@@ -1529,12 +1537,13 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
         g.sets = (size_t)E;
         g.set_stride = C;
         TPST_HIP(ctx, fbt_msm<Fq>(arD, sD, tA, sc, g, (Xyzz<Fq>*)xl[r & 1].p));
-        const uint32_t* hp = H0;  // h^(0), or h^(r-2) prepared by stream C in round r-2
+        const int src = la_src(r);  // h^(0), or h^(src) prepared by stream C in round src
+        const uint32_t* hp = H0;
         const LineCoeff* lp = L0;
-        if (r >= 3) {
-          TPST_HIP(ctx, hipStreamWaitEvent(sD, ev_c(r - 2), 0));
-          hp = Hb[(r - 2) % 4].u();
-          lp = (const LineCoeff*)Lb[(r - 2) % 4].p;
+        if (src > 0) {
+          TPST_HIP(ctx, hipStreamWaitEvent(sD, ev_c(src), 0));
+          hp = Hb[(src >> 1) & 1].u();
+          lp = (const LineCoeff*)Lb[(src >> 1) & 1].p;
         }
         TPST_HIP(ctx, mipp_lookahead(arD, sD, lp, (size_t)E * len, hp, xl[r & 1].u(), true, len, E,
                                      (Fq12*)LAo[r & 1].p));
@@ -1562,10 +1571,10 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     if (r == 0)
       if (int rc = pst_q()) return rc;
 
-    // -- C: h^(r) for round r+1 (r >= 1; round 1 pairs against h^(0) itself)
-    if (r >= 1 && r + 4 <= m) {  // h^(r) for the look-ahead of round r+2
+    // -- C: h^(r) prepared at odd r for the look-aheads of rounds r+2, r+3
+    if ((r & 1) && r + 4 <= m) {
       TPST_HIP(ctx, hipStreamWaitEvent(sC, ev_up(r), 0));
-      if (r - 2 >= 3) TPST_HIP(ctx, hipStreamWaitEvent(sC, ev_la(r - 2), 0));  // the last reader of slot r % 4
+      if (r >= 5) TPST_HIP(ctx, hipStreamWaitEvent(sC, ev_la(r - 1), 0));  // last reader of h^(r-4)'s slot
       TPST_HIP(ctx, mipp_scalars(sC, dWi, nullptr, len, 0, C, ScC.u()));
       FbGroups g;
       g.groups = len;
@@ -1573,8 +1582,8 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
       g.L = len;
       g.D = 1;
       TPST_HIP(ctx, fbt_msm<Fq2>(arC, sC, tH, ScC.u(), g, (Xyzz<Fq2>*)xh.p));
-      TPST_HIP(ctx, xyzz_to_affine_mont<Fq2>(sC, (Xyzz<Fq2>*)xh.p, Hb[r % 4].u(), len));
-      TPST_HIP(ctx, g2_prepare_batch(sC, Hb[r % 4].u(), len, (LineCoeff*)Lb[r % 4].p));
+      TPST_HIP(ctx, xyzz_to_affine_mont<Fq2>(sC, (Xyzz<Fq2>*)xh.p, Hb[(r >> 1) & 1].u(), len));
+      TPST_HIP(ctx, g2_prepare_batch(sC, Hb[(r >> 1) & 1].u(), len, (LineCoeff*)Lb[(r >> 1) & 1].p));
       TPST_HIP(ctx, hipEventRecord(ev_c(r), sC));
     }
 
