@@ -22,6 +22,7 @@ LIB = os.path.join(HERE, "libtpst.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("TPST_ARCH", "gfx950")
 FLAGS = ["-std=c++17", "-O3", "--offload-arch=" + ARCH, "-fPIC", "-Wno-unused-result",
+         "-Xarch_host", "-march=x86-64-v3", "-Xarch_host", "-madx",
          "-I" + CSRC, "-I" + os.path.join(ROOT, "include")]
 
 

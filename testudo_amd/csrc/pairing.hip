@@ -264,7 +264,7 @@ static hipError_t tree_partials(Arena& ar, hipStream_t s, Fq12*& partial, size_t
 // product of a group is
 //     prod_p f_p = prod_b M_b^(2^b),   M_b = prod_p m_{p,b}.
 // The M_b do not depend on f, so they are a parallel tree over the pairs
-// (k_line_eval, then k_f12_chunk_prod levels); the only serial chain left is
+// (k_line_pair, then k_f12_chunk_prod levels); the only serial chain left is
 // Horner over the bits: per block of LB bits a block multiplier
 // MB_j = prod_{b in block} M_b^(2^(b - lo_j)) (k_miller_blocks, all blocks in
 // parallel), then F = MB_top, F = F^(2^LB) MB_j for the lower blocks, and the
@@ -287,39 +287,102 @@ __global__ void k_set_one(Fq12* __restrict__ v, size_t n) {
   if (i < n) v[i] = Fq12::one();
 }
 
-// out[(g * 69 + idx) * n + k] = line idx of pair (g, k) at its G1 point (dense Fq12)
-__global__ void __launch_bounds__(64) k_line_eval(const LineCoeff* __restrict__ coeffs, const uint32_t* __restrict__ g1,
-                                                  size_t rot_L, const uint32_t* __restrict__ g2, size_t groups,
-                                                  size_t n, size_t map_s, Fq12* __restrict__ out) {
-  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= groups * N_LINE_COEFFS * n) return;
-  const size_t k = t % n, gi = t / n, idx = gi % N_LINE_COEFFS, g = gi / N_LINE_COEFFS;
-  const size_t ncol = groups * n;
-  const size_t j = pair_column(g, k, n, map_s);
-  Fq12 r = Fq12::one();
-  if (!is_inf(load_affine<Fq2>(g2, j))) {
-    Fq px, py, lam;
-    bool inf, scaled = rot_L != 0;
-    if (scaled) {
-      const size_t src = (j / rot_L) * rot_L + ((j % rot_L) + rot_L / 2) % rot_L;
-      const Xyzz<Fq> P = load_xyzz(reinterpret_cast<const Xyzz<Fq>*>(g1), src);
-      inf = is_inf(P);
-      px = mul(P.X, P.ZZZ);
-      py = mul(P.Y, P.ZZ);
-      lam = mul(P.ZZ, P.ZZZ);
-    } else {
-      const G1A P = load_affine<Fq>(g1, j);
-      inf = is_inf(P);
-      px = P.x;
-      py = P.y;
-    }
-    if (!inf) {
-      const LineCoeff c = coeffs[idx * ncol + j];
-      r = Fq12{{mul_fq(c.c0, py), Fq2::zero(), Fq2::zero()},
-               {mul_fq(c.c1, px), scaled ? mul_fq(c.c2, lam) : c.c2, Fq2::zero()}};
-    }
+// Sparse line value c0' + c3' w + c4' v w of one pair at its G1 point
+// (ark ell(): c0 py, c1 px, c2), or the G1 point's lambda = ZZ ZZZ scaling of
+// all three when P is XYZZ (a factor the final exponentiation removes).
+// Returns false when the pair contributes 1 (either point at infinity).
+// Products kept in program order: sched_barrier stops the scheduler from
+// interleaving independent Montgomery products, which multiplies the live
+// limbs past the register file (hundreds of spilled VGPRs otherwise).
+__device__ __forceinline__ Fq smul(const Fq& a, const Fq& b) {
+  const Fq r = mul(a, b);
+  __builtin_amdgcn_sched_barrier(0);
+  return r;
+}
+__device__ __forceinline__ Fq2 smul(const Fq2& a, const Fq2& b) {
+  const Fq v0 = smul(a.c0, b.c0);
+  const Fq v1 = smul(a.c1, b.c1);
+  const Fq t = smul(add(a.c0, a.c1), add(b.c0, b.c1));
+  return {sub(v0, mul5(v1)), sub(sub(t, v0), v1)};
+}
+__device__ __forceinline__ Fq2 smul_fq(const Fq2& a, const Fq& b) { return {smul(a.c0, b), smul(a.c1, b)}; }
+
+__device__ __forceinline__ bool line_at(const LineCoeff* __restrict__ coeffs, size_t col, const uint32_t* g1, size_t p,
+                                        bool xyzz, Fq2& c0, Fq2& c3, Fq2& c4) {
+  Fq px, py, lam;
+  if (xyzz) {
+    const Xyzz<Fq> P = load_xyzz(reinterpret_cast<const Xyzz<Fq>*>(g1), p);
+    if (is_inf(P)) return false;
+    px = smul(P.X, P.ZZZ);
+    py = smul(P.Y, P.ZZ);
+    lam = smul(P.ZZ, P.ZZZ);
+  } else {
+    const G1A P = load_affine<Fq>(g1, p);
+    if (is_inf(P)) return false;
+    px = P.x;
+    py = P.y;
   }
-  out[t] = r;
+  const LineCoeff c = coeffs[col];
+  c0 = smul_fq(c.c0, py);
+  c3 = smul_fq(c.c1, px);
+  c4 = xyzz ? smul_fq(c.c2, lam) : c.c2;
+  return true;
+}
+
+// Pair maps: pair (g, k) of a multi-pairing -> (G1 index, G2 column).
+// Standard: column pair_column(g, k), G1 = the same index (affine), or the
+// half-rotated XYZZ index within blocks of rot_L (MIPP's t_l / t_r pairs).
+struct PairMapStd {
+  size_t n, map_s, rot_L;
+  __device__ void at(size_t g, size_t k, size_t& p, size_t& q) const {
+    q = pair_column(g, k, n, map_s);
+    p = rot_L ? (q / rot_L) * rot_L + ((q % rot_L) + rot_L / 2) % rot_L : q;
+  }
+};
+
+// Pair products of the lines: out[(g 69 + idx) nout + c] = line idx of pair
+// (g, 2c) times that of pair (g, 2c + 1) (the lone line when n is odd), one
+// lane per product.  Two sparse line values A = a0 + (a3 + a4 v) w and B
+// multiply to
+//   (a0 b0 + u a4 b4, a3 b3, a3 b4 + a4 b3) + (a0 b3 + a3 b0, a0 b4 + a4 b0, 0) w
+// -- six Fq2 products with Karatsuba cross terms -- stored as a dense Fq12:
+// half as many values for the wave-cooperative tree that follows, and none of
+// its dense x dense products at the widest level (its lone waves are
+// latency-bound at their LDS-limited occupancy; this is throughput work).
+template <class Map>
+__global__ void __launch_bounds__(64, 1) k_line_pair(const LineCoeff* __restrict__ coeffs, size_t ncol,
+                                                     const uint32_t* __restrict__ g1, int xyzz,
+                                                     const uint32_t* __restrict__ g2, size_t groups, size_t n,
+                                                     Map map, size_t nout, Fq12* __restrict__ out) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= groups * N_LINE_COEFFS * nout) return;
+  const size_t c = t % nout, gi = t / nout, idx = gi % N_LINE_COEFFS, g = gi / N_LINE_COEFFS;
+  Fq2 a0, a3, a4, b0, b3, b4;
+  bool ha = false, hb = false;
+  size_t p, q;
+  map.at(g, 2 * c, p, q);
+  if (!is_inf(load_affine<Fq2>(g2, q))) ha = line_at(coeffs, idx * ncol + q, g1, p, xyzz != 0, a0, a3, a4);
+  if (2 * c + 1 < n) {
+    map.at(g, 2 * c + 1, p, q);
+    if (!is_inf(load_affine<Fq2>(g2, q))) hb = line_at(coeffs, idx * ncol + q, g1, p, xyzz != 0, b0, b3, b4);
+  }
+  Fq12* o = out + t;
+  if (ha && hb) {
+    const Fq2 m33 = smul(a3, b3);
+    o->c0.c1 = m33;
+    const Fq2 m00 = smul(a0, b0);
+    o->c1.c0 = sub(sub(smul(add(a0, a3), add(b0, b3)), m00), m33);
+    const Fq2 m44 = smul(a4, b4);
+    o->c0.c2 = sub(sub(smul(add(a3, a4), add(b3, b4)), m33), m44);
+    o->c0.c0 = add(m00, mul_by_u(m44));
+    o->c1.c1 = sub(sub(smul(add(a0, a4), add(b0, b4)), m00), m44);
+    o->c1.c2 = Fq2::zero();
+  } else if (ha || hb) {
+    *o = ha ? Fq12{{a0, Fq2::zero(), Fq2::zero()}, {a3, a4, Fq2::zero()}}
+            : Fq12{{b0, Fq2::zero(), Fq2::zero()}, {b3, b4, Fq2::zero()}};
+  } else {
+    *o = Fq12::one();
+  }
 }
 
 // line index of the doubling at bit b (62..0); its addition line follows it
@@ -490,8 +553,11 @@ hipError_t multi_pairing_prepared(Arena& ar, hipStream_t s, const uint32_t* d_g1
   const size_t G = groups * N_LINE_COEFFS;
   Fq12* lines = ar.take<Fq12>(G * (n ? n : 1));
   if (n) {
-    k_line_eval<<<grid_for(G * n, 64), 64, 0, s>>>(d_coeffs, d_g1, rot_L, d_g2, groups, n, map_s, lines);
+    const size_t nout = (n + 1) / 2;
+    k_line_pair<PairMapStd><<<grid_for(G * nout, 64), 64, 0, s>>>(d_coeffs, groups * n, d_g1, rot_L ? 1 : 0, d_g2,
+                                                                 groups, n, PairMapStd{n, map_s, rot_L}, nout, lines);
     TPST_TRY(hipGetLastError());
+    n = nout;
   } else {
     k_set_one<<<grid_for(G, 64), 64, 0, s>>>(lines, G);
     TPST_TRY(hipGetLastError());
@@ -512,41 +578,14 @@ hipError_t multi_pairing_prepared(Arena& ar, hipStream_t s, const uint32_t* d_g1
 __constant__ uint32_t LA_P[8] = {0, 2, 0, 2, 1, 3, 1, 3};  // G1 offset in units of s'
 __constant__ uint32_t LA_Q[8] = {1, 3, 3, 1, 0, 2, 2, 0};  // G2 offset in units of s'
 
-__global__ void __launch_bounds__(64) k_line_eval_la(const LineCoeff* __restrict__ coeffs, size_t ncol,
-                                                     const uint32_t* __restrict__ g1, int xyzz,
-                                                     const uint32_t* __restrict__ g2, size_t sp, size_t len, int E,
-                                                     Fq12* __restrict__ out) {
-  const size_t n = sp * (size_t)E;
-  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 8 * N_LINE_COEFFS * n) return;
-  const size_t k = t % n, gi = t / n, idx = gi % N_LINE_COEFFS, g = gi / N_LINE_COEFFS;
-  const size_t i = k % sp, j = k / sp;
-  const size_t p = LA_P[g] * sp + i + j * len;
-  const size_t q = LA_Q[g] * sp + i + j * len;
-  Fq12 r = Fq12::one();
-  if (!is_inf(load_affine<Fq2>(g2, q))) {
-    Fq px, py, lam;
-    bool inf;
-    if (xyzz) {
-      const Xyzz<Fq> P = load_xyzz(reinterpret_cast<const Xyzz<Fq>*>(g1), p);
-      inf = is_inf(P);
-      px = mul(P.X, P.ZZZ);
-      py = mul(P.Y, P.ZZ);
-      lam = mul(P.ZZ, P.ZZZ);
-    } else {
-      const G1A P = load_affine<Fq>(g1, p);
-      inf = is_inf(P);
-      px = P.x;
-      py = P.y;
-    }
-    if (!inf) {
-      const LineCoeff c = coeffs[idx * ncol + q];
-      r = Fq12{{mul_fq(c.c0, py), Fq2::zero(), Fq2::zero()},
-               {mul_fq(c.c1, px), xyzz ? mul_fq(c.c2, lam) : c.c2, Fq2::zero()}};
-    }
+struct PairMapLA {
+  size_t sp, len;
+  __device__ void at(size_t g, size_t k, size_t& p, size_t& q) const {
+    const size_t i = k % sp, j = k / sp;
+    p = LA_P[g] * sp + i + j * len;
+    q = LA_Q[g] * sp + i + j * len;
   }
-  out[t] = r;
-}
+};
 
 size_t mipp_lookahead_scratch(size_t sp, int E) {
   const size_t n = sp * (size_t)E;
@@ -559,10 +598,11 @@ hipError_t mipp_lookahead(Arena& ar, hipStream_t s, const LineCoeff* d_coeffs, s
   if (!sp || E < 1 || E > 8 || (E & (E - 1)) || ncol < (size_t)E * len) return hipErrorInvalidValue;
   const size_t n = sp * (size_t)E;
   Fq12* lines = ar.take<Fq12>(8 * N_LINE_COEFFS * n);
-  k_line_eval_la<<<grid_for(8 * N_LINE_COEFFS * n, 64), 64, 0, s>>>(d_coeffs, ncol, d_g1, xyzz ? 1 : 0, d_g2, sp,
-                                                                      len, E, lines);
+  const size_t G = 8 * N_LINE_COEFFS, nout = (n + 1) / 2;
+  k_line_pair<PairMapLA><<<grid_for(G * nout, 64), 64, 0, s>>>(d_coeffs, ncol, d_g1, xyzz ? 1 : 0, d_g2, 8, n,
+                                                              PairMapLA{sp, len}, nout, lines);
   TPST_TRY(hipGetLastError());
-  return pairing_from_lines(ar, s, lines, 8, n, d_out8, true);
+  return pairing_from_lines(ar, s, lines, 8, nout, d_out8, true);
 }
 
 hipError_t gt_product_final(Arena& ar, hipStream_t s, const Fq12* d_partials, size_t groups, size_t n, Fq12* d_out) {

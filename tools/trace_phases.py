@@ -32,7 +32,7 @@ def summ(name, s):
 
 
 # commit = from batch_sort until the first k_final_wave completes (IPP final exp)
-j = next(k for k in range(len(seg)) if "k_final_wave" in seg[k][2])
+j = next(k for k in range(len(seg)) if "k_final_wave" in seg[k][2] or "k_chain_final" in seg[k][2])
 summ("commit", seg[:j + 1])
 summ("open", seg[j + 1:])
 if len(sys.argv) > 2:
