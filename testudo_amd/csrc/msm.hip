@@ -1119,6 +1119,154 @@ __global__ void __launch_bounds__(256) k_batch_sort(const uint32_t* __restrict__
   for (size_t e = total + threadIdx.x; e < N * (size_t)W; e += blockDim.x) keys[rowbase + e] = sent;
 }
 
+// Staged variant (N <= SB_THREADS * SB_SPT, nb <= SB_NB): one 1024-thread
+// workgroup per row.  After the LDS counting pass and the scan, the row's
+// output is produced in position ranges of at most SB_STAGE entries: a pass
+// takes the buckets [b_lo, b_hi) whose entries fit the range, recomputes the
+// row's signed digits (the scalars are L2-resident after the counting pass),
+// scatters the pass's digits into LDS and flushes the range to global memory
+// with consecutive (coalesced) stores.  The direct scatter of k_batch_sort
+// writes every 4-byte key and entry to a random position of a ~720 KB row
+// region while dozens of rows per XCD are in flight (far over the L2), so
+// nearly every store was a partial-line write; here the row's keys and
+// entries are written once, contiguously.  A bucket larger than the stage
+// (degenerate scalars) is scattered directly in a pass of its own.
+constexpr int SB_THREADS = 1024;
+constexpr int SB_SPT = 4;                 // scalars per thread: N <= 4096
+constexpr uint32_t SB_NB = 2048;          // buckets per row (c <= 12)
+constexpr uint32_t SB_STAGE = 15 * 1024;  // staged entries per pass (120 KB)
+
+__global__ void __launch_bounds__(SB_THREADS) k_batch_sort_staged(const uint32_t* __restrict__ scalars, size_t rows,
+                                                                 size_t N, size_t row_stride, size_t col_stride, int c,
+                                                                 int W, uint32_t* __restrict__ keys,
+                                                                 uint32_t* __restrict__ entries,
+                                                                 uint32_t* __restrict__ bstart,
+                                                                 uint32_t* __restrict__ bend) {
+  __shared__ uint32_t start[SB_NB + 1];
+  __shared__ uint32_t cur[SB_NB];
+  __shared__ uint2 stage[SB_STAGE];
+  __shared__ uint32_t part[SB_THREADS / 64];
+  __shared__ uint32_t pass_lo, pass_hi;
+  const size_t nblk = gridDim.x;
+  size_t r = blockIdx.x;
+  if (nblk % 8 == 0) r = (blockIdx.x % 8) * (nblk / 8) + blockIdx.x / 8;  // XCD-aware, as k_batch_sort
+  if (r >= rows) return;
+  const uint32_t nb = 1u << (c - 1);
+  const int tid = threadIdx.x;
+  for (uint32_t b = tid; b < nb; b += SB_THREADS) cur[b] = 0;
+  __syncthreads();
+  for (int k = 0; k < SB_SPT; k++) {
+    const size_t j = (size_t)tid + (size_t)k * SB_THREADS;
+    if (j >= N) break;
+    uint32_t sc[8];
+    load_scalar(scalars + 8 * (r * row_stride + j * col_stride), sc);
+    uint32_t carry = 0;
+    for (int w = 0; w < W; w++) {
+      const int d = signed_digit(sc, 8, w, c, W, carry);
+      if (d) atomicAdd(&cur[abs(d) - 1], 1u);
+    }
+  }
+  __syncthreads();
+  // exclusive scan of the counts -> start[] (row-relative)
+  {
+    const uint32_t per = (nb + SB_THREADS - 1) / SB_THREADS;
+    const uint32_t b0 = tid * per;
+    uint32_t local = 0;
+    for (uint32_t b = b0; b < b0 + per && b < nb; b++) local += cur[b];
+    const int lane = tid & 63, wv = tid >> 6;
+    uint32_t incl = local;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    if (lane == 63) part[wv] = incl;
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t run = 0;
+      for (int i = 0; i < SB_THREADS / 64; i++) {
+        const uint32_t v = part[i];
+        part[i] = run;
+        run += v;
+      }
+      start[nb] = run;
+    }
+    __syncthreads();
+    uint32_t run = part[wv] + incl - local;
+    for (uint32_t b = b0; b < b0 + per && b < nb; b++) {
+      const uint32_t v = cur[b];
+      start[b] = run;
+      run += v;
+    }
+  }
+  __syncthreads();
+  const size_t rowbase = r * N * (size_t)W;
+  for (uint32_t b = tid; b < nb; b += SB_THREADS) {
+    bstart[r * nb + b] = (uint32_t)(rowbase + start[b]);
+    bend[r * nb + b] = (uint32_t)(rowbase + start[b + 1]);
+    cur[b] = start[b];
+  }
+  const uint32_t total = start[nb];
+  if (tid == 0) pass_hi = 0;
+  __syncthreads();
+  for (;;) {
+    // next pass: buckets [lo, hi) from the end of the previous one, as many
+    // as fit the stage (at least one)
+    if (tid == 0) {
+      const uint32_t lo = pass_hi;
+      uint32_t hi = lo;
+      if (lo < nb) {
+        const uint32_t lim = start[lo] + SB_STAGE;
+        uint32_t a = lo + 1, z = nb;  // largest hi in (lo, nb] with start[hi] <= lim
+        while (a < z) {
+          const uint32_t m = (a + z + 1) >> 1;
+          if (start[m] <= lim) a = m; else z = m - 1;
+        }
+        hi = a;
+      }
+      pass_lo = lo;
+      pass_hi = hi;
+    }
+    __syncthreads();
+    const uint32_t lo = pass_lo, hi = pass_hi;
+    if (lo >= nb) break;
+    const uint32_t p0 = start[lo], cnt = start[hi] - p0;
+    const bool direct = cnt > SB_STAGE;  // one oversized bucket
+    for (int k = 0; k < SB_SPT; k++) {
+      const size_t j = (size_t)tid + (size_t)k * SB_THREADS;
+      if (j >= N) break;
+      uint32_t sc[8];
+      load_scalar(scalars + 8 * (r * row_stride + j * col_stride), sc);
+      uint32_t carry = 0;
+      for (int w = 0; w < W; w++) {
+        const int d = signed_digit(sc, 8, w, c, W, carry);
+        if (!d) continue;
+        const uint32_t b = (uint32_t)abs(d) - 1;
+        if (b < lo || b >= hi) continue;
+        const uint32_t pos = atomicAdd(&cur[b], 1u);
+        const uint2 e = make_uint2((uint32_t)(r * nb + b), (uint32_t)(w * N + j) | (d < 0 ? 0x80000000u : 0u));
+        if (direct) {
+          keys[rowbase + pos] = e.x;
+          entries[rowbase + pos] = e.y;
+        } else {
+          stage[pos - p0] = e;
+        }
+      }
+    }
+    __syncthreads();
+    if (!direct) {
+      for (uint32_t i = tid; i < cnt; i += SB_THREADS) {
+        const uint2 e = stage[i];
+        keys[rowbase + p0 + i] = e.x;
+        entries[rowbase + p0 + i] = e.y;
+      }
+    }
+    __syncthreads();
+  }
+  // zero digits leave the row's region short: pad it with the sentinel
+  const uint32_t sent = (uint32_t)(rows * nb);
+  for (size_t e = total + tid; e < N * (size_t)W; e += SB_THREADS) keys[rowbase + e] = sent;
+}
+
 hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint32_t* d_scalars, size_t rows,
                      size_t row_stride, size_t col_stride, Xyzz<Fq>* d_out) {
   if (rows == 0) return hipSuccess;
@@ -1149,8 +1297,12 @@ hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint3
   if (!pf) pf = &dummy;
   pf->begin(ST_BATCH_SORT, s);
   TPST_TRY(hipMemsetAsync(buckets, 0, nbk * sizeof(Xyzz<Fq>), s));  // ZZ = 0 == infinity
-  k_batch_sort<<<nrow_blk, 256, nb * sizeof(uint32_t), s>>>(d_scalars, rows, N, row_stride, col_stride, c, W, keys,
-                                                        entries, bstart, bend);
+  if (N <= (size_t)SB_THREADS * SB_SPT && nb <= SB_NB && !getenv("TPST_BATCH_SORT_DIRECT"))
+    k_batch_sort_staged<<<nrow_blk, SB_THREADS, 0, s>>>(d_scalars, rows, N, row_stride, col_stride, c, W, keys,
+                                                         entries, bstart, bend);
+  else
+    k_batch_sort<<<nrow_blk, 256, nb * sizeof(uint32_t), s>>>(d_scalars, rows, N, row_stride, col_stride, c, W, keys,
+                                                          entries, bstart, bend);
   TPST_TRY(hipGetLastError());
   pf->end(ST_BATCH_SORT, s);
   pf->begin(ST_BUCKET_ACC, s);
