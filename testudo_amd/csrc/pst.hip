@@ -244,6 +244,53 @@ hipError_t mipp_scalars(hipStream_t s, const uint32_t* d_W, const uint32_t* d_y,
   return hipGetLastError();
 }
 
+// E fold sets at once: out[j n + k] = canonical(W[k / len] * f[j])
+__global__ void k_mipp_scalar_sets(const uint32_t* __restrict__ W, const uint32_t* __restrict__ f, int E, size_t len,
+                                   size_t n, uint32_t* __restrict__ out) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)E * n) return;
+  const size_t j = t / n, k = t % n;
+  store_f<Fr>(out + 8 * t, from_mont(mul(load_f<Fr>(W + 8 * (k / len)), load_f<Fr>(f + 8 * j))));
+}
+
+hipError_t mipp_scalar_sets(hipStream_t s, const uint32_t* d_W, const uint32_t* d_f, int E, size_t len, size_t n,
+                            uint32_t* d_out) {
+  if (!n || E <= 0) return hipSuccess;
+  k_mipp_scalar_sets<<<grid_for((size_t)E * n, 256), 256, 0, s>>>(d_W, d_f, E, len, n, d_out);
+  return hipGetLastError();
+}
+
+// MIPP fold weights of round r from round r-1's (mipp.rs:58-120 unrolled):
+// W_r[2t] = W_{r-1}[t], W_r[2t+1] = W_{r-1}[t] c, and Wi likewise with c^-1;
+// round r's 2^r weights live at offset 2^r - 1 of W / Wi (r = 0: W_0 = Wi_0 = 1)
+__global__ void k_mipp_weights(uint32_t* __restrict__ W, uint32_t* __restrict__ Wi, int r,
+                               const uint32_t* __restrict__ c, const uint32_t* __restrict__ cinv) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t nw = (size_t)1 << r;
+  if (t >= nw) return;
+  const size_t o = nw - 1 + t;
+  if (r == 0) {
+    store_f<Fr>(W + 8 * o, Fr::one());
+    store_f<Fr>(Wi + 8 * o, Fr::one());
+    return;
+  }
+  const size_t src = (nw / 2 - 1) + (t >> 1);
+  Fr w = load_f<Fr>(W + 8 * src), wi = load_f<Fr>(Wi + 8 * src);
+  if (t & 1) {
+    w = mul(w, load_f<Fr>(c));
+    wi = mul(wi, load_f<Fr>(cinv));
+  }
+  store_f<Fr>(W + 8 * o, w);
+  store_f<Fr>(Wi + 8 * o, wi);
+}
+
+hipError_t mipp_weights(hipStream_t s, uint32_t* d_W, uint32_t* d_Wi, int r, const uint32_t* d_c,
+                        const uint32_t* d_cinv) {
+  const size_t nw = (size_t)1 << r;
+  k_mipp_weights<<<grid_for(nw, 256), 256, 0, s>>>(d_W, d_Wi, r, d_c, d_cinv);
+  return hipGetLastError();
+}
+
 template hipError_t compress_points<Fq>(hipStream_t, uint32_t*, size_t, const uint32_t*);
 template hipError_t compress_points<Fq2>(hipStream_t, uint32_t*, size_t, const uint32_t*);
 template hipError_t fixed_base_mul<Fq>(hipStream_t, const uint32_t*, const uint32_t*, size_t, uint32_t*);

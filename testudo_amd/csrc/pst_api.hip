@@ -1342,12 +1342,15 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   // ---- host staging layout (bytes): per-round uploads, final upload, downloads
   std::vector<size_t> up_off(m + 2);
   size_t off = 0;
-  for (int r = 0; r < m; r++) {  // f_j W (j < 8, f_0 = 1) | Wi | c' (Fr) | base-x digits of (c^-1, c, c^-1, c)
+  // per round: c_{r-1}, c_{r-1}^-1, f_0..f_7 (Montgomery Fr), base-x digits of
+  // (c^-1, c, c^-1, c); the fold weights themselves are formed on the device
+  constexpr size_t UP_ROUND = 10 * 32 + 128;
+  for (int r = 0; r < m; r++) {
     up_off[r] = off;
-    off += (9 * ((size_t)1 << r) + 1) * 32 + 128;
+    off += UP_ROUND;
   }
-  up_off[m] = off;  // final: W | Wi | evals | rs (Fr), a_rev (canonical Fr)
-  off += (3 * C + m + k) * 32;
+  up_off[m] = off;  // final: c_{m-1}, c_{m-1}^-1, rs (Montgomery Fr), a_rev (canonical Fr)
+  off += (2 + m + k) * 32;
   const size_t up_bytes = off;
   const size_t dn_U = up_bytes, dn_round = dn_U + 96, dn_final = dn_round + (size_t)m * (192 + 1152);
   const size_t dn_bytes = 96 + (size_t)m * (192 + 1152) + 96 + 192 + (size_t)m * 96 + (size_t)k * 192;
@@ -1378,8 +1381,10 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   // ---- device buffers (allocated before any stream runs: no hipFree mid-open)
   const size_t Ch = C > 1 ? C / 2 : 1;
   DevBuf up, A, P, Y, chiC, ScA, ScB, ScC, ScD[2], xa, xb, xd, xh, xp, xl[2], LAo[2], Hb[2], Lb[2], gts, canA, canB,
-      canC, canD, pstA, pstB;
+      canC, canD, pstA, pstB, Wall, Wiall;
   TPST_HIP(ctx, up.alloc(up_bytes));
+  TPST_HIP(ctx, Wall.alloc(2 * C * 32));  // round r's 2^r fold weights at offset 2^r - 1
+  TPST_HIP(ctx, Wiall.alloc(2 * C * 32));
   TPST_HIP(ctx, A.alloc(C * 96));
   TPST_HIP(ctx, P.alloc(C * 96));
   TPST_HIP(ctx, Y.alloc(C * 32));
@@ -1420,7 +1425,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
 
   // ---- prologue (stream A): comm_list -> Montgomery, y = chi(b), canonical chi
   {
-    uint8_t* a_stage = pin + up_off[m] + (3 * C + m) * 32;  // a_rev (canonical) -> D
+    uint8_t* a_stage = pin + up_off[m] + (2 + m) * 32;  // a_rev (canonical) -> D
     for (int i = 0; i < k; i++) memcpy(a_stage + 32 * i, point + 4 * (k - 1 - i), 32);
   }
   TPST_HIP(ctx, hipMemcpyAsync(A.p, comms, C * 96, hipMemcpyHostToDevice, sA));  // pageable: staged by HIP
@@ -1450,7 +1455,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   }
   // PST proof of q at a_rev (stream B, after round 0's cross terms)
   auto pst_q = [&]() -> int {
-    const size_t a_off = up_off[m] + (3 * C + m) * 32;
+    const size_t a_off = up_off[m] + (2 + m) * 32;
     TPST_HIP(ctx, hipMemcpyAsync(dup(a_off), pin + a_off, (size_t)k * 32, hipMemcpyHostToDevice, sB));
     TPST_HIP(ctx, fr_to_mont(sB, dup(a_off), dup(a_off), k));
     Xyzz<Fq2>* x2 = (Xyzz<Fq2>*)xd.p + 1;
@@ -1463,15 +1468,17 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   if (m == 0)
     if (int rc = pst_q()) return rc;
 
-  // W[t] / Wi[t]: products of the challenges (inverses) folded so far, so that
-  // a^(r)_i = sum_t W[t] a_{i + t len}, h^(r)_i = sum_t Wi[t] h_{i + t len}
-  std::vector<Fr> W(1, Fr::one()), Wi(1, Fr::one()), xs_inv;
-  Fr cprev = Fr::one();
+  // W_r[t] / Wi_r[t] (device, mipp_weights): products of the challenges
+  // (inverses) folded so far, so that a^(r)_i = sum_t W_r[t] a_{i + t len},
+  // h^(r)_i = sum_t Wi_r[t] h_{i + t len}
+  std::vector<Fr> xs_inv;
+  Fr cprev = Fr::one(), cprev_c = Fr::one();
   uint64_t la_digits[16] = {};
   bool have_U = false;
   for (int r = 0; r < m; r++) {  // mipp.rs:58-120
     const size_t len = C >> r, s = len / 2, nW = (size_t)1 << r;
-    // stage W | c'W | Wi | c' and upload once (stream A); B and C wait on it
+    // stage c_{r-1}, c_{r-1}^-1, the look-ahead factors and digits; upload
+    // once (stream A), form this round's weights there; B, C, D wait on it
     uint8_t* stg = pin + up_off[r];
     // look-ahead fold factors of h^(r) over h^(s), s = la_src(r): f_j = product
     // of c'_{r-1-b} over the set bits b of j (offset j len of h^(s)'s row)
@@ -1482,21 +1489,18 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
       const int b = 31 - __builtin_clz((unsigned)j);
       f[j] = mul(f[j ^ (1 << b)], xs_inv[r - 1 - b]);
     }
-    for (size_t t = 0; t < nW; t++) {
-      memcpy(stg + 32 * t, W[t].v, 32);
-      for (int j = 1; j < E; j++) {
-        const Fr fw = mul(W[t], f[j]);
-        memcpy(stg + 32 * (j * nW + t), fw.v, 32);
-      }
-      memcpy(stg + 32 * (8 * nW + t), Wi[t].v, 32);
-    }
-    memcpy(stg + 32 * 9 * nW, cprev.v, 32);
-    memcpy(stg + 32 * (9 * nW + 1), la_digits, 128);
-    uint32_t* dW = dup(up_off[r]);
-    uint32_t* dWi = dW + 64 * nW;
-    uint32_t* dcp = dW + 72 * nW;
-    const uint64_t* ddig = (const uint64_t*)(dW + 8 * (9 * nW + 1));
-    TPST_HIP(ctx, hipMemcpyAsync(dW, stg, (9 * nW + 1) * 32 + 128, hipMemcpyHostToDevice, sA));
+    memcpy(stg, cprev_c.v, 32);
+    memcpy(stg + 32, cprev.v, 32);
+    for (int j = 0; j < E; j++) memcpy(stg + 64 + 32 * j, f[j].v, 32);
+    memcpy(stg + 320, la_digits, 128);
+    uint32_t* dup_r = dup(up_off[r]);
+    uint32_t* dcp = dup_r + 8;   // c' = c_{r-1}^-1 (the y fold)
+    uint32_t* dfs = dup_r + 16;  // f_0..f_{E-1}
+    const uint64_t* ddig = (const uint64_t*)(dup_r + 80);
+    TPST_HIP(ctx, hipMemcpyAsync(dup_r, stg, UP_ROUND, hipMemcpyHostToDevice, sA));
+    TPST_HIP(ctx, mipp_weights(sA, Wall.u(), Wiall.u(), r, dup_r, dcp));
+    uint32_t* dW = Wall.u() + 8 * (nW - 1);
+    uint32_t* dWi = Wiall.u() + 8 * (nW - 1);
     TPST_HIP(ctx, hipEventRecord(ev_up(r), sA));
 
     // -- A: t_l / t_r of this round
@@ -1527,8 +1531,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
         // E fold sets f_j a^(r): h^(r)_q = sum_j f_j h^(s)[q + j len]
         TPST_HIP(ctx, hipStreamWaitEvent(sD, ev[EV_TABLE], 0));
         uint32_t* sc = ScD[r & 1].u();
-        for (int j = 0; j < E; j++)
-          TPST_HIP(ctx, mipp_scalars(sD, dW + 8 * nW * j, nullptr, len, 0, C, sc + 8 * C * j));
+        TPST_HIP(ctx, mipp_scalar_sets(sD, dW, dfs, E, len, C, sc));
         FbGroups g;
         g.groups = len;
         g.members = C / len;
@@ -1616,15 +1619,9 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     sp.challenge(ci_c);  // mipp.rs:101
     const Fr c_inv = fr_canon(ci_c);
     const Fr c = fr_inv(c_inv);  // mipp.rs:106
-    std::vector<Fr> W2(2 * W.size()), Wi2(2 * Wi.size());
-    for (size_t t = 0; t < W2.size(); t++) {
-      W2[t] = (t & 1) ? mul(W[t >> 1], c) : W[t >> 1];
-      Wi2[t] = (t & 1) ? mul(Wi[t >> 1], c_inv) : Wi[t >> 1];
-    }
-    W.swap(W2);
-    Wi.swap(Wi2);
     xs_inv.push_back(c_inv);
     cprev = c_inv;
+    cprev_c = c;
     // base-x digits of (c^-1, c, c^-1, c) for the next round's combination
     {
       uint64_t ci[4], cc[4];
@@ -1645,31 +1642,30 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
 
   // ---- epilogue: final_a (A), final_h (C), pst_proof_h (B); rs need only the
   // transcript state after the last round (mipp.rs:138-141)
+  // final weights W_m, Wi_m (device); the p_h evaluations of mipp.rs:159-180,
+  // prod over the set bits j of t of c^-1_{m-1-j}, are exactly Wi_m[t]
   {
     uint8_t* stg = pin + up_off[m];
-    for (size_t t = 0; t < C; t++) {
-      memcpy(stg + 32 * t, W[t].v, 32);
-      memcpy(stg + 32 * (C + t), Wi[t].v, 32);
-      Fr v = Fr::one();  // p_h evaluations from the challenges (mipp.rs:159-180)
-      for (int j = 0; j < m; j++)
-        if ((t >> j) & 1) v = mul(v, xs_inv[m - j - 1]);
-      memcpy(stg + 32 * (2 * C + t), v.v, 32);
-    }
+    memcpy(stg, cprev_c.v, 32);
+    memcpy(stg + 32, cprev.v, 32);
     for (int i = 0; i < m; i++) {
       uint64_t cc[4];
       sp.challenge(cc);
       const Fr rr = fr_canon(cc);
-      memcpy(stg + 32 * (3 * C + i), rr.v, 32);
+      memcpy(stg + 32 * (2 + i), rr.v, 32);
     }
   }
-  uint32_t* dWf = dup(up_off[m]);
-  TPST_HIP(ctx, hipMemcpyAsync(dWf, pin + up_off[m], (3 * C + m) * 32, hipMemcpyHostToDevice, sA));
+  uint32_t* dfin = dup(up_off[m]);
+  TPST_HIP(ctx, hipMemcpyAsync(dfin, pin + up_off[m], (2 + m) * 32, hipMemcpyHostToDevice, sA));
+  TPST_HIP(ctx, mipp_weights(sA, Wall.u(), Wiall.u(), m, dfin, dfin + 8));
+  const uint32_t* dWm = Wall.u() + 8 * (C - 1);
+  const uint32_t* dWim = Wiall.u() + 8 * (C - 1);
   TPST_HIP(ctx, hipEventRecord(ev[EV_FINAL_UP], sA));
   TPST_HIP(ctx, hipStreamWaitEvent(sA, ev[EV_TABLE], 0));
   {  // final_a = a^(m)_0 (one group over all C bases)
     FbGroups g;
     g.members = C;
-    TPST_HIP(ctx, mipp_scalars(sA, dWf, nullptr, 1, 0, C, ScA.u()));
+    TPST_HIP(ctx, mipp_scalars(sA, dWm, nullptr, 1, 0, C, ScA.u()));
     TPST_HIP(ctx, fbt_msm<Fq>(arA, sA, tA, ScA.u(), g, (Xyzz<Fq>*)xa.p));
     TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(sA, (Xyzz<Fq>*)xa.p, canA.u(), 1));
     TPST_HIP(ctx, hipMemcpyAsync(pin + dn_final, canA.p, 96, hipMemcpyDeviceToHost, sA));
@@ -1678,7 +1674,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   {  // final_h = h^(m)_0
     FbGroups g;
     g.members = C;
-    TPST_HIP(ctx, mipp_scalars(sC, dWf + 8 * C, nullptr, 1, 0, C, ScC.u()));
+    TPST_HIP(ctx, mipp_scalars(sC, dWim, nullptr, 1, 0, C, ScC.u()));
     TPST_HIP(ctx, fbt_msm<Fq2>(arC, sC, tH, ScC.u(), g, (Xyzz<Fq2>*)xh.p));
     TPST_HIP(ctx, xyzz_to_affine_canonical<Fq2>(sC, (Xyzz<Fq2>*)xh.p, canC.u(), 1));
     TPST_HIP(ctx, hipMemcpyAsync(pin + dn_final + 96, canC.p, 192, hipMemcpyDeviceToHost, sC));
@@ -1686,7 +1682,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   }
   if (m > 0) {  // pst_proof_h = open_g1(p_h, rs) (mipp.rs:144)
     TPST_HIP(ctx, hipStreamWaitEvent(sB, ev[EV_FINAL_UP], 0));
-    TPST_HIP(ctx, pst_open_fbt_s<Fq>(sB, arB, st, st->t_pgp.u(), st->nv - m, dWf + 16 * C, m, dWf + 24 * C,
+    TPST_HIP(ctx, pst_open_fbt_s<Fq>(sB, arB, st, st->t_pgp.u(), st->nv - m, dWim, m, dfin + 16,
                                      (Xyzz<Fq>*)xp.p, pstA.u()));
     TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(sB, (Xyzz<Fq>*)xp.p, canC.u() + 48, m));
     TPST_HIP(ctx, hipMemcpyAsync(pin + dn_final + 96 + 192, canC.u() + 48, (size_t)m * 96, hipMemcpyDeviceToHost,

@@ -41,6 +41,13 @@ hipError_t compress_fr(hipStream_t s, uint32_t* d_y, size_t split, const uint32_
 // y == nullptr: out[k] = W[k / len]; else out[k] = W[k / len] * y[(k % len + split) % len]
 hipError_t mipp_scalars(hipStream_t s, const uint32_t* d_W, const uint32_t* d_y, size_t len, size_t split, size_t n,
                         uint32_t* d_out);
+// E fold sets: out[j n + k] = canonical(W[k / len] * f[j]) (Montgomery W, f)
+hipError_t mipp_scalar_sets(hipStream_t s, const uint32_t* d_W, const uint32_t* d_f, int E, size_t len, size_t n,
+                            uint32_t* d_out);
+// round r's fold weights W_r / Wi_r (2^r Montgomery Fr at offset 2^r - 1) from
+// round r-1's and its challenge c (and c^-1), both Montgomery Fr on the device
+hipError_t mipp_weights(hipStream_t s, uint32_t* d_W, uint32_t* d_Wi, int r, const uint32_t* d_c,
+                        const uint32_t* d_cinv);
 
 // out[i] = k_i * P for a fixed affine (Montgomery) point P at d_p; scalars canonical
 template <class F>
