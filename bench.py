@@ -53,7 +53,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
 VALU_PEAK_WAVE_INSTS = 256 * 4 * 0.5 * 2.4e9  # CUs x SIMDs x (1 wave-instr / 2 cycles) x 2.4 GHz
 BYTES_PER_PAIR = 128           # 32 B scalar + 96 B affine base
 SEED = 0x7E57D0
-PMC_FILE = os.path.join(ROOT, "profiles", "r02", "pmc_bucket_acc_short.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r03", "pmc_bucket_acc_short.json")
 
 
 def parse():
@@ -108,8 +108,14 @@ def _cpu_threads():
     return n
 
 
-def fq_mults_per_madd():
-    return 12  # 8M + 2S + the modular adds ~ 2 mult-equivalents
+def fq_mults_per_madd(pmc=None):
+    """Fq-product equivalents of one XYZZ mixed add: counted (SQ_INSTS_VALU of
+    the accumulation per madd over that of the Fq-multiply microbenchmark per
+    product, tools/pmc_summary.py) when the round's PMC file holds it, else the
+    formula's 8M + 2S plus ~2 products' worth of modular adds."""
+    if pmc and pmc.get("fq_mul_equiv_per_madd"):
+        return float(pmc["fq_mul_equiv_per_madd"])
+    return 12.0
 
 
 def _max_over_ranks(dist, dev, x):
@@ -262,11 +268,14 @@ def main():
     c_bits = 16
     windows = 8  # GLV: two 127-bit halves, 8 signed 16-bit windows each
     madds = 2 * n * windows
-    achieved_fqmul = madds * fq_mults_per_madd() / (acc_avg_ms * 1e-3)
+    fq_per_madd = fq_mults_per_madd(pmc)
+    achieved_fqmul = madds * fq_per_madd / (acc_avg_ms * 1e-3)
     compute = {"bound": "valu-int32", "kernel": "k_bucket_acc_short<Fq>",
                "achieved_fq_mul_per_s": achieved_fqmul, "peak_fq_mul_per_s_measured": peak_fqmul,
                "frac": round(achieved_fqmul / peak_fqmul, 4),
-               "fq_mul_per_madd": fq_mults_per_madd()}
+               "fq_mul_per_madd": round(fq_per_madd, 3),
+               "fq_mul_per_madd_source": ("SQ_INSTS_VALU ratio, " + os.path.relpath(PMC_FILE, ROOT))
+               if pmc and pmc.get("fq_mul_equiv_per_madd") else "formula (8M + 2S + adds)"}
     if pmc and pmc.get("valu_insts_per_launch"):
         rate = pmc["valu_insts_per_launch"] / (acc_avg_ms * 1e-3)
         compute.update({"valu_wave_insts_per_launch": pmc["valu_insts_per_launch"],

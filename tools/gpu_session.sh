@@ -17,4 +17,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 $SHORT > $OUT/pmc_fetch.log 2>&1 || exit 1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 $SHORT > $OUT/pmc_write.log 2>&1 || exit 1
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES --output-format csv -d $OUT/pmc_valu -o run -- python3 $SHORT > $OUT/pmc_valu.log 2>&1 || exit 1
-cd $GRAFT_REPO_ROOT && python tools/pmc_summary.py $OUT/pmc_bucket_acc_chunk.json $OUT/pmc_fetch $OUT/pmc_write $OUT/pmc_valu > $OUT/pmc_summary.log 2>&1
+cd $GRAFT_REPO_ROOT && python tools/pmc_summary.py $OUT/pmc_bucket_acc_short.json $OUT/pmc_fetch $OUT/pmc_write $OUT/pmc_valu $OUT/prof > $OUT/pmc_summary.log 2>&1
