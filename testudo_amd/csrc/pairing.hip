@@ -734,6 +734,142 @@ hipError_t mipp_combine(hipStream_t s, Fq12* d_la8, const uint64_t* d_digits, Fq
   return hipGetLastError();
 }
 
+// ---- look-ahead combination by squaring tables ------------------------------
+// The combination t = A0 A3 A1^(c^-1) A2^c needs the four exponentiated
+// look-ahead values to 253-bit exponents, known only once c is.  Their
+// squarings do not depend on c: right after the look-ahead (off the critical
+// path) k_gt_sq_table stores S_b[k] = X_b^(2^k), k < 64, for the four bases
+// X_b = la8[MIPP_POW_SEL[b]] (63 cyclotomic squarings each, one wave per base).
+// With the base-x digits e = sum_i e_i x^i of the exponent (f^p = f^x in GT),
+//     X^e = prod_i frob^i( prod_{bit k of e_i} S[k] ),
+// a product of <= 256 table entries: k_gt_table_prod runs one workgroup per
+// (base, digit) -- 8 waves each multiply the entries of 8 bit positions, a
+// 3-level tree in LDS, then frob^i -- and two short tree levels finish
+// t_l = A0 A3 X_A1 X_A2 and t_r = B0 B3 X_B1 X_B2: ~17 wave-engine stages on the
+// critical path instead of ~140 (63 squarings + ~60 products + table).
+constexpr int SQ_OPS[] = {wave::OP_CYC_SQR};
+constexpr wave::OpSet<1> SQ_SET(SQ_OPS);
+constexpr size_t SQ_LDS = (size_t)(SQ_SET.words + (wave::N_CONSTS + 100) * wave::SLOT) * 4;
+static_assert(SQ_LDS <= 65536, "squaring-table kernel LDS");
+
+__global__ void __launch_bounds__(64) k_gt_sq_table(const Fq12* __restrict__ la8, Fq12* __restrict__ tab,
+                                                    Fq12* __restrict__ G) {
+  extern __shared__ uint4 smem4[];
+  wave::lds_t* prog = (wave::lds_t*)(smem4);
+  wave::lds_t* vals = prog + SQ_SET.words;
+  wave::load_set(prog, SQ_SET);
+  wave::load_consts(vals, 0);
+  __syncthreads();
+  const int b = blockIdx.x;
+  if (b >= 4) {  // blocks 4, 5: copy A0, A3 / B0, B3 into the final product lists
+    const int g = b - 4, lane = threadIdx.x & 63;
+    for (int t = 0; t < 2; t++)
+      if (lane < 12)
+        reinterpret_cast<Fq*>(G + g * 10 + t)[lane] = reinterpret_cast<const Fq*>(la8 + 4 * g + t)[lane];
+    return;
+  }
+  const int base = wave::N_CONSTS;
+  const wave::Eng e{vals, base, 0};
+  int cur = base + 64, nxt = base + 76;
+  wave::load_f12(vals, cur, la8 + MIPP_POW_SEL[b]);
+  Fq12* T = tab + 64 * b;
+  for (int k = 0; k < 64; k++) {
+    wave::store_f12(vals, cur, T + k);
+    if (k == 63) break;
+    wave::run(e, prog, cur, 0, nxt);
+    const int t = cur;
+    cur = nxt;
+    nxt = t;
+  }
+}
+
+constexpr int TP_WAVES = 4;
+constexpr int TP_OPS[] = {wave::OP_F12_MUL, wave::OP_FROB1, wave::OP_FROB2};
+constexpr wave::OpSet<3> TP_SET(TP_OPS);
+constexpr size_t TP_LDS = (size_t)(TP_SET.words + (wave::N_CONSTS + TP_WAVES * 100) * wave::SLOT) * 4;
+static_assert(TP_LDS <= 65536, "table-product kernel LDS");
+
+// block (b, i): G[g][2 + 4 (b % 2) + i] = frob^i( prod_{bit k of e_{b,i}} S_b[k] ),
+// g = b / 2; digits: 4 x u64 per base in MIPP_POW_SEL order.  Wave w multiplies
+// the entries of bit positions [16 w, 16 w + 16) in its three registers, then
+// a 2-level tree across the waves (operands read from the other wave's slots).
+__global__ void __launch_bounds__(64 * TP_WAVES) k_gt_table_prod(const Fq12* __restrict__ tab,
+                                                                 const uint64_t* __restrict__ digits,
+                                                                 Fq12* __restrict__ G) {
+  extern __shared__ uint4 smem4[];
+  __shared__ int acc_of[TP_WAVES];
+  wave::lds_t* prog = (wave::lds_t*)(smem4);
+  wave::lds_t* vals = prog + TP_SET.words;
+  wave::load_set(prog, TP_SET);
+  wave::load_consts(vals, 0);
+  __syncthreads();
+  const int b = blockIdx.x >> 2, i = blockIdx.x & 3, w = threadIdx.x >> 6;
+  const uint64_t e_i = digits[4 * b + i];
+  const int base = wave::N_CONSTS + w * 100;
+  const wave::Eng e{vals, base, 0};
+  auto reg = [&](int j) { return base + 64 + 12 * (j % 3); };
+  int acc = -1;  // register index 0..2 of the running product
+  const Fq12* T = tab + 64 * b;
+  constexpr int BITS = 64 / TP_WAVES;
+  for (int k = BITS * w; k < BITS * w + BITS; k++) {
+    if (!((e_i >> k) & 1)) continue;
+    if (acc < 0) {
+      acc = 0;
+      wave::load_f12(vals, reg(0), T + k);
+    } else {
+      wave::load_f12(vals, reg(acc + 1), T + k);
+      wave::run(e, prog + TP_SET.off[0], reg(acc), reg(acc + 1), reg(acc + 2));
+      acc = (acc + 2) % 3;
+    }
+  }
+  if (acc < 0) {
+    acc = 0;
+    wave::set_one(vals, reg(0));
+  }
+  if ((threadIdx.x & 63) == 0) acc_of[w] = acc;
+  __syncthreads();
+  for (int h = TP_WAVES / 2; h >= 1; h >>= 1) {
+    if (w < h) {
+      const int other = wave::N_CONSTS + (w + h) * 100 + 64 + 12 * acc_of[w + h];
+      wave::run(e, prog + TP_SET.off[0], reg(acc), other, reg(acc + 1));
+      acc = (acc + 1) % 3;
+    }
+    __syncthreads();
+    if (w < h && (threadIdx.x & 63) == 0) acc_of[w] = acc;
+    __syncthreads();
+  }
+  if (w != 0) return;
+  int r = acc;
+  if (i == 1) {
+    wave::run(e, prog + TP_SET.off[1], reg(r), 0, reg(r + 1));
+    r = (r + 1) % 3;
+  } else if (i == 2) {
+    wave::run(e, prog + TP_SET.off[2], reg(r), 0, reg(r + 1));
+    r = (r + 1) % 3;
+  } else if (i == 3) {
+    wave::run(e, prog + TP_SET.off[2], reg(r), 0, reg(r + 1));
+    wave::run(e, prog + TP_SET.off[1], reg(r + 1), 0, reg(r + 2));
+    r = (r + 2) % 3;
+  }
+  wave::store_f12(vals, reg(r), G + (b >> 1) * 10 + 2 + 4 * (b & 1) + i);
+}
+
+hipError_t mipp_sq_tables(hipStream_t s, const Fq12* d_la8, Fq12* d_tab, Fq12* d_G) {
+  k_gt_sq_table<<<6, 64, SQ_LDS, s>>>(d_la8, d_tab, d_G);
+  return hipGetLastError();
+}
+
+hipError_t mipp_combine_tab(hipStream_t s, const Fq12* d_tab, const uint64_t* d_digits, Fq12* d_G, Fq12* d_mid,
+                            Fq12* d_out2) {
+  k_gt_table_prod<<<16, 64 * TP_WAVES, TP_LDS, s>>>(d_tab, d_digits, d_G);
+  TPST_TRY(hipGetLastError());
+  // 2 groups x 10 factors -> 3 partials (chunk 4) -> 1
+  k_f12_chunk_prod<<<grid_for(2 * 3, RW), 64 * RW, RW_LDS, s>>>(d_G, 2, 10, 3, d_mid, 4);
+  TPST_TRY(hipGetLastError());
+  k_f12_chunk_prod<<<1, 64 * RW, RW_LDS, s>>>(d_mid, 2, 3, 1, d_out2, 3);
+  return hipGetLastError();
+}
+
 __global__ void k_fq12_from_mont(const Fq12* __restrict__ in, uint32_t* __restrict__ out, size_t n) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n * 12) return;

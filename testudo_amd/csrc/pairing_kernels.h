@@ -60,6 +60,13 @@ hipError_t mipp_lookahead(Arena& ar, hipStream_t s, const LineCoeff* d_coeffs, s
 // t_l = A0 A3 A1^(c^-1) A2^c, t_r = B0 B3 B1^(c^-1) B2^c.  d_digits: base-x
 // digits of (c^-1, c, c^-1, c) (4 x 4 u64); d_la8 is overwritten.
 hipError_t mipp_combine(hipStream_t s, Fq12* d_la8, const uint64_t* d_digits, Fq12* d_out2);
+// the same combination from squaring tables built off the critical path:
+// mipp_sq_tables right after the look-ahead (d_tab: 4 x 64 Fq12, d_G: 2 x 10
+// Fq12 product lists, A0 A3 / B0 B3 copied in), then once c is known
+// mipp_combine_tab (d_mid: 2 x 3 Fq12 scratch) -> d_out2 = (t_l, t_r)
+hipError_t mipp_sq_tables(hipStream_t s, const Fq12* d_la8, Fq12* d_tab, Fq12* d_G);
+hipError_t mipp_combine_tab(hipStream_t s, const Fq12* d_tab, const uint64_t* d_digits, Fq12* d_G, Fq12* d_mid,
+                            Fq12* d_out2);
 
 hipError_t fq12_from_mont(hipStream_t s, const Fq12* d_in, uint32_t* d_out, size_t n);
 

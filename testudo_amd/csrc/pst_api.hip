@@ -1381,7 +1381,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   // ---- device buffers (allocated before any stream runs: no hipFree mid-open)
   const size_t Ch = C > 1 ? C / 2 : 1;
   DevBuf up, A, P, Y, chiC, ScA, ScB, ScC, ScD[2], xa, xb, xd, xh, xp, xl[2], LAo[2], Hb[2], Lb[2], gts, canA, canB,
-      canC, canD, pstA, pstB, Wall, Wiall;
+      canC, canD, pstA, pstB, Wall, Wiall, SqT[2], SqG[2], SqM;
   TPST_HIP(ctx, up.alloc(up_bytes));
   TPST_HIP(ctx, Wall.alloc(2 * C * 32));  // round r's 2^r fold weights at offset 2^r - 1
   TPST_HIP(ctx, Wiall.alloc(2 * C * 32));
@@ -1406,7 +1406,10 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     TPST_HIP(ctx, ScD[i].alloc(8 * C * 32));
     TPST_HIP(ctx, xl[i].alloc(C * sizeof(Xyzz<Fq>)));
     TPST_HIP(ctx, LAo[i].alloc(8 * sizeof(Fq12)));
+    TPST_HIP(ctx, SqT[i].alloc(4 * 64 * sizeof(Fq12)));
+    TPST_HIP(ctx, SqG[i].alloc(2 * 10 * sizeof(Fq12)));
   }
+  TPST_HIP(ctx, SqM.alloc(2 * 3 * sizeof(Fq12)));
   TPST_HIP(ctx, canA.alloc(2 * 576));
   TPST_HIP(ctx, canB.alloc(2 * 96));
   TPST_HIP(ctx, canC.alloc((size_t)(m + 1) * 192));
@@ -1511,7 +1514,8 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
       TPST_HIP(ctx, multi_pairing_prepared(arA, sA, P.u(), H0, L0, 2, s, (Fq12*)gts.p, true, s, 0));
     } else {  // round r-1's look-ahead products, combined with c_{r-1}
       TPST_HIP(ctx, hipStreamWaitEvent(sA, ev_la(r - 1), 0));
-      TPST_HIP(ctx, mipp_combine(sA, (Fq12*)LAo[(r - 1) & 1].p, ddig, (Fq12*)gts.p));
+      TPST_HIP(ctx, mipp_combine_tab(sA, (Fq12*)SqT[(r - 1) & 1].p, ddig, (Fq12*)SqG[(r - 1) & 1].p,
+                                     (Fq12*)SqM.p, (Fq12*)gts.p));
     }
     TPST_HIP(ctx, fq12_from_mont(sA, (Fq12*)gts.p, canA.u(), 2));
     uint8_t* dn_r = pin + dn_round + (size_t)r * (192 + 1152);
@@ -1551,6 +1555,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
         TPST_HIP(ctx, mipp_lookahead(arD, sD, lp, (size_t)E * len, hp, xl[r & 1].u(), true, len, E,
                                      (Fq12*)LAo[r & 1].p));
       }
+      TPST_HIP(ctx, mipp_sq_tables(sD, (Fq12*)LAo[r & 1].p, (Fq12*)SqT[r & 1].p, (Fq12*)SqG[r & 1].p));
       TPST_HIP(ctx, hipEventRecord(ev_la(r), sD));
     }
 
