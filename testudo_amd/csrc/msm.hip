@@ -5,6 +5,7 @@
 #include "device_util.h"
 #include "coop.h"
 #include "msm.h"
+#include "pair_fq2.h"
 #include <type_traits>
 
 namespace tpst {
@@ -367,6 +368,75 @@ __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
     key = key_n;
     pt = pt_n;
   }
+}
+
+// k_bucket_acc_short over G2 with pair-distributed Fq2 (pair_fq2.h): lanes
+// 2t and 2t+1 run chunk t's bucket chain together, each holding one Fq
+// coordinate of every Fq2 value; same chunking, parking and bucket stores.
+static __device__ __forceinline__ Affine<Fq2P> fetch_point_pair(const uint32_t* bases, const uint32_t* phib, uint32_t nbase,
+                                                        uint32_t v) {
+  const uint32_t idx = v & 0x7fffffffu;
+  Affine<Fq2P> p = (idx < nbase) ? load_affine_pair(bases, idx) : load_affine_pair(phib, idx - nbase);
+  if (v >> 31) p.y = neg(p.y);
+  return p;
+}
+
+static __global__ void __launch_bounds__(64, 2)
+    k_bucket_acc_short_pair(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                            const uint32_t* __restrict__ range, int wlo, int whi, uint32_t sent,
+                            const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend,
+                            const uint32_t* __restrict__ bases, const uint32_t* __restrict__ phib, uint32_t nbase,
+                            int lg, Xyzz<Fq2>* __restrict__ buckets, Xyzz<Fq2>* __restrict__ part) {
+  const size_t e_lo = range[wlo], e_hi = range[whi];
+  const size_t t = (e_lo >> lg) + (((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 1);
+  size_t c0 = t << lg;
+  if (c0 >= e_hi) return;  // pair-uniform
+  const size_t c1 = (c0 + ((size_t)1 << lg) < e_hi) ? c0 + ((size_t)1 << lg) : e_hi;
+  if (c0 < e_lo) c0 = e_lo;
+  uint32_t key = keys[c0];
+  Affine<Fq2P> pt;
+  if (key < sent) pt = fetch_point_pair(bases, phib, nbase, vals[c0]);
+  Xyzz<Fq2P> acc = Xyzz<Fq2P>::inf();
+  for (size_t e = c0; e < c1; e++) {
+    uint32_t key_n = sent;
+    Affine<Fq2P> pt_n;
+    if (e + 1 < c1) {
+      key_n = keys[e + 1];
+      if (key_n < sent) pt_n = fetch_point_pair(bases, phib, nbase, vals[e + 1]);
+    }
+    if (key < sent) {
+      acc = add_affine(acc, pt);
+      if (key_n != key) {
+        const bool starts = bstart[key] >= c0;
+        const bool ends = bend[key] <= c1;
+        if (starts && ends)
+          store_xyzz_pair(buckets, key, acc);
+        else
+          store_xyzz_pair(part, 2 * t + (starts ? 1 : 0), acc);
+        acc = Xyzz<Fq2P>::inf();
+      }
+    }
+    key = key_n;
+    pt = pt_n;
+  }
+}
+
+// k_bucket_fixup_short over G2 with pair-distributed Fq2: lanes 2b, 2b+1
+// finish bucket b0 + b together
+static __global__ void __launch_bounds__(64, 2)
+    k_bucket_fixup_short_pair(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend, size_t b0,
+                              size_t b1, int lg, const Xyzz<Fq2>* __restrict__ part, Xyzz<Fq2>* __restrict__ buckets,
+                              int prio) {
+  set_wave_prio(prio);
+  const size_t b = b0 + (((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 1);
+  if (b >= b1) return;
+  const uint32_t s = bstart[b], e = bend[b];
+  if (e <= s) return;
+  const size_t t0 = (size_t)s >> lg, t1 = (size_t)(e - 1) >> lg;
+  if (t0 == t1) return;
+  Xyzz<Fq2P> acc = load_xyzz_pair(part, 2 * t0 + 1);
+  for (size_t t = t0 + 1; t <= t1; t++) acc = add(acc, load_xyzz_pair(part, 2 * t));
+  store_xyzz_pair(buckets, b, acc);
 }
 
 // buckets crossing chunk boundaries: trailing piece of the first chunk plus
@@ -752,6 +822,17 @@ static void msm_group_bounds(int W, int NG, int* wb) {
   for (int g = 0; g < NG; g++) wb[g + 1] = wb[g] + cnt[g];
 }
 
+// G2 window (TPST_G2_WINDOW overrides, for sweeps): a G2 bucket costs ~3x a G1
+// one in the fixup / reduction passes, so fewer, fuller buckets can pay for
+// the extra window of entries
+static int g2_window_bits(int c) {
+  static const int env = [] {
+    const char* e = getenv("TPST_G2_WINDOW");
+    return e ? atoi(e) : 0;
+  }();
+  return (env >= 4 && env <= 16) ? env : c;
+}
+
 template <class F>
 hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint32_t* d_scalars, size_t n,
                    Xyzz<F>* d_out) {
@@ -762,7 +843,8 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   if (n > MSM_MAX_POINTS) return hipErrorInvalidValue;
   const bool glv = n >= 64;  // phi(x, y) = (beta x, y) on G1, (beta^2 x, y) on G2
   constexpr size_t PW = 2 * Words<F>::n;
-  const int c = msm_window_bits(glv ? 2 * n : n);
+  int c = msm_window_bits(glv ? 2 * n : n);
+  if constexpr (std::is_same<F, Fq2>::value) c = g2_window_bits(c);
   const int W = glv ? num_windows_bits(c, 128) : num_windows(c);
   const uint32_t nb = 1u << (c - 1);
   const size_t per_win = (size_t)(glv ? 2 : 1) * n;  // entries of one window (zero digits included)
@@ -869,9 +951,15 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   for (int g = NG - 1; g >= 0; g--) {  // top windows first: their chains are the longest
     const int wlo = wb[g], whi = wb[g + 1];
     const size_t gchunks = ((per_win * (size_t)(whi - wlo)) >> lg) + 2;
-    k_bucket_acc_short<F><<<grid_for(gchunks, 64), 64, 0, bulk>>>(keys2, vals2, range, wlo, whi, sent, bstart,
-                                                                   bend, d_bases, phib, (uint32_t)n, lg, buckets,
-                                                                   part);
+    if constexpr (std::is_same<F, Fq2>::value) {
+      k_bucket_acc_short_pair<<<grid_for(2 * gchunks, 64), 64, 0, bulk>>>(keys2, vals2, range, wlo, whi, sent,
+                                                                          bstart, bend, d_bases, phib, (uint32_t)n,
+                                                                          lg, buckets, part);
+    } else {
+      k_bucket_acc_short<F><<<grid_for(gchunks, 64), 64, 0, bulk>>>(keys2, vals2, range, wlo, whi, sent, bstart,
+                                                                     bend, d_bases, phib, (uint32_t)n, lg, buckets,
+                                                                     part);
+    }
     TPST_TRY(hipGetLastError());
     if (g == 0) pf->end(ST_BUCKET_ACC, bulk);
     const size_t b0 = (size_t)wlo * nb, b1 = (size_t)whi * nb;
@@ -880,8 +968,12 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
       TPST_TRY(hipEventRecord(ar.aux_ev[2 * g], bulk));
       TPST_TRY(hipStreamWaitEvent(a, ar.aux_ev[2 * g], 0));
     }
-    k_bucket_fixup_short<F><<<grid_for(b1 - b0, 64), 64, 0, a>>>(bstart, bend, b0, b1, lg, part, buckets,
-                                                                  g ? red_prio() : 0);
+    if constexpr (std::is_same<F, Fq2>::value)
+      k_bucket_fixup_short_pair<<<grid_for(2 * (b1 - b0), 64), 64, 0, a>>>(bstart, bend, b0, b1, lg, part, buckets,
+                                                                          g ? red_prio() : 0);
+    else
+      k_bucket_fixup_short<F><<<grid_for(b1 - b0, 64), 64, 0, a>>>(bstart, bend, b0, b1, lg, part, buckets,
+                                                                    g ? red_prio() : 0);
     TPST_TRY(hipGetLastError());
     if (g == 0) break;
     if (red2_mode() >= 1 && red2_ok(nb))

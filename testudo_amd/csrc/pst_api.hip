@@ -62,44 +62,64 @@ const HostP64& hp64() {
   return h;
 }
 
+// no-carry CIOS (p's top word < 2^62: the running value fits 6 words + the
+// carry word of each row), fully unrolled over the 6 words of b
 Fq hmul(const Fq& a, const Fq& b) {
   typedef unsigned __int128 u128;
   const HostP64& P = hp64();
-  uint64_t x[6], y[6], t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t x[6], y[6];
   memcpy(x, a.v, 48);
   memcpy(y, b.v, 48);
-  for (int i = 0; i < 6; i++) {
-    u128 c = 0;
-    for (int j = 0; j < 6; j++) {
-      c += (u128)x[j] * y[i] + t[j];
-      t[j] = (uint64_t)c;
-      c >>= 64;
-    }
-    c += t[6];
-    t[6] = (uint64_t)c;
-    t[7] = (uint64_t)(c >> 64);
-    const uint64_t m = t[0] * P.inv;
-    c = ((u128)m * P.p[0] + t[0]) >> 64;
-    for (int j = 1; j < 6; j++) {
-      c += (u128)m * P.p[j] + t[j];
-      t[j - 1] = (uint64_t)c;
-      c >>= 64;
-    }
-    c += t[6];
-    t[5] = (uint64_t)c;
-    t[6] = t[7] + (uint64_t)(c >> 64);
+  uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0, t5 = 0;
+#define TPST_HMUL_ROW(i)                                                              \
+  {                                                                                   \
+    const uint64_t yi = y[i];                                                         \
+    u128 c = (u128)x[0] * yi + t0;                                                    \
+    const uint64_t a0 = (uint64_t)c;                                                  \
+    uint64_t A = (uint64_t)(c >> 64);                                                 \
+    const uint64_t m = a0 * P.inv;                                                    \
+    u128 d = (u128)m * P.p[0] + a0;                                                   \
+    uint64_t C = (uint64_t)(d >> 64);                                                 \
+    c = (u128)x[1] * yi + t1 + A;                                                     \
+    A = (uint64_t)(c >> 64);                                                          \
+    d = (u128)m * P.p[1] + (uint64_t)c + C;                                           \
+    C = (uint64_t)(d >> 64);                                                          \
+    t0 = (uint64_t)d;                                                                 \
+    c = (u128)x[2] * yi + t2 + A;                                                     \
+    A = (uint64_t)(c >> 64);                                                          \
+    d = (u128)m * P.p[2] + (uint64_t)c + C;                                           \
+    C = (uint64_t)(d >> 64);                                                          \
+    t1 = (uint64_t)d;                                                                 \
+    c = (u128)x[3] * yi + t3 + A;                                                     \
+    A = (uint64_t)(c >> 64);                                                          \
+    d = (u128)m * P.p[3] + (uint64_t)c + C;                                           \
+    C = (uint64_t)(d >> 64);                                                          \
+    t2 = (uint64_t)d;                                                                 \
+    c = (u128)x[4] * yi + t4 + A;                                                     \
+    A = (uint64_t)(c >> 64);                                                          \
+    d = (u128)m * P.p[4] + (uint64_t)c + C;                                           \
+    C = (uint64_t)(d >> 64);                                                          \
+    t3 = (uint64_t)d;                                                                 \
+    c = (u128)x[5] * yi + t5 + A;                                                     \
+    A = (uint64_t)(c >> 64);                                                          \
+    d = (u128)m * P.p[5] + (uint64_t)c + C;                                           \
+    C = (uint64_t)(d >> 64);                                                          \
+    t4 = (uint64_t)d;                                                                 \
+    t5 = C + A;                                                                       \
   }
+  TPST_HMUL_ROW(0) TPST_HMUL_ROW(1) TPST_HMUL_ROW(2) TPST_HMUL_ROW(3) TPST_HMUL_ROW(4) TPST_HMUL_ROW(5)
+#undef TPST_HMUL_ROW
   // t < 2p: one conditional subtraction
+  const uint64_t t[6] = {t0, t1, t2, t3, t4, t5};
   uint64_t r[6];
   u128 br = 0;
   for (int j = 0; j < 6; j++) {
-    const u128 d = (u128)t[j] - P.p[j] - (uint64_t)br;
-    r[j] = (uint64_t)d;
-    br = (d >> 64) & 1;
+    const u128 dd = (u128)t[j] - P.p[j] - (uint64_t)br;
+    r[j] = (uint64_t)dd;
+    br = (dd >> 64) & 1;
   }
-  const bool ge = t[6] || !br;
   Fq out;
-  memcpy(out.v, ge ? r : t, 48);
+  memcpy(out.v, br ? t : r, 48);
   return out;
 }
 
