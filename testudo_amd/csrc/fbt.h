@@ -17,6 +17,7 @@ namespace tpst {
 constexpr int FBT_C = 4;   // window bits (signed digits in [-8, 8])
 constexpr int FBT_W = 64;  // windows: 64 * 4 >= 253 + carry
 constexpr int FBT_M = 8;   // multiples per window
+constexpr int FBT_WG = 32;  // GLV tables (G1): windows of the two 127-bit halves
 
 template <class F>
 constexpr size_t fbt_entries(size_t n) { return n * FBT_W * FBT_M; }
@@ -24,8 +25,12 @@ template <class F>
 constexpr size_t fbt_words(size_t n) { return fbt_entries<F>(n) * 2 * Words<F>::n; }
 
 // Build the table of n affine Montgomery bases into d_table (fbt_words(n) u32).
+// glv (G1 only): windows w < 32 only -- a scalar is split k = k1 + lambda k2
+// (both < 2^127) and k2's digits look up phi(T) = (beta x, y) = lambda T, so
+// the same 64 lookups per scalar need half the table and half the doublings.
 template <class F>
-hipError_t fbt_build(Arena& ar, hipStream_t s, const uint32_t* d_bases, size_t n, uint32_t* d_table);
+hipError_t fbt_build(Arena& ar, hipStream_t s, const uint32_t* d_bases, size_t n, uint32_t* d_table,
+                     bool glv = false);
 
 // Grouped fixed-base MSM: out[g] = sum_{k in group g} S_k * B_k, S canonical
 // Fr indexed by base.  Membership:
@@ -41,6 +46,7 @@ struct FbGroups {
   size_t L = 1, D = 1;
   const uint32_t* d_seg = nullptr;
   size_t sets = 1, set_stride = 0;
+  bool glv = false;  // the table was built with glv = true
 };
 
 template <class F>

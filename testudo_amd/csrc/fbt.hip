@@ -1,6 +1,7 @@
 // Fixed-base lookup tables + grouped fixed-base MSM (see fbt.h).
 #include "coop.h"
 #include "fbt.h"
+#include "glv.h"
 
 namespace tpst {
 
@@ -33,15 +34,15 @@ __global__ void __launch_bounds__(64) k_fbt_pow(const uint32_t* __restrict__ bas
 // the same chain on a quad of lanes per base (coop.h): 3 product latencies
 // per doubling instead of 9
 template <class F>
-__global__ void __launch_bounds__(64) k_fbt_pow_quad(const uint32_t* __restrict__ bases, size_t n,
+__global__ void __launch_bounds__(64) k_fbt_pow_quad(const uint32_t* __restrict__ bases, size_t n, int nw,
                                                      Xyzz<F>* __restrict__ tmp) {
   const size_t k = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
   const int qi = threadIdx.x & 3;
   if (k >= n) return;  // quad-uniform
   Xyzz<F> p = to_xyzz(load_affine<F>(bases, k));
-  for (int w = 0; w < FBT_W; w++) {
-    if (qi == 0) store_xyzz(tmp, k * FBT_W + w, p);
-    if (w + 1 < FBT_W) {
+  for (int w = 0; w < nw; w++) {
+    if (qi == 0) store_xyzz(tmp, k * nw + w, p);
+    if (w + 1 < nw) {
       p = dbl_quad(p, qi);
       p = dbl_quad(p, qi);
       p = dbl_quad(p, qi);
@@ -55,14 +56,14 @@ __global__ void __launch_bounds__(64) k_fbt_pow_quad(const uint32_t* __restrict_
 // batch trick over d_m = ZZ_m ZZZ_m; the multiples are recomputed for the
 // output pass instead of being held in registers)
 template <class F>
-__global__ void __launch_bounds__(64) k_fbt_mult8(const Xyzz<F>* __restrict__ tmp, size_t n,
+__global__ void __launch_bounds__(64) k_fbt_mult8(const Xyzz<F>* __restrict__ tmp, size_t n, int nw,
                                                   uint32_t* __restrict__ table) {
   // d_m and the prefix products live in LDS (a lane's column), not in
   // dynamically indexed registers
   __shared__ F sd[FBT_M][64], spre[FBT_M][64];
   const int l = threadIdx.x;
   const size_t i = (size_t)blockIdx.x * blockDim.x + l;
-  if (i >= n * FBT_W) return;
+  if (i >= n * (size_t)nw) return;
   const Xyzz<F> P = load_xyzz(tmp, i);
   Xyzz<F> q = P;
   F pre = F::one();
@@ -109,16 +110,18 @@ __global__ void __launch_bounds__(64) k_fbt_mult(const Xyzz<F>* __restrict__ tmp
 }
 
 template <class F>
-hipError_t fbt_build(Arena& ar, hipStream_t s, const uint32_t* d_bases, size_t n, uint32_t* d_table) {
+hipError_t fbt_build(Arena& ar, hipStream_t s, const uint32_t* d_bases, size_t n, uint32_t* d_table, bool glv) {
   if (!n) return hipSuccess;
   ar.reset();
   TPST_TRY(ar.reserve(Arena::need(n * FBT_W, sizeof(Xyzz<F>))));
   Xyzz<F>* tmp = ar.take<Xyzz<F>>(n * FBT_W);
   if constexpr (sizeof(F) == sizeof(Fq)) {  // G1 (timed: the opening's comm_list table)
-    k_fbt_pow_quad<F><<<fbt_grid(4 * n, 64), 64, 0, s>>>(d_bases, n, tmp);
+    const int nw = glv ? FBT_WG : FBT_W;
+    k_fbt_pow_quad<F><<<fbt_grid(4 * n, 64), 64, 0, s>>>(d_bases, n, nw, tmp);
     TPST_TRY(hipGetLastError());
-    k_fbt_mult8<F><<<fbt_grid(n * FBT_W, 64), 64, 0, s>>>(tmp, n, d_table);
+    k_fbt_mult8<F><<<fbt_grid(n * nw, 64), 64, 0, s>>>(tmp, n, nw, d_table);
   } else {  // G2 tables are built once per SRS
+    if (glv) return hipErrorInvalidValue;
     k_fbt_pow<F><<<fbt_grid(n, 64), 64, 0, s>>>(d_bases, n, tmp);
     TPST_TRY(hipGetLastError());
     k_fbt_mult<F><<<fbt_grid(fbt_entries<F>(n), 64), 64, 0, s>>>(tmp, n, d_table);
@@ -162,13 +165,34 @@ __global__ void __launch_bounds__(64) k_fbt_partial_quad(const uint32_t* __restr
     const uint4 a = sp[0], b = sp[1];
     s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w;
     s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
+    // GLV table: chunks 0-3 take k1's windows from T, chunks 4-7 k2's from
+    // phi(T) = (beta x, y)
+    int wb = 8 * ch, nw = FBT_W;
+    bool phi = false;
+    if constexpr (sizeof(F) == sizeof(Fq)) {
+      if (gr.glv) {
+        uint32_t k1[4], k2[4];
+        glv_split(s, k1, k2);
+        phi = ch >= 4;
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+          s[t] = phi ? k2[t] : k1[t];
+          s[4 + t] = 0;
+        }
+        wb = 8 * (ch & 3);
+        nw = FBT_WG;
+      }
+    }
     int carry = 0;
-    for (int w = 0; w < 8 * ch; w++) fbt_digit(s, w, carry);
+    for (int w = 0; w < wb; w++) fbt_digit(s, w, carry);
     for (int j = 0; j < 8; j++) {
-      const int w = 8 * ch + j;
+      const int w = wb + j;
       const int d = fbt_digit(s, w, carry);
       if (d) {
-        Affine<F> t = load_affine<F>(table, (k * FBT_W + w) * FBT_M + (d < 0 ? -d : d) - 1);
+        Affine<F> t = load_affine<F>(table, (k * nw + w) * FBT_M + (d < 0 ? -d : d) - 1);
+        if constexpr (sizeof(F) == sizeof(Fq)) {
+          if (phi) t.x = mul(t.x, Fq::from_limbs(params::G1_BETA));
+        }
         if (d < 0) t = neg(t);
         acc = add_affine_quad(acc, t, qi);
       }
@@ -236,8 +260,8 @@ hipError_t fbt_msm(Arena& ar, hipStream_t s, const uint32_t* d_table, const uint
   return hipMemcpyAsync(d_out, a, G * sizeof(Xyzz<F>), hipMemcpyDeviceToDevice, s);
 }
 
-template hipError_t fbt_build<Fq>(Arena&, hipStream_t, const uint32_t*, size_t, uint32_t*);
-template hipError_t fbt_build<Fq2>(Arena&, hipStream_t, const uint32_t*, size_t, uint32_t*);
+template hipError_t fbt_build<Fq>(Arena&, hipStream_t, const uint32_t*, size_t, uint32_t*, bool);
+template hipError_t fbt_build<Fq2>(Arena&, hipStream_t, const uint32_t*, size_t, uint32_t*, bool);
 template hipError_t fbt_msm<Fq>(Arena&, hipStream_t, const uint32_t*, const uint32_t*, const FbGroups&, Xyzz<Fq>*);
 template hipError_t fbt_msm<Fq2>(Arena&, hipStream_t, const uint32_t*, const uint32_t*, const FbGroups&, Xyzz<Fq2>*);
 

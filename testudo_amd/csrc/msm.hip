@@ -6,6 +6,7 @@
 #include "coop.h"
 #include "msm.h"
 #include "pair_fq2.h"
+#include "glv.h"
 #include <type_traits>
 
 namespace tpst {
@@ -83,66 +84,6 @@ __device__ __forceinline__ void load_scalar(const uint32_t* p, uint32_t* s) {
   const uint4 a = q[0], b = q[1];
   s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w;
   s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
-}
-
-// GLV split k = k1 + k2 * lambda (lambda = x^2 - 1, 127 bits), both halves
-// < 2^127: k2 = floor(k * mu / 2^256) (+1 correction), k1 = k - k2 * lambda
-__device__ __forceinline__ void glv_split(const uint32_t* k, uint32_t* k1, uint32_t* k2) {
-  uint32_t prod[13];
-#pragma unroll
-  for (int i = 0; i < 13; i++) prod[i] = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    uint64_t carry = 0;
-#pragma unroll
-    for (int j = 0; j < 5; j++) {
-      const uint64_t t = (uint64_t)k[i] * params::GLV_MU[j] + prod[i + j] + carry;
-      prod[i + j] = (uint32_t)t;
-      carry = t >> 32;
-    }
-    prod[i + 5] = (uint32_t)carry;
-  }
-  uint32_t q[4] = {prod[8], prod[9], prod[10], prod[11]};
-  uint32_t ql[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) ql[i] = 0;
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    uint64_t carry = 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const uint64_t t = (uint64_t)q[i] * params::GLV_LAMBDA[j] + ql[i + j] + carry;
-      ql[i + j] = (uint32_t)t;
-      carry = t >> 32;
-    }
-    ql[i + 4] = (uint32_t)carry;
-  }
-  uint32_t r[4];
-  int64_t br = 0;
-#pragma unroll
-  for (int i = 0; i < 4; i++) {  // k - q*lambda < 2*lambda < 2^128
-    const int64_t d = (int64_t)k[i] - ql[i] + br;
-    r[i] = (uint32_t)d;
-    br = d >> 32;
-  }
-  // r >= lambda ?  -> subtract once more
-  uint32_t s[4];
-  br = 0;
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const int64_t d = (int64_t)r[i] - params::GLV_LAMBDA[i] + br;
-    s[i] = (uint32_t)d;
-    br = d >> 32;
-  }
-  const bool ge = (br == 0);
-  uint64_t c = ge ? 1 : 0;
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    k1[i] = ge ? s[i] : r[i];
-    c += q[i];
-    k2[i] = (uint32_t)c;
-    c >>= 32;
-  }
 }
 
 // wave issue priority on its SIMD (s_setprio): the latency-bound reduction and
@@ -844,7 +785,15 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   const bool glv = n >= 64;  // phi(x, y) = (beta x, y) on G1, (beta^2 x, y) on G2
   constexpr size_t PW = 2 * Words<F>::n;
   int c = msm_window_bits(glv ? 2 * n : n);
-  if constexpr (std::is_same<F, Fq2>::value) c = g2_window_bits(c);
+  if constexpr (std::is_same<F, Fq2>::value) {
+    c = g2_window_bits(c);
+  } else {
+    static const int env_c = [] {  // TPST_MSM_C: G1 window override (sweeps)
+      const char* e = getenv("TPST_MSM_C");
+      return e ? atoi(e) : 0;
+    }();
+    if (env_c >= 4 && env_c <= 22 && n >= 64) c = env_c;
+  }
   const int W = glv ? num_windows_bits(c, 128) : num_windows(c);
   const uint32_t nb = 1u << (c - 1);
   const size_t per_win = (size_t)(glv ? 2 : 1) * n;  // entries of one window (zero digits included)

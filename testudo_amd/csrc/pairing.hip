@@ -234,9 +234,16 @@ __global__ void __launch_bounds__(64 * RW) k_f12_chunk_prod(const Fq12* __restri
   const int base = wave::N_CONSTS + w * RW_SLOTS;
   const wave::Eng e{vals, base, 0};
   int acc = base + 64, in_r = base + 76, tmp = base + 88;
+  // the next factor's global load is issued before the current product runs
+  // (12 lanes hold it in VGPRs), so its latency hides under the stage
+  const int lane = threadIdx.x & 63;
+  const Fq* src = reinterpret_cast<const Fq*>(in + g * n);
   wave::load_f12(vals, acc, in + g * n + k0);
+  Fq nxt = lane < 12 && k0 + 1 < k1 ? src[12 * (k0 + 1) + lane] : Fq::zero();
   for (size_t k = k0 + 1; k < k1; k++) {
-    wave::load_f12(vals, in_r, in + g * n + k);
+    if (lane < 12) wave::put_slot(vals, in_r + lane, nxt);
+    wave::wave_sync();
+    if (lane < 12 && k + 1 < k1) nxt = src[12 * (k + 1) + lane];
     wave::run(e, prog + RW_SET.off[0], acc, in_r, tmp);
     const int t = acc;
     acc = tmp;

@@ -1459,7 +1459,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   for (hipStream_t s2 : {sB, sLA[0], sLA[1]}) TPST_HIP(ctx, hipStreamWaitEvent(s2, ev[EV_PRE], 0));
 
   // ---- look-ahead stream 1 (idle until round 1): the fold table over comm_list
-  TPST_HIP(ctx, fbt_build<Fq>(*arLA[1], sLA[1], A.u(), C, st->t_A.u()));
+  TPST_HIP(ctx, fbt_build<Fq>(*arLA[1], sLA[1], A.u(), C, st->t_A.u(), true));
   TPST_HIP(ctx, hipEventRecord(ev[EV_TABLE], sLA[1]));
   // ---- stream B: U = MSM(comm_list, chi(b)) on that table, or the c_u the
   // ranks combined for an opening-only handle
@@ -1471,6 +1471,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     FbGroups gu;
     gu.members = C;
     gu.L = gu.D = C;
+    gu.glv = true;
     TPST_HIP(ctx, fbt_msm<Fq>(arB, sB, tA, chiC.u(), gu, (Xyzz<Fq>*)xd.p));
     TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(sB, (Xyzz<Fq>*)xd.p, canD.u(), 1));
     TPST_HIP(ctx, hipMemcpyAsync(pin + dn_U, canD.p, 96, hipMemcpyDeviceToHost, sB));
@@ -1563,6 +1564,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
         g.D = 1;
         g.sets = (size_t)E;
         g.set_stride = C;
+        g.glv = true;
         TPST_HIP(ctx, fbt_msm<Fq>(arD, sD, tA, sc, g, (Xyzz<Fq>*)xl[r & 1].p));
         const int src = la_src(r);  // h^(0), or h^(src) prepared by stream C in round src
         const uint32_t* hp = H0;
@@ -1591,6 +1593,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
       g.members = C / len * s;
       g.L = len;
       g.D = s;
+      g.glv = true;
       TPST_HIP(ctx, fbt_msm<Fq>(arB, sB, tA, ScB.u(), g, (Xyzz<Fq>*)xb.p));
     }
     TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(sB, (Xyzz<Fq>*)xb.p, canB.u(), 2));
@@ -1691,6 +1694,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     FbGroups g;
     g.members = C;
     TPST_HIP(ctx, mipp_scalars(sA, dWm, nullptr, 1, 0, C, ScA.u()));
+    g.glv = true;
     TPST_HIP(ctx, fbt_msm<Fq>(arA, sA, tA, ScA.u(), g, (Xyzz<Fq>*)xa.p));
     TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(sA, (Xyzz<Fq>*)xa.p, canA.u(), 1));
     TPST_HIP(ctx, hipMemcpyAsync(pin + dn_final, canA.p, 96, hipMemcpyDeviceToHost, sA));
