@@ -399,6 +399,26 @@ __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
   store_xyzz(buckets, b, acc);
 }
 
+// the same fixup, one quad of lanes per bucket (coop.h: 4 product latencies
+// per addition instead of ~14): for the last window group, whose fixup sits on
+// the MSM's tail with one lone lane per bucket at ~2 waves per CU
+template <class F>
+__global__ void __launch_bounds__(64) k_bucket_fixup_quad(const uint32_t* __restrict__ bstart,
+                                                          const uint32_t* __restrict__ bend, size_t b0, size_t b1,
+                                                          int lg, const Xyzz<F>* __restrict__ part,
+                                                          Xyzz<F>* __restrict__ buckets) {
+  const size_t b = b0 + (((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2);
+  const int qi = threadIdx.x & 3;
+  if (b >= b1) return;  // quad-uniform
+  const uint32_t s = bstart[b], e = bend[b];
+  if (e <= s) return;
+  const size_t t0 = (size_t)s >> lg, t1 = (size_t)(e - 1) >> lg;
+  if (t0 == t1) return;
+  Xyzz<F> acc = load_xyzz(part, 2 * t0 + 1);
+  for (size_t t = t0 + 1; t <= t1; t++) acc = add_quad(acc, load_xyzz(part, 2 * t), qi);
+  if (qi == 0) store_xyzz(buckets, b, acc);
+}
+
 // segment t of group g: sum_{b in seg} (b+1) * S_b with b the bucket index
 // inside the group (bucket b holds digit value b+1): running sums over the L
 // buckets plus (segment offset) * (segment sum).  One quad of lanes per
@@ -694,6 +714,15 @@ static hipError_t reduce_buckets2(Arena& ar, hipStream_t s, const Xyzz<F>* d_buc
   return hipGetLastError();
 }
 
+// TPST_MSM_FIXUP_QUAD=0: the last group's fixup one lane per bucket (A/B)
+static bool fixup_quad() {
+  static const bool v = [] {
+    const char* e = getenv("TPST_MSM_FIXUP_QUAD");
+    return !(e && atoi(e) == 0);
+  }();
+  return v;
+}
+
 // TPST_MSM_PRIO: s_setprio level of the aux-stream reductions (default 2)
 static int red_prio() {
   static const int v = [] {
@@ -920,6 +949,8 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
     if constexpr (std::is_same<F, Fq2>::value)
       k_bucket_fixup_short_pair<<<grid_for(2 * (b1 - b0), 64), 64, 0, a>>>(bstart, bend, b0, b1, lg, part, buckets,
                                                                           g ? red_prio() : 0);
+    else if (g == 0 && fixup_quad())
+      k_bucket_fixup_quad<F><<<grid_for(4 * (b1 - b0), 64), 64, 0, a>>>(bstart, bend, b0, b1, lg, part, buckets);
     else
       k_bucket_fixup_short<F><<<grid_for(b1 - b0, 64), 64, 0, a>>>(bstart, bend, b0, b1, lg, part, buckets,
                                                                     g ? red_prio() : 0);

@@ -759,26 +759,44 @@ constexpr wave::OpSet<1> SQ_SET(SQ_OPS);
 constexpr size_t SQ_LDS = (size_t)(SQ_SET.words + (wave::N_CONSTS + 100) * wave::SLOT) * 4;
 static_assert(SQ_LDS <= 65536, "squaring-table kernel LDS");
 
-__global__ void __launch_bounds__(64) k_gt_sq_table(const Fq12* __restrict__ la8, Fq12* __restrict__ tab,
-                                                    Fq12* __restrict__ G) {
+// tables of the bases src[sel[b]], b < n (one wave each); blocks n.. copy
+// src[cp.src[j]] (or 1 when cp.src[j] < 0) to dst[cp.dst[j]]
+struct SqPlan {
+  int n;
+  int sel[12];
+};
+struct CopyPlan {
+  int n;
+  int src[12], dst[12];
+};
+
+__global__ void __launch_bounds__(64) k_gt_sq_table(const Fq12* __restrict__ src, SqPlan sp, Fq12* __restrict__ tab,
+                                                    CopyPlan cp, Fq12* __restrict__ dst) {
   extern __shared__ uint4 smem4[];
   wave::lds_t* prog = (wave::lds_t*)(smem4);
   wave::lds_t* vals = prog + SQ_SET.words;
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  if (b >= sp.n) {  // the copies
+    for (int j = 0; j < cp.n; j++)
+      if (lane < 12) {
+        Fq v = Fq::zero();
+        if (cp.src[j] < 0) {
+          if (lane == 0) v = Fq::one();
+        } else {
+          v = reinterpret_cast<const Fq*>(src + cp.src[j])[lane];
+        }
+        reinterpret_cast<Fq*>(dst + cp.dst[j])[lane] = v;
+      }
+    return;
+  }
   wave::load_set(prog, SQ_SET);
   wave::load_consts(vals, 0);
   __syncthreads();
-  const int b = blockIdx.x;
-  if (b >= 4) {  // blocks 4, 5: copy A0, A3 / B0, B3 into the final product lists
-    const int g = b - 4, lane = threadIdx.x & 63;
-    for (int t = 0; t < 2; t++)
-      if (lane < 12)
-        reinterpret_cast<Fq*>(G + g * 10 + t)[lane] = reinterpret_cast<const Fq*>(la8 + 4 * g + t)[lane];
-    return;
-  }
   const int base = wave::N_CONSTS;
   const wave::Eng e{vals, base, 0};
   int cur = base + 64, nxt = base + 76;
-  wave::load_f12(vals, cur, la8 + MIPP_POW_SEL[b]);
+  wave::load_f12(vals, cur, src + sp.sel[b]);
   Fq12* T = tab + 64 * b;
   for (int k = 0; k < 64; k++) {
     wave::store_f12(vals, cur, T + k);
@@ -796,12 +814,18 @@ constexpr wave::OpSet<3> TP_SET(TP_OPS);
 constexpr size_t TP_LDS = (size_t)(TP_SET.words + (wave::N_CONSTS + TP_WAVES * 100) * wave::SLOT) * 4;
 static_assert(TP_LDS <= 65536, "table-product kernel LDS");
 
-// block (b, i): G[g][2 + 4 (b % 2) + i] = frob^i( prod_{bit k of e_{b,i}} S_b[k] ),
-// g = b / 2; digits: 4 x u64 per base in MIPP_POW_SEL order.  Wave w multiplies
-// the entries of bit positions [16 w, 16 w + 16) in its three registers, then
-// a 2-level tree across the waves (operands read from the other wave's slots).
+// block (b, i): G[tp.out[b] + i] = frob^i( prod_{bit k of e_{b,i}} S_b[k] ),
+// e_{b,i} = digits[4 tp.dig[b] + i] (base-x digits, 4 x u64 per exponent).
+// Wave w multiplies the entries of bit positions [16 w, 16 w + 16) in its
+// three registers, then a 2-level tree across the waves (operands read from
+// the other wave's slots).
+struct TpPlan {
+  int n;
+  int dig[12], out[12];
+};
+
 __global__ void __launch_bounds__(64 * TP_WAVES) k_gt_table_prod(const Fq12* __restrict__ tab,
-                                                                 const uint64_t* __restrict__ digits,
+                                                                 const uint64_t* __restrict__ digits, TpPlan tp,
                                                                  Fq12* __restrict__ G) {
   extern __shared__ uint4 smem4[];
   __shared__ int acc_of[TP_WAVES];
@@ -811,7 +835,7 @@ __global__ void __launch_bounds__(64 * TP_WAVES) k_gt_table_prod(const Fq12* __r
   wave::load_consts(vals, 0);
   __syncthreads();
   const int b = blockIdx.x >> 2, i = blockIdx.x & 3, w = threadIdx.x >> 6;
-  const uint64_t e_i = digits[4 * b + i];
+  const uint64_t e_i = digits[4 * tp.dig[b] + i];
   const int base = wave::N_CONSTS + w * 100;
   const wave::Eng e{vals, base, 0};
   auto reg = [&](int j) { return base + 64 + 12 * (j % 3); };
@@ -858,17 +882,21 @@ __global__ void __launch_bounds__(64 * TP_WAVES) k_gt_table_prod(const Fq12* __r
     wave::run(e, prog + TP_SET.off[1], reg(r + 1), 0, reg(r + 2));
     r = (r + 2) % 3;
   }
-  wave::store_f12(vals, reg(r), G + (b >> 1) * 10 + 2 + 4 * (b & 1) + i);
+  wave::store_f12(vals, reg(r), G + tp.out[b] + i);
 }
 
 hipError_t mipp_sq_tables(hipStream_t s, const Fq12* d_la8, Fq12* d_tab, Fq12* d_G) {
-  k_gt_sq_table<<<6, 64, SQ_LDS, s>>>(d_la8, d_tab, d_G);
+  // tables of A1 A2 B1 B2; A0 A3 / B0 B3 into slots 0, 1 of the two product lists
+  const SqPlan sp{4, {2, 3, 6, 7}};
+  const CopyPlan cp{4, {0, 1, 4, 5}, {0, 1, 10, 11}};
+  k_gt_sq_table<<<5, 64, SQ_LDS, s>>>(d_la8, sp, d_tab, cp, d_G);
   return hipGetLastError();
 }
 
 hipError_t mipp_combine_tab(hipStream_t s, const Fq12* d_tab, const uint64_t* d_digits, Fq12* d_G, Fq12* d_mid,
                             Fq12* d_out2) {
-  k_gt_table_prod<<<16, 64 * TP_WAVES, TP_LDS, s>>>(d_tab, d_digits, d_G);
+  const TpPlan tp{4, {0, 1, 2, 3}, {2, 6, 12, 16}};
+  k_gt_table_prod<<<16, 64 * TP_WAVES, TP_LDS, s>>>(d_tab, d_digits, tp, d_G);
   TPST_TRY(hipGetLastError());
   // 2 groups x 10 factors -> 3 partials (chunk 4) -> 1
   k_f12_chunk_prod<<<grid_for(2 * 3, RW), 64 * RW, RW_LDS, s>>>(d_G, 2, 10, 3, d_mid, 4);
