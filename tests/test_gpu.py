@@ -94,17 +94,24 @@ def test_g1_msm_linearity_full_size(ctx, lg):
     assert np.array_equal(got, orc.g1_mul_gen(fr_array([tot]))[0])
 
 
-@pytest.mark.parametrize("case", ["uniform", "clustered"])
+@pytest.mark.parametrize("case", ["uniform", "clustered", "short"])
 def test_g1_msm_window_groups_vs_oracle(ctx, case):
     """n >= 2^17 takes the window-grouped pipeline (msm.hip msm_groups: per-group
     accumulation launches, group reductions + doubling chains on aux streams).
     'clustered' puts whole windows into a handful of buckets, so buckets span
-    many chunks and the chunks straddling two window groups."""
+    many chunks and the chunks straddling two window groups; its sort bins
+    overflow the bin sort's LDS stage (k_sort_bin's direct-scatter path).
+    'short' scalars (< 2^70) leave the top windows all zero digits: one large
+    sentinel bin, and the lower windows' GLV digits skewed."""
     n = (1 << 17) + 37
     k, _ = orc.fr_stream(71, n)
     bases = ctx.g1_mul_generator(k)
     if case == "uniform":
         s, _ = orc.fr_stream(72, n)
+    elif case == "short":
+        s, _ = orc.fr_stream(73, n)
+        s[:, 1] &= np.uint64(0x3f)
+        s[:, 2:] = 0
     else:
         vals = [0, 1, 3, O.R - 1, (1 << 128) + 5, 12345678901234567890123]
         s = fr_array([vals[(i // 1000) % len(vals)] for i in range(n)])

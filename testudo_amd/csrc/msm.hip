@@ -1,7 +1,6 @@
 // Pippenger MSM kernels for gfx950 (see msm.h for the pipeline).
 #include <cstdlib>
 #include <string>
-#include <hipcub/hipcub.hpp>
 #include "device_util.h"
 #include "coop.h"
 #include "msm.h"
@@ -97,46 +96,45 @@ __device__ __forceinline__ void set_wave_prio(int prio) {
     __builtin_amdgcn_s_setprio(3);
 }
 
-// ------------------------------------------------------ K2 decomposition --
-// entries (key = window*nb + |digit|-1, val = point index | sign<<31); with
-// GLV, point index i < n is P_i and n + i is phi(P_i)
-static __global__ void k_decompose_var(const uint32_t* __restrict__ scalars, size_t n, int c, int W, int glv,
-                                       uint32_t sent, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t s[8];
-  load_scalar(scalars + 8 * i, s);
-  const uint32_t nb = 1u << (c - 1);
-  const int halves = glv ? 2 : 1;
-  uint32_t parts[2][4];
-  if (glv) glv_split(s, parts[0], parts[1]);
-  for (int h = 0; h < halves; h++) {
-    const uint32_t* sc = glv ? parts[h] : s;
-    const int nw = glv ? 4 : 8;
-    const uint32_t idx = (uint32_t)(h * n + i);
-    uint32_t carry = 0;
-    for (int w = 0; w < W; w++) {
-      const int d = signed_digit(sc, nw, w, c, W, carry);
-      uint32_t key = sent, val = 0;
-      if (d != 0) {
-        key = (uint32_t)w * nb + (uint32_t)(abs(d) - 1);
-        val = idx | (d < 0 ? 0x80000000u : 0u);
-      }
-      const size_t slot = ((size_t)h * W + w) * n + i;
-      keys[slot] = key;
-      vals[slot] = val;
-    }
-  }
-}
+// ------------------------------------------------------- K2 bucket sort ---
+// The decomposed entries (key = window*nb + |digit|-1, val = point index |
+// sign<<31; with GLV, index i < n is P_i and n + i is phi(P_i); zero digits
+// get the sentinel key nb*W) are grouped by key in two passes, no library sort:
+//  * k_decompose_hist writes a tile of scalars' entries window-major and
+//    counts them per bin (key >> lo) in LDS -> tab[tile][bin];
+//  * k_sort_colscan / k_sort_binscan turn the counts into every tile's slot
+//    range inside every bin and the bin starts;
+//  * k_sort_scatter moves each tile's entries to its slots of their bins;
+//  * k_sort_bin sorts one bin by the low lo key bits in LDS and writes the
+//    entries in key order, the bucket bounds [bstart, bend), zeroes (=
+//    infinity) the buckets without entries and the window starts range[w].
+// Entries of one bucket land in an unspecified order: the bucket sum is a
+// group element, so the MSM result does not depend on it.
+constexpr int SORT_THREADS = 1024;                   // decomposition / scatter workgroup
+constexpr uint32_t SORT_MAX_BINS = 16384;            // LDS histogram of a tile
+constexpr int SORTB_THREADS = 512;                   // bin-sort workgroup
+constexpr int SORTB_IT = 24;                         // entries per thread kept in registers
+constexpr int SORTB_CAP = SORTB_THREADS * SORTB_IT;  // largest bin sorted in LDS
+constexpr int SORTB_LO_MAX = 10;  // bin-sort LDS: 2^(lo+3) + 4 SORTB_CAP bytes <= 64 KB
 
-static __global__ void k_bucket_bounds(const uint32_t* __restrict__ keys, size_t m, uint32_t sent,
-                                       uint32_t* __restrict__ bstart, uint32_t* __restrict__ bend) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= m) return;
-  const uint32_t k = keys[i];
-  if (k >= sent) return;
-  if (i == 0 || keys[i - 1] != k) bstart[k] = (uint32_t)i;
-  if (i == m - 1 || keys[i + 1] != k) bend[k] = (uint32_t)i + 1;
+struct SortPlan {
+  int lo = 0;          // key bits sorted inside a bin
+  uint32_t nbins = 0;  // (sent >> lo) + 1: the last bin holds the sentinel
+  size_t tile = 0;     // scalars per decomposition tile
+  uint32_t ntile = 0;
+};
+
+static bool sort_plan(uint32_t sent, size_t n, size_t m, SortPlan& p) {
+  p.lo = 1;
+  while ((sent >> p.lo) + 1 > SORT_MAX_BINS) p.lo++;
+  // fewer, larger bins while a mean bin stays <= CAP/2 (headroom for skewed digits)
+  while (p.lo < SORTB_LO_MAX && m / ((size_t)(sent >> (p.lo + 1)) + 1) <= (size_t)SORTB_CAP / 2) p.lo++;
+  if (p.lo > SORTB_LO_MAX) return false;
+  p.nbins = (sent >> p.lo) + 1;
+  p.tile = 2048;
+  while ((n + p.tile - 1) / p.tile > 1024) p.tile *= 2;
+  p.ntile = (uint32_t)((n + p.tile - 1) / p.tile);
+  return true;
 }
 
 // phi(P) = (beta x, y), the GLV endomorphism (phi(P) = [x^2 - 1] P on G1).
@@ -147,9 +145,7 @@ __constant__ uint32_t G2_GLV_BETA[12] = {0x5a7b8727u, 0x2c766f92u, 0x253d58b5u, 
                                          0xec122131u, 0x838ec0deu, 0xf658bb10u, 0xbd5eb3e9u,
                                          0x6ed3e52eu, 0x6942bd12u, 0xdd04ed6au, 0x01673786u};  // Montgomery
 template <class F>
-static __global__ void k_glv_phi(const uint32_t* __restrict__ bases, size_t n, uint32_t* __restrict__ out) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+__device__ __forceinline__ void glv_phi_point(const uint32_t* __restrict__ bases, size_t i, uint32_t* __restrict__ out) {
   Affine<F> p = load_affine<F>(bases, i);
   if (!is_inf(p)) {
     if constexpr (sizeof(F) == sizeof(Fq)) {
@@ -161,6 +157,354 @@ static __global__ void k_glv_phi(const uint32_t* __restrict__ bases, size_t n, u
     }
   }
   store_affine(out, i, p);
+}
+
+// one tile of scalars: signed digits (arkworks make_digits over the GLV
+// halves), entries at slot (h W + w) n + i, bin counts, and phi of the bases
+template <class F>
+static __global__ void __launch_bounds__(SORT_THREADS)
+    k_decompose_hist(const uint32_t* __restrict__ scalars, size_t n, int c, int W, int glv, uint32_t sent, int lo,
+                     uint32_t nbins, size_t tile, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                     uint32_t* __restrict__ tab, const uint32_t* __restrict__ bases, uint32_t* __restrict__ phib) {
+  extern __shared__ uint32_t hist[];
+  for (uint32_t b = threadIdx.x; b < nbins; b += SORT_THREADS) hist[b] = 0;
+  __syncthreads();
+  const uint32_t nb = 1u << (c - 1);
+  const size_t i0 = (size_t)blockIdx.x * tile;
+  const size_t i1 = (i0 + tile < n) ? i0 + tile : n;
+  for (size_t i = i0 + threadIdx.x; i < i1; i += SORT_THREADS) {
+    uint32_t s[8];
+    load_scalar(scalars + 8 * i, s);
+    const int halves = glv ? 2 : 1;
+    uint32_t parts[2][4];
+    if (glv) glv_split(s, parts[0], parts[1]);
+    for (int h = 0; h < halves; h++) {
+      const uint32_t* sc = glv ? parts[h] : s;
+      const int nw = glv ? 4 : 8;
+      const uint32_t idx = (uint32_t)(h * n + i);
+      uint32_t carry = 0;
+      for (int w = 0; w < W; w++) {
+        const int d = signed_digit(sc, nw, w, c, W, carry);
+        uint32_t key = sent, val = 0;
+        if (d != 0) {
+          key = (uint32_t)w * nb + (uint32_t)(abs(d) - 1);
+          val = idx | (d < 0 ? 0x80000000u : 0u);
+        }
+        const size_t slot = ((size_t)h * W + w) * n + i;
+        keys[slot] = key;
+        vals[slot] = val;
+        atomicAdd(&hist[key >> lo], 1u);
+      }
+    }
+    if (glv) glv_phi_point<F>(bases, i, phib);
+  }
+  __syncthreads();
+  uint32_t* row = tab + (size_t)blockIdx.x * nbins;
+  for (uint32_t b = threadIdx.x; b < nbins; b += SORT_THREADS) row[b] = hist[b];
+}
+
+// per bin: exclusive scan of the tiles' counts (in place: tab[t][bin] becomes
+// tile t's first slot inside the bin) and the bin total.  64 bins x 16 tile
+// chunks per workgroup.
+static __global__ void __launch_bounds__(1024) k_sort_colscan(uint32_t* __restrict__ tab, uint32_t ntile,
+                                                              uint32_t nbins, uint32_t* __restrict__ tot) {
+  __shared__ uint32_t part[16][64];
+  const uint32_t lane = threadIdx.x & 63, ch = threadIdx.x >> 6;
+  const uint32_t bin = blockIdx.x * 64 + lane;
+  const uint32_t per = (ntile + 15) / 16;
+  const uint32_t t0 = (ch * per < ntile) ? ch * per : ntile;
+  const uint32_t t1 = (t0 + per < ntile) ? t0 + per : ntile;
+  uint32_t sum = 0;
+  if (bin < nbins)
+    for (uint32_t t = t0; t < t1; t++) sum += tab[(size_t)t * nbins + bin];
+  part[ch][lane] = sum;
+  __syncthreads();
+  if (ch == 0) {
+    uint32_t acc = 0;
+    for (int k = 0; k < 16; k++) {
+      const uint32_t v = part[k][lane];
+      part[k][lane] = acc;
+      acc += v;
+    }
+    if (bin < nbins) tot[bin] = acc;
+  }
+  __syncthreads();
+  if (bin < nbins) {
+    uint32_t acc = part[ch][lane];
+    for (uint32_t t = t0; t < t1; t++) {
+      const size_t o = (size_t)t * nbins + bin;
+      const uint32_t v = tab[o];
+      tab[o] = acc;
+      acc += v;
+    }
+  }
+}
+
+// start[b] = sum of the totals of bins < b, start[nbins] = entry count (one workgroup)
+static __global__ void __launch_bounds__(1024) k_sort_binscan(const uint32_t* __restrict__ tot, uint32_t nbins,
+                                                              uint32_t* __restrict__ start) {
+  __shared__ uint32_t ws[1024];
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (nbins + 1023) / 1024;
+  const uint32_t b0 = t * per;
+  uint32_t sum = 0;
+  for (uint32_t k = 0; k < per; k++)
+    if (b0 + k < nbins) sum += tot[b0 + k];
+  ws[t] = sum;
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024; off <<= 1) {
+    const uint32_t v = t >= off ? ws[t - off] : 0u;
+    __syncthreads();
+    ws[t] += v;
+    __syncthreads();
+  }
+  uint32_t acc = ws[t] - sum;
+  for (uint32_t k = 0; k < per; k++)
+    if (b0 + k < nbins) {
+      start[b0 + k] = acc;
+      acc += tot[b0 + k];
+    }
+  if (t == 1023) start[nbins] = ws[1023];
+}
+
+// tile -> bins: each entry takes the next slot of its bin from the tile's
+// cursors in LDS (reads coalesced; writes in runs of the tile's entries per bin)
+static __global__ void __launch_bounds__(SORT_THREADS)
+    k_sort_scatter(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals, size_t n, uint32_t segs,
+                   int lo, uint32_t nbins, size_t tile, const uint32_t* __restrict__ tab,
+                   const uint32_t* __restrict__ start, uint32_t* __restrict__ keys2, uint32_t* __restrict__ vals2) {
+  extern __shared__ uint32_t cur[];
+  const uint32_t* row = tab + (size_t)blockIdx.x * nbins;
+  for (uint32_t b = threadIdx.x; b < nbins; b += SORT_THREADS) cur[b] = start[b] + row[b];
+  __syncthreads();
+  const size_t i0 = (size_t)blockIdx.x * tile;
+  const uint32_t cnt = (uint32_t)((i0 + tile < n) ? tile : n - i0);
+  const uint32_t total = segs * cnt;
+  constexpr int U = 4;
+  for (uint32_t q0 = 0; q0 < total; q0 += U * SORT_THREADS) {
+    uint32_t k[U], v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t q = q0 + u * SORT_THREADS + threadIdx.x;
+      if (q < total) {
+        const uint32_t sg = q / cnt;
+        const size_t slot = (size_t)sg * n + i0 + (q - sg * cnt);
+        k[u] = keys[slot];
+        v[u] = vals[slot];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t q = q0 + u * SORT_THREADS + threadIdx.x;
+      if (q < total) {
+        const uint32_t pos = atomicAdd(&cur[k[u] >> lo], 1u);
+        keys2[pos] = k[u];
+        vals2[pos] = v[u];
+      }
+    }
+  }
+}
+
+constexpr int SCAT_E = 4;  // staged entries per thread (k_sort_scatter_win)
+
+// exclusive prefix sums of a[0, len) into o (may alias a) by NT threads:
+// per-thread runs, wave scan, wave totals; returns the total
+template <int NT>
+__device__ uint32_t block_scan_excl(const uint32_t* a, uint32_t* o, uint32_t len, uint32_t* wsum) {
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (len + NT - 1) / NT, d0 = t * per;
+  uint32_t sum = 0;
+  for (uint32_t k = 0; k < per; k++)
+    if (d0 + k < len) sum += a[d0 + k];
+  uint32_t incl = sum;
+#pragma unroll
+  for (int s = 1; s < 64; s <<= 1) {
+    const uint32_t v = __shfl_up(incl, s, 64);
+    if ((t & 63) >= (uint32_t)s) incl += v;
+  }
+  if ((t & 63) == 63) wsum[t >> 6] = incl;
+  __syncthreads();
+  uint32_t acc = incl - sum, total = 0;
+  for (uint32_t w = 0; w < NT / 64; w++) {
+    if (w < (t >> 6)) acc += wsum[w];
+    total += wsum[w];
+  }
+  for (uint32_t k = 0; k < per; k++)
+    if (d0 + k < len) {
+      const uint32_t v = a[d0 + k];
+      o[d0 + k] = acc;
+      acc += v;
+    }
+  __syncthreads();
+  return total;
+}
+
+// k_sort_scatter with the tile staged per window through LDS (bins aligned to
+// windows: lo <= c - 1): the tile's entries of window w (both GLV halves)
+// are ordered by bin in LDS, then written out in per-bin runs, so a wave's
+// store covers a few runs instead of 64 scattered words
+static __global__ void __launch_bounds__(SORT_THREADS)
+    k_sort_scatter_win(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals, size_t n, int halves,
+                       int W, uint32_t sent, int lo, uint32_t nbins, uint32_t bpw, size_t tile,
+                       const uint32_t* __restrict__ tab, const uint32_t* __restrict__ start,
+                       uint32_t* __restrict__ keys2, uint32_t* __restrict__ vals2) {
+  extern __shared__ uint32_t sm[];
+  __shared__ uint32_t wsum[SORT_THREADS / 64];
+  uint32_t* cur = sm;              // global cursor of every bin
+  uint32_t* lc = cur + nbins;      // the window's bins + the sentinel bin: counts
+  uint32_t* lo_ = lc + bpw + 1;    //   and their first staged slot
+  uint32_t* sk = lo_ + bpw + 1;    // staged keys / values
+  uint32_t* sv = sk + (size_t)SCAT_E * SORT_THREADS;
+  const uint32_t t = threadIdx.x;
+  const uint32_t* row = tab + (size_t)blockIdx.x * nbins;
+  for (uint32_t b = t; b < nbins; b += SORT_THREADS) cur[b] = start[b] + row[b];
+  constexpr int E = SCAT_E;  // entries per thread and window of a sub-tile
+  const size_t sub = (size_t)E * SORT_THREADS / halves;
+  const size_t t0 = (size_t)blockIdx.x * tile, t1 = (t0 + tile < n) ? t0 + tile : n;
+  for (size_t i0 = t0; i0 < t1; i0 += sub)  // sub-tiles append at the tile's cursors
+  for (int w = 0; w < W; w++) {
+    const uint32_t cnt = (uint32_t)((i0 + sub < t1) ? sub : t1 - i0);
+    const uint32_t tot = (uint32_t)halves * cnt;
+    const uint32_t wb = (uint32_t)w * bpw;
+    for (uint32_t j = t; j <= bpw; j += SORT_THREADS) lc[j] = 0;
+    __syncthreads();
+    uint32_t k[E], v[E], r[E];
+#pragma unroll
+    for (int u = 0; u < E; u++) {
+      const uint32_t q = u * SORT_THREADS + t;
+      if (q < tot) {
+        const uint32_t h = q >= cnt ? 1u : 0u;
+        const size_t slot = ((size_t)h * W + w) * n + i0 + (q - h * cnt);
+        k[u] = keys[slot];
+        v[u] = vals[slot];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < E; u++)
+      if (u * SORT_THREADS + t < tot) r[u] = atomicAdd(&lc[k[u] >= sent ? bpw : (k[u] >> lo) - wb], 1u);
+    __syncthreads();
+    block_scan_excl<SORT_THREADS>(lc, lo_, bpw + 1, wsum);
+#pragma unroll
+    for (int u = 0; u < E; u++)
+      if (u * SORT_THREADS + t < tot) {
+        const uint32_t p = lo_[k[u] >= sent ? bpw : (k[u] >> lo) - wb] + r[u];
+        sk[p] = k[u];
+        sv[p] = v[u];
+      }
+    __syncthreads();
+    for (uint32_t p = t; p < tot; p += SORT_THREADS) {
+      const uint32_t key = sk[p];
+      const bool z = key >= sent;
+      const uint32_t lb = z ? bpw : (key >> lo) - wb;
+      const uint32_t pos = cur[z ? nbins - 1 : key >> lo] + (p - lo_[lb]);
+      keys2[pos] = key;
+      vals2[pos] = sv[p];
+    }
+    __syncthreads();
+    for (uint32_t j = t; j <= bpw; j += SORT_THREADS) cur[j == bpw ? nbins - 1 : wb + j] += lc[j];
+    __syncthreads();
+  }
+}
+
+// one bin: counting sort by the low lo key bits.  A bin of <= SORTB_CAP
+// entries is staged in registers + LDS and written out contiguously; a larger
+// one (skewed digits) scatters straight to its slots.
+static __global__ void __launch_bounds__(SORTB_THREADS)
+    k_sort_bin(const uint32_t* __restrict__ keys2, const uint32_t* __restrict__ vals2,
+               const uint32_t* __restrict__ start, int lo, uint32_t sent, uint32_t nb, int W,
+               uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t* __restrict__ bstart,
+               uint32_t* __restrict__ bend, uint4* __restrict__ buckets, uint32_t bucket_u4,
+               uint32_t* __restrict__ range) {
+  extern __shared__ uint32_t sm[];
+  __shared__ uint32_t wsum[SORTB_THREADS / 64];
+  const uint32_t D = 1u << lo, mask = D - 1;
+  uint32_t* off = sm;           // bucket offsets inside the bin (counts first)
+  uint32_t* cur = sm + D;       // placement cursors
+  uint32_t* sval = sm + 2 * D;  // staged values
+  const uint32_t b = blockIdx.x, t = threadIdx.x;
+  const uint32_t s = start[b], len = start[b + 1] - s;
+  for (uint32_t d = t; d < D; d += SORTB_THREADS) off[d] = 0;
+  __syncthreads();
+  const bool fits = len <= (uint32_t)SORTB_CAP;
+  uint32_t kk[SORTB_IT], vv[SORTB_IT];
+  if (fits) {
+#pragma unroll
+    for (int k = 0; k < SORTB_IT; k++) {
+      const uint32_t p = k * SORTB_THREADS + t;
+      if (p < len) {
+        kk[k] = keys2[s + p];
+        vv[k] = vals2[s + p];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < SORTB_IT; k++)
+      if (k * SORTB_THREADS + t < len) atomicAdd(&off[kk[k] & mask], 1u);
+  } else {
+    for (uint32_t p = t; p < len; p += SORTB_THREADS) atomicAdd(&off[keys2[s + p] & mask], 1u);
+  }
+  __syncthreads();
+  // exclusive scan of the counts: per-thread runs, wave scan, wave totals
+  const uint32_t per = (D + SORTB_THREADS - 1) / SORTB_THREADS;
+  const uint32_t d0 = t * per;
+  uint32_t sum = 0;
+  for (uint32_t k = 0; k < per; k++)
+    if (d0 + k < D) sum += off[d0 + k];
+  uint32_t incl = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(incl, o, 64);
+    if ((t & 63) >= (uint32_t)o) incl += v;
+  }
+  if ((t & 63) == 63) wsum[t >> 6] = incl;
+  __syncthreads();
+  uint32_t acc = incl - sum;
+  for (uint32_t w = 0; w < (t >> 6); w++) acc += wsum[w];
+  for (uint32_t k = 0; k < per; k++) {
+    const uint32_t d = d0 + k;
+    if (d >= D) break;
+    const uint32_t cn = off[d];
+    cur[d] = acc;
+    const uint32_t key = (b << lo) | d;
+    if (key < sent) {
+      bstart[key] = s + acc;
+      bend[key] = s + acc + cn;
+      if (cn == 0 && buckets)
+        for (uint32_t u = 0; u < bucket_u4; u++) buckets[(size_t)key * bucket_u4 + u] = make_uint4(0, 0, 0, 0);
+    }
+    acc += cn;
+  }
+  __syncthreads();
+  for (uint32_t d = t; d < D; d += SORTB_THREADS) off[d] = cur[d];
+  if (t <= (uint32_t)W) {
+    const uint32_t target = t * nb;  // first key of window t (t = W: the sentinel)
+    if ((target >> lo) == b) range[t] = s + cur[target & mask];
+  }
+  __syncthreads();
+  if (fits) {
+#pragma unroll
+    for (int k = 0; k < SORTB_IT; k++)
+      if (k * SORTB_THREADS + t < len) sval[atomicAdd(&cur[kk[k] & mask], 1u)] = vv[k];
+    __syncthreads();
+    for (uint32_t p = t; p < len; p += SORTB_THREADS) {
+      uint32_t a = 0, z = D;  // first bucket offset > p
+      while (a < z) {
+        const uint32_t mid = (a + z) >> 1;
+        if (off[mid] <= p)
+          a = mid + 1;
+        else
+          z = mid;
+      }
+      keys[s + p] = (b << lo) | (a - 1);
+      vals[s + p] = sval[p];
+    }
+  } else {
+    for (uint32_t p = t; p < len; p += SORTB_THREADS) {
+      const uint32_t key = keys2[s + p];
+      const uint32_t pos = s + atomicAdd(&cur[key & mask], 1u);
+      keys[pos] = key;
+      vals[pos] = vals2[s + p];
+    }
+  }
 }
 
 template <class F>
@@ -512,24 +856,6 @@ static __global__ void __launch_bounds__(64, 1) k_window_chain(const Xyzz<F>* __
   if (threadIdx.x == 0) store_xyzz(out, 0, acc);
 }
 
-// range[w] = first sorted entry of window w (keys = w nb + digit; range[W] =
-// number of non-zero digits, the sentinels sort last)
-static __global__ void k_window_range(const uint32_t* __restrict__ keys, size_t m, uint32_t nb, int W,
-                                      uint32_t* __restrict__ range) {
-  const int w = threadIdx.x;
-  if (w > W) return;
-  const uint32_t target = (uint32_t)w * nb;
-  size_t lo = 0, hi = m;
-  while (lo < hi) {
-    const size_t mid = (lo + hi) >> 1;
-    if (keys[mid] < target)
-      lo = mid + 1;
-    else
-      hi = mid;
-  }
-  range[w] = (uint32_t)lo;
-}
-
 template <class F>
 __global__ void k_points_to_mont(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, size_t n) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -830,10 +1156,8 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   if (m >= ((size_t)1 << 31)) return hipErrorInvalidValue;
   const size_t nbk = (size_t)W * nb;
   const uint32_t sent = (uint32_t)nbk;  // zero digits; sorts after every bucket key
-  const int end_bit = bit_length(sent);
-  size_t sort_bytes = 0;
-  TPST_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                              (uint32_t*)nullptr, (uint32_t*)nullptr, (int)m, 0, end_bit, s));
+  SortPlan sp;
+  if (!sort_plan(sent, n, m, sp)) return hipErrorInvalidValue;
   const int NG = msm_groups(n, W);
   int wb[Arena::N_AUX_EV / 2 + 1];
   msm_group_bounds(W, NG, wb);
@@ -862,7 +1186,8 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   size_t need = Arena::need(m, 4) * 4 + Arena::need(nbk, 4) * 2 + Arena::need(nbk, sizeof(Xyzz<F>)) +
                 Arena::need(2 * nchunk, sizeof(Xyzz<F>)) + Arena::need(nblk, sizeof(Xyzz<F>)) + red_need +
                 Arena::need(W, sizeof(Xyzz<F>)) + Arena::need(NG, sizeof(Xyzz<F>)) + Arena::need(W + 1, 4) +
-                Arena::need(glv ? n * PW : 1, 4) + Arena::need(sort_bytes, 1) + 8192;
+                Arena::need(glv ? n * PW : 1, 4) + Arena::need((size_t)sp.ntile * sp.nbins, 4) +
+                Arena::need(sp.nbins, 4) + Arena::need(sp.nbins + 1, 4) + 8192;
   ar.reset();
   TPST_TRY(ar.reserve(need));
   uint32_t* keys = ar.take<uint32_t>(m);
@@ -878,37 +1203,46 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   Xyzz<F>* contrib = ar.take<Xyzz<F>>(NG);
   uint32_t* range = ar.take<uint32_t>(W + 1);
   uint32_t* phib = ar.take<uint32_t>(glv ? n * PW : 1);
-  void* tmp = ar.take<char>(sort_bytes);
+  uint32_t* tab = ar.take<uint32_t>((size_t)sp.ntile * sp.nbins);
+  uint32_t* btot = ar.take<uint32_t>(sp.nbins);
+  uint32_t* bin0 = ar.take<uint32_t>(sp.nbins + 1);
 
   Profiler* pf = ar.prof;
   Profiler dummy;
   if (!pf) pf = &dummy;
   pf->begin(ST_DECOMPOSE, s);
-  k_decompose_var<<<grid_for(n, 256), 256, 0, s>>>(d_scalars, n, c, W, glv ? 1 : 0, sent, keys, vals);
+  k_decompose_hist<F><<<sp.ntile, SORT_THREADS, sp.nbins * 4, s>>>(d_scalars, n, c, W, glv ? 1 : 0, sent, sp.lo,
+                                                                  sp.nbins, sp.tile, keys, vals, tab, d_bases, phib);
   TPST_TRY(hipGetLastError());
-  if (glv) {
-    k_glv_phi<F><<<grid_for(n, 256), 256, 0, s>>>(d_bases, n, phib);
-    TPST_TRY(hipGetLastError());
-  }
   pf->end(ST_DECOMPOSE, s);
   pf->begin(ST_SORT, s);
-  TPST_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, sort_bytes, keys, keys2, vals, vals2, (int)m, 0, end_bit, s));
+  k_sort_colscan<<<grid_for(sp.nbins, 64), 1024, 0, s>>>(tab, sp.ntile, sp.nbins, btot);
+  TPST_TRY(hipGetLastError());
+  k_sort_binscan<<<1, 1024, 0, s>>>(btot, sp.nbins, bin0);
+  TPST_TRY(hipGetLastError());
+  const int halves = glv ? 2 : 1;
+  const uint32_t bpw = nb >> sp.lo;
+  const size_t lds = ((size_t)sp.nbins + 2 * (bpw + 1) + 2 * (size_t)SCAT_E * SORT_THREADS) * 4;
+  if (sp.lo <= c - 1 && lds <= 60 * 1024) {  // bins aligned to windows, stage fits
+    k_sort_scatter_win<<<sp.ntile, SORT_THREADS, lds, s>>>(keys, vals, n, halves, W, sent, sp.lo, sp.nbins, bpw,
+                                                           sp.tile, tab, bin0, keys2, vals2);
+  } else {
+    k_sort_scatter<<<sp.ntile, SORT_THREADS, sp.nbins * 4, s>>>(keys, vals, n, (uint32_t)(halves * W), sp.lo,
+                                                                sp.nbins, sp.tile, tab, bin0, keys2, vals2);
+  }
+  TPST_TRY(hipGetLastError());
+  // sorted entries back into keys / vals; bucket bounds, empty buckets, range
+  k_sort_bin<<<sp.nbins, SORTB_THREADS, (2u << sp.lo) * 4 + SORTB_CAP * 4, s>>>(
+      keys2, vals2, bin0, sp.lo, sent, nb, W, keys, vals, bstart, bend, reinterpret_cast<uint4*>(buckets),
+      (uint32_t)(sizeof(Xyzz<F>) / 16), range);
+  TPST_TRY(hipGetLastError());
   pf->end(ST_SORT, s);
-  pf->begin(ST_BOUNDS, s);
-  TPST_TRY(hipMemsetAsync(bstart, 0, nbk * 4, s));
-  TPST_TRY(hipMemsetAsync(bend, 0, nbk * 4, s));
-  TPST_TRY(hipMemsetAsync(buckets, 0, nbk * sizeof(Xyzz<F>), s));  // ZZ = 0 == infinity
-  k_bucket_bounds<<<grid_for(m, 256), 256, 0, s>>>(keys2, m, sent, bstart, bend);
-  TPST_TRY(hipGetLastError());
-  k_window_range<<<1, 64 * ((W + 64) / 64), 0, s>>>(keys2, m, nb, W, range);
-  TPST_TRY(hipGetLastError());
-  pf->end(ST_BOUNDS, s);
   if (!short_chunks) {  // one launch, long chunks (more than ~2^21 points)
     pf->begin(ST_BUCKET_ACC, s);
-    k_bucket_acc_chunk<F><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys2, vals2, m, sent, bstart, bend, d_bases, phib,
+    k_bucket_acc_chunk<F><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys, vals, m, sent, bstart, bend, d_bases, phib,
                                                                 (uint32_t)n, lg, buckets, part, bpart);
     TPST_TRY(hipGetLastError());
-    k_bucket_fixup<F><<<grid_for(nblk, 64), 64, 0, s>>>(keys2, m, sent, bstart, bend, lg, nblk, part, bpart,
+    k_bucket_fixup<F><<<grid_for(nblk, 64), 64, 0, s>>>(keys, m, sent, bstart, bend, lg, nblk, part, bpart,
                                                         buckets);
     TPST_TRY(hipGetLastError());
     pf->end(ST_BUCKET_ACC, s);
@@ -930,11 +1264,11 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
     const int wlo = wb[g], whi = wb[g + 1];
     const size_t gchunks = ((per_win * (size_t)(whi - wlo)) >> lg) + 2;
     if constexpr (std::is_same<F, Fq2>::value) {
-      k_bucket_acc_short_pair<<<grid_for(2 * gchunks, 64), 64, 0, bulk>>>(keys2, vals2, range, wlo, whi, sent,
+      k_bucket_acc_short_pair<<<grid_for(2 * gchunks, 64), 64, 0, bulk>>>(keys, vals, range, wlo, whi, sent,
                                                                           bstart, bend, d_bases, phib, (uint32_t)n,
                                                                           lg, buckets, part);
     } else {
-      k_bucket_acc_short<F><<<grid_for(gchunks, 64), 64, 0, bulk>>>(keys2, vals2, range, wlo, whi, sent, bstart,
+      k_bucket_acc_short<F><<<grid_for(gchunks, 64), 64, 0, bulk>>>(keys, vals, range, wlo, whi, sent, bstart,
                                                                      bend, d_bases, phib, (uint32_t)n, lg, buckets,
                                                                      part);
     }

@@ -9,7 +9,7 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], int(r["Grid_Size_X"]),
              r.get("Queue_Id", r.get("Stream_Id", "?"))) for r in rows)
-starts = [i for i, e in enumerate(ev) if "k_decompose_var" in e[2]]
+starts = [i for i, e in enumerate(ev) if "k_decompose" in e[2]]
 i0 = starts[-2] if len(starts) > 1 else starts[-1]  # the last complete MSM
 i1 = starts[starts.index(i0) + 1] if starts.index(i0) + 1 < len(starts) else len(ev)
 seg = ev[i0:i1]
