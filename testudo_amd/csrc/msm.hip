@@ -305,8 +305,6 @@ static __global__ void __launch_bounds__(SORT_THREADS)
   }
 }
 
-constexpr int SCAT_E = 4;  // staged entries per thread (k_sort_scatter_win)
-
 // exclusive prefix sums of a[0, len) into o (may alias a) by NT threads:
 // per-thread runs, wave scan, wave totals; returns the total
 template <int NT>
@@ -343,6 +341,7 @@ __device__ uint32_t block_scan_excl(const uint32_t* a, uint32_t* o, uint32_t len
 // windows: lo <= c - 1): the tile's entries of window w (both GLV halves)
 // are ordered by bin in LDS, then written out in per-bin runs, so a wave's
 // store covers a few runs instead of 64 scattered words
+template <int E>
 static __global__ void __launch_bounds__(SORT_THREADS)
     k_sort_scatter_win(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals, size_t n, int halves,
                        int W, uint32_t sent, int lo, uint32_t nbins, uint32_t bpw, size_t tile,
@@ -354,11 +353,10 @@ static __global__ void __launch_bounds__(SORT_THREADS)
   uint32_t* lc = cur + nbins;      // the window's bins + the sentinel bin: counts
   uint32_t* lo_ = lc + bpw + 1;    //   and their first staged slot
   uint32_t* sk = lo_ + bpw + 1;    // staged keys / values
-  uint32_t* sv = sk + (size_t)SCAT_E * SORT_THREADS;
+  uint32_t* sv = sk + (size_t)E * SORT_THREADS;
   const uint32_t t = threadIdx.x;
   const uint32_t* row = tab + (size_t)blockIdx.x * nbins;
   for (uint32_t b = t; b < nbins; b += SORT_THREADS) cur[b] = start[b] + row[b];
-  constexpr int E = SCAT_E;  // entries per thread and window of a sub-tile
   const size_t sub = (size_t)E * SORT_THREADS / halves;
   const size_t t0 = (size_t)blockIdx.x * tile, t1 = (t0 + tile < n) ? t0 + tile : n;
   for (size_t i0 = t0; i0 < t1; i0 += sub)  // sub-tiles append at the tile's cursors
@@ -1222,10 +1220,16 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   TPST_TRY(hipGetLastError());
   const int halves = glv ? 2 : 1;
   const uint32_t bpw = nb >> sp.lo;
-  const size_t lds = ((size_t)sp.nbins + 2 * (bpw + 1) + 2 * (size_t)SCAT_E * SORT_THREADS) * 4;
-  if (sp.lo <= c - 1 && lds <= 60 * 1024) {  // bins aligned to windows, stage fits
-    k_sort_scatter_win<<<sp.ntile, SORT_THREADS, lds, s>>>(keys, vals, n, halves, W, sent, sp.lo, sp.nbins, bpw,
-                                                           sp.tile, tab, bin0, keys2, vals2);
+  // stage of E entries per thread (E = 4, or 2 when the bin cursors are many)
+  const auto scat_lds = [&](int E) { return ((size_t)sp.nbins + 2 * (bpw + 1) + 2 * (size_t)E * SORT_THREADS) * 4; };
+  const int E = scat_lds(4) <= 60 * 1024 ? 4 : (scat_lds(2) <= 60 * 1024 ? 2 : 0);
+  if (sp.lo <= c - 1 && E) {  // bins aligned to windows, stage fits
+    if (E == 4)
+      k_sort_scatter_win<4><<<sp.ntile, SORT_THREADS, scat_lds(4), s>>>(keys, vals, n, halves, W, sent, sp.lo,
+                                                                       sp.nbins, bpw, sp.tile, tab, bin0, keys2, vals2);
+    else
+      k_sort_scatter_win<2><<<sp.ntile, SORT_THREADS, scat_lds(2), s>>>(keys, vals, n, halves, W, sent, sp.lo,
+                                                                       sp.nbins, bpw, sp.tile, tab, bin0, keys2, vals2);
   } else {
     k_sort_scatter<<<sp.ntile, SORT_THREADS, sp.nbins * 4, s>>>(keys, vals, n, (uint32_t)(halves * W), sp.lo,
                                                                 sp.nbins, sp.tile, tab, bin0, keys2, vals2);
