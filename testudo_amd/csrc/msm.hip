@@ -1038,11 +1038,12 @@ static hipError_t reduce_buckets2(Arena& ar, hipStream_t s, const Xyzz<F>* d_buc
   return hipGetLastError();
 }
 
-// TPST_MSM_FIXUP_QUAD=0: the last group's fixup one lane per bucket (A/B)
-static bool fixup_quad() {
-  static const bool v = [] {
+// TPST_MSM_FIXUP_QUAD=k: the fixups of the window groups g < k run one quad of
+// lanes per bucket (default 1: the last group's, on the MSM's tail; 0 = none)
+static int fixup_quad_groups() {
+  static const int v = [] {
     const char* e = getenv("TPST_MSM_FIXUP_QUAD");
-    return !(e && atoi(e) == 0);
+    return e ? atoi(e) : 1;
   }();
   return v;
 }
@@ -1287,7 +1288,7 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
     if constexpr (std::is_same<F, Fq2>::value)
       k_bucket_fixup_short_pair<<<grid_for(2 * (b1 - b0), 64), 64, 0, a>>>(bstart, bend, b0, b1, lg, part, buckets,
                                                                           g ? red_prio() : 0);
-    else if (g == 0 && fixup_quad())
+    else if (g < fixup_quad_groups())
       k_bucket_fixup_quad<F><<<grid_for(4 * (b1 - b0), 64), 64, 0, a>>>(bstart, bend, b0, b1, lg, part, buckets);
     else
       k_bucket_fixup_short<F><<<grid_for(b1 - b0, 64), 64, 0, a>>>(bstart, bend, b0, b1, lg, part, buckets,

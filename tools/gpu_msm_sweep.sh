@@ -1,4 +1,4 @@
-# MSM GPU tests, then a bench sweep over "GROUPS:LG:RED2:SPLIT:PRIO" tuples (MSM only)
+# MSM GPU tests, then a bench sweep over "GROUPS:LG:RED2:SPLIT:PRIO[:FIXUPQUAD]" tuples (MSM only)
 set -o pipefail
 OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-sw}
 mkdir -p $OUT
@@ -8,7 +8,8 @@ if [ -n "$3" ]; then
   tail -2 $OUT/gpu_tests.log
 fi
 for p in $2; do
-  IFS=: read g l r sp pr <<< "$p"
-  TPST_MSM_GROUPS=$g TPST_MSM_LG=$l TPST_MSM_RED2=$r TPST_MSM_SPLIT=$sp TPST_MSM_PRIO=$pr timeout -k 10 200 python -u bench.py --no-cpu --no-pst --no-sharded --no-r1cs --no-groth16 > $OUT/bench_${g}_${l}_${r}_${sp}_${pr}.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
-  python -c "import json,sys; d=json.load(open('$OUT/bench_${g}_${l}_${r}_${sp}_${pr}.json')); print('g $g lg $l red2 $r split $sp prio $pr', d['value'], d['ms_per_step'], d['stages_ms_per_step'], d['parity_ok'])"
+  IFS=: read g l r sp pr fq <<< "$p"
+  fq=${fq:-1}
+  TPST_MSM_GROUPS=$g TPST_MSM_LG=$l TPST_MSM_RED2=$r TPST_MSM_SPLIT=$sp TPST_MSM_PRIO=$pr TPST_MSM_FIXUP_QUAD=$fq timeout -k 10 200 python -u bench.py --no-cpu --no-pst --no-sharded --no-r1cs --no-groth16 > $OUT/bench_${g}_${l}_${r}_${sp}_${pr}_${fq}.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
+  python -c "import json,sys; d=json.load(open('$OUT/bench_${g}_${l}_${r}_${sp}_${pr}_${fq}.json')); print('g $g lg $l red2 $r split $sp prio $pr fq $fq', d['value'], d['ms_per_step'], d['stages_ms_per_step'], d['parity_ok'])"
 done
