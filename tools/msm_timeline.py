@@ -1,5 +1,5 @@
 """Timeline of the last variable-base MSM in a rocprofv3 kernel trace (from its
-k_decompose_var to the end of its k_window_chain): queue, start (ms from the
+k_decompose_hist to the end of its k_window_chain): queue, start (ms from the
 MSM's start), duration, kernel, grid -- to read the accumulation / reduction /
 chain overlap of the window-grouped pipeline (csrc/msm.hip msm_var)."""
 import csv
