@@ -50,10 +50,13 @@ sys.path.insert(0, ROOT)
 METRIC = "PST commit+open sec, 2^20-var poly BLS12-377; G1 MSM Mscalar/s at 1/2/4/8 GPU"
 LOG_N = 20
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
-VALU_PEAK_WAVE_INSTS = 256 * 4 * 0.5 * 2.4e9  # CUs x SIMDs x (1 wave-instr / 2 cycles) x 2.4 GHz
 BYTES_PER_PAIR = 128           # 32 B scalar + 96 B affine base
+LIMB_PRODUCTS_PER_FQ_MUL = 276  # 12 x 12 a*b + 11 x 12 m*p limb products (v_mad_u64_u32 each, field.h mul)
 SEED = 0x7E57D0
-PMC_FILE = os.path.join(ROOT, "profiles", "r03", "pmc_bucket_acc_short.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r04", "pmc_bucket_acc_short.json")
+PMC_FILE_K1 = os.path.join(ROOT, "profiles", "r04", "pmc_bucket_acc_chunk_2p24.json")
+if not os.path.exists(PMC_FILE):  # the latest round that has one
+    PMC_FILE = os.path.join(ROOT, "profiles", "r03", "pmc_bucket_acc_short.json")
 
 
 def parse():
@@ -116,6 +119,29 @@ def fq_mults_per_madd(pmc=None):
     if pmc and pmc.get("fq_mul_equiv_per_madd"):
         return float(pmc["fq_mul_equiv_per_madd"])
     return 12.0
+
+
+def issue_rates(ctx):
+    """Chip-wide wave-instruction issue rates (per s) of v_mad_u64_u32 and
+    v_add_u32 (microbench kinds 6 and 9: 8 independent chains per lane, 8
+    waves per SIMD), measured live (tools/mb_wave.py does the same sweep)."""
+    out = {}
+    thr, iters = 256 * 4 * 8 * 64, 2000
+    for kind, name in ((6, "v_mad_u64_u32"), (9, "v_add_u32")):
+        ctx.microbench(kind, 64, 4)
+        ms = min(ctx.microbench(kind, thr, iters) for _ in range(3))
+        out[name] = thr / 64 * iters * 32 / (ms * 1e-3)
+    return out
+
+
+def _stage_ms(ctx):
+    """Average device span (ms) per recorded stage since the last reset."""
+    return {k: round(v[0] / v[1], 4) for k, v in ctx.profile_read().items() if v[1]}
+
+
+def _median(xs):
+    xs = sorted(xs)
+    return xs[len(xs) // 2]
 
 
 def _max_over_ranks(dist, dev, x):
@@ -235,12 +261,22 @@ def main():
     tot = int(np.dot(sv, bv) % R)
     parity_ok = bool(np.array_equal(out, ctx.g1_mul_generator(fr_array([tot]))[0]))
 
-    sharded = None
-    if dist is not None and not args.no_sharded:  # every rank takes part
+    sharded = sharded20 = split = None
+    if dist is not None:  # every rank takes part in the multi-rank legs
         try:
-            sharded = sharded_leg(ctx, args.sharded_log_n, dist, dev)
+            split = split_msm_leg(ctx, n, dist, dev, args.steps, args.warmup, out)
         except Exception as e:
-            sharded = {"error": repr(e)}
+            split = {"error": repr(e)}
+        if not args.no_pst:
+            try:
+                sharded20 = sharded_leg(ctx, args.pst_log_n, dist, dev)
+            except Exception as e:
+                sharded20 = {"error": repr(e)}
+        if not args.no_sharded:
+            try:
+                sharded = sharded_leg(ctx, args.sharded_log_n, dist, dev)
+            except Exception as e:
+                sharded = {"error": repr(e)}
     if rank != 0:
         if dist:
             dist.barrier()
@@ -260,27 +296,36 @@ def main():
         except ValueError:
             pmc = None
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
-    # compute roof: measured Fq-mult peak vs achieved in the dominant kernel
+    # compute roof, measured live on this GPU: the chip-wide issue rate of
+    # v_mad_u64_u32 (one limb product) prices an Fq product at its 276 limb
+    # products -- the multiply-issue roof; the Fq-product microbenchmark is the
+    # achieved-in-isolation rate; v_add_u32's rate is the VALU issue peak
+    rates = issue_rates(ctx)
+    mad_roof_fqmul = rates["v_mad_u64_u32"] * 64 / LIMB_PRODUCTS_PER_FQ_MUL
     mb_threads = 256 * 16 * 64
     mb_iters = 200
     ctx.microbench(0, mb_threads, 10)  # warm: first launch loads the code object
-    peak_fqmul = mb_threads * mb_iters / (min(ctx.microbench(0, mb_threads, mb_iters) for _ in range(3)) * 1e-3)
+    mb_fqmul = mb_threads * mb_iters / (min(ctx.microbench(0, mb_threads, mb_iters) for _ in range(3)) * 1e-3)
     c_bits = 16
     windows = 8  # GLV: two 127-bit halves, 8 signed 16-bit windows each
     madds = 2 * n * windows
     fq_per_madd = fq_mults_per_madd(pmc)
     achieved_fqmul = madds * fq_per_madd / (acc_avg_ms * 1e-3)
     compute = {"bound": "valu-int32", "kernel": "k_bucket_acc_short<Fq>",
-               "achieved_fq_mul_per_s": achieved_fqmul, "peak_fq_mul_per_s_measured": peak_fqmul,
-               "frac": round(achieved_fqmul / peak_fqmul, 4),
+               "roof": "v_mad_u64_u32 issue (measured) / %d limb products per Fq product" % LIMB_PRODUCTS_PER_FQ_MUL,
+               "mad_wave_insts_per_s": rates["v_mad_u64_u32"], "peak_fq_mul_per_s": mad_roof_fqmul,
+               "achieved_fq_mul_per_s": achieved_fqmul, "frac": round(achieved_fqmul / mad_roof_fqmul, 4),
+               "microbench_fq_mul_per_s": mb_fqmul, "microbench_frac": round(mb_fqmul / mad_roof_fqmul, 4),
+               "achieved_vs_microbench": round(achieved_fqmul / mb_fqmul, 4),
                "fq_mul_per_madd": round(fq_per_madd, 3),
                "fq_mul_per_madd_source": ("SQ_INSTS_VALU ratio, " + os.path.relpath(PMC_FILE, ROOT))
                if pmc and pmc.get("fq_mul_equiv_per_madd") else "formula (8M + 2S + adds)"}
     if pmc and pmc.get("valu_insts_per_launch"):
         rate = pmc["valu_insts_per_launch"] / (acc_avg_ms * 1e-3)
         compute.update({"valu_wave_insts_per_launch": pmc["valu_insts_per_launch"],
-                        "valu_issue_per_s": rate, "valu_issue_peak_per_s": VALU_PEAK_WAVE_INSTS,
-                        "valu_issue_frac": round(rate / VALU_PEAK_WAVE_INSTS, 4)})
+                        "valu_issue_per_s": rate, "valu_issue_peak_per_s": rates["v_add_u32"],
+                        "valu_issue_peak_source": "v_add_u32 chip issue rate, measured",
+                        "valu_issue_frac": round(rate / rates["v_add_u32"], 4)})
 
     result = {
         "metric": METRIC,
@@ -309,6 +354,10 @@ def main():
                      "note": "HBM column secondary: the kernel is bound by 32-bit integer VALU issue"},
         "compute": compute,
     }
+    if split is not None:
+        result["msm_split"] = split
+    if sharded20 is not None:
+        result["pst"] = sharded20
     if sharded is not None:
         result["pst_2p24"] = sharded
     if not args.no_pst and world == 1:
@@ -339,9 +388,12 @@ def main():
 
 def pst_leg(ctx, log_n, reps=5):
     """sqrt-PST commit + open at 2^log_n variables (BASELINE configs[2]),
-    timed like benches/pst.rs:52-62 (eval / get_q before the open timer).
-    Also reported: the H2D upload of Z (from_evaluations, BASELINE.md's
-    GPU-time definition includes it) and commit+open including it."""
+    timed like benches/pst.rs:52-62 (eval / get_q before the open timer):
+    the median of `reps` warm runs.  Also reported: the H2D upload of Z
+    (from_evaluations; BASELINE.md's GPU-time definition includes it),
+    commit+open including it, and the device spans of one further, profiled
+    run under the reference's Timer labels (hipEvents on the library's streams:
+    first command to last, host launch overhead excluded)."""
     from testudo_amd import sqrt_pst as S
     nv = (log_n + 1) // 2
     t = time.perf_counter()
@@ -352,11 +404,15 @@ def pst_leg(ctx, log_n, reps=5):
     # the first commit+open of the process (cold: code objects load, scratch
     # arenas grow) is reported separately; then the median of `reps` warm runs
     runs = []
-    for _ in range(reps + 1):
+    for rep in range(reps + 2):
+        prof = rep == reps + 1  # the last run: device spans only, not timed
         ctx.synchronize()
         t = time.perf_counter()
         pl = S.Polynomial.from_evaluations(ctx, Z)
         h2d_s = time.perf_counter() - t
+        if prof:
+            ctx.profile_reset()
+            ctx.profile(True)
         t = time.perf_counter()
         comms, T = pl.commit()
         commit_s = time.perf_counter() - t
@@ -365,22 +421,33 @@ def pst_leg(ctx, log_n, reps=5):
         t = time.perf_counter()
         U, pst_proof, mipp = pl.open(tr, comms, pt, T)
         open_s = time.perf_counter() - t
-        runs.append((commit_s, open_s, h2d_s))
+        if prof:
+            ctx.profile(False)
+            spans = _stage_ms(ctx)
+        else:
+            runs.append((commit_s, open_s, h2d_s))
     _PST_LAST[log_n] = {"comms": comms, "T": T, "U": U, "comms_t": mipp.comms_t}
     cold = runs[0]
-    warm = sorted(runs[1:], key=lambda r: r[0] + r[1])[len(runs[1:]) // 2]
+    warm = runs[1:]
+    c, o, h = (_median([r[i] for r in warm]) for i in range(3))
+    co = _median([r[0] + r[1] for r in warm])
     t = time.perf_counter()
     ok = S.verify(ctx, S.PoseidonTranscript(), U, pt, v, pst_proof, mipp, T)
     verify_s = time.perf_counter() - t
     sizes = _wire_sizes(ctx, nv, pst_proof, mipp)
-    return {"log_n": log_n, "commit_s": round(warm[0], 4), "open_s": round(warm[1], 4), **sizes,
-            "commit_plus_open_s": round(warm[0] + warm[1], 4), "reps": reps,
-            "h2d_s": round(warm[2], 4), "commit_open_incl_h2d_s": round(warm[0] + warm[1] + warm[2], 4),
+    return {"log_n": log_n, "commit_s": round(c, 4), "open_s": round(o, 4), **sizes,
+            "commit_plus_open_s": round(co, 4), "reps": reps, "timing": "median of the warm reps",
+            "h2d_s": round(h, 4), "commit_open_incl_h2d_s": round(co + h, 4),
+            "device_commit_s": round(spans.get("sqrt_commit", 0.0) * 1e-3, 5),
+            "device_open_s": round(spans.get("sqrt_open", 0.0) * 1e-3, 5),
+            "stages_ms": {k: spans[k] for k in ("comm_list", "ipp", "sqrt_commit", "msm", "mipp_prove", "pst_open",
+                                                "sqrt_open", "batch_sort", "bucket_acc") if k in spans},
             "first_call": {"commit_s": round(cold[0], 4), "open_s": round(cold[1], 4)},
             "verify_s": round(verify_s, 4), "srs_setup_s": round(setup_s, 3), "verified": ok,
             "note": "Z resident in HBM for commit_s/open_s (benches/pst.rs:48-62: the polynomial is built before "
                     "the timers); h2d_s = from_evaluations from pageable host memory; eval before the open timer; "
-                    "SRS tables built in srs_setup"}
+                    "SRS tables built in srs_setup; device_*_s / stages_ms = hipEvent spans of one extra profiled "
+                    "run (reference Timer labels, sqrt_pst.rs:118-228)"}
 
 
 _R1CS_LAST = None
@@ -463,8 +530,9 @@ def _wire_sizes(ctx, nv, pst_proof, mipp):
             "commiter_key_size": len(W.ser_committer_key(nv, S.srs_export(ctx, nv)))}
 
 
-def sharded_leg(ctx, log_n, dist, dev):
-    """sqrt-PST commit + open at 2^log_n variables (BASELINE configs[3]).
+def sharded_leg(ctx, log_n, dist, dev, reps=5):
+    """sqrt-PST commit + open at 2^log_n variables (BASELINE configs[3] at
+    2^24; configs[2] at 2^20 when N > 1).
     N > 1: every rank uploads only its column block of Z and commits its rows
     AND their share of the IPP's Miller loops (one all-gather of [row
     commitments | Miller partial] device buffers, one final exponentiation on
@@ -472,7 +540,10 @@ def sharded_leg(ctx, log_n, dist, dev):
     share of get_q's z_q and of c_u (one all-gather, summed on rank 0 -- the
     q / eval step that benches/pst.rs runs before the open timer), and rank 0
     opens from q alone (transcript-sequential MIPP + PST open, SURVEY.md
-    §8(e)).  No rank holds the whole Z.  N = 1: the plain commit + open."""
+    §8(e)).  No rank holds the whole Z.  N = 1: the plain commit + open.
+    Timing as BASELINE.md:43-45: the median of `reps` warm runs (commit: max
+    over ranks), plus the H2D upload of Z; then one profiled run for the
+    device spans and K1's roofline (the dominant kernel of the commit)."""
     from testudo_amd import sqrt_pst as S
     from testudo_amd.distributed import shard_rows, sharded_commit, sharded_open_inputs
     nv = (log_n + 1) // 2
@@ -484,19 +555,27 @@ def sharded_leg(ctx, log_n, dist, dev):
     rank = dist.get_rank() if dist else 0
     world = dist.get_world_size() if dist else 1
     r0, r1 = shard_rows(1 << (log_n // 2), world, rank)
+    if dist:
+        dist.barrier()
     t = time.perf_counter()
     if dist:  # the rank-local column block only
         shard = S.Polynomial.from_evaluations_cols(ctx, Z, r0, r1)
     else:
         shard = S.Polynomial.from_evaluations(ctx, Z)
-    h2d_s = time.perf_counter() - t
+    ctx.synchronize()
+    h2d_s = _max_over_ranks(dist, dev, time.perf_counter() - t)
     del Z
-    reps = 2
     commits, qs, opens = [], [], []
-    for _ in range(reps + 1):
+    k1 = {}
+    spans = {}
+    for rep in range(reps + 2):
+        prof = rep == reps + 1  # the last run: device spans only, not timed
         if dist:
             dist.barrier()
         ctx.synchronize()
+        if prof:
+            ctx.profile_reset()
+            ctx.profile(True)
         t = time.perf_counter()
         if dist:
             comms, T, own = sharded_commit(log_n, shard.commit_rows_partial_into,
@@ -506,7 +585,12 @@ def sharded_leg(ctx, log_n, dist, dev):
         ctx.synchronize()
         if dist:
             dist.barrier()
-        commits.append(_max_over_ranks(dist, dev, time.perf_counter() - t))
+        c_el = _max_over_ranks(dist, dev, time.perf_counter() - t)
+        if prof:
+            ctx.profile(False)
+            k1 = _stage_ms(ctx)
+        else:
+            commits.append(c_el)
         # q (and c_u) before the open timer, as eval does in benches/pst.rs:48-62
         t = time.perf_counter()
         if dist:
@@ -520,28 +604,112 @@ def sharded_leg(ctx, log_n, dist, dev):
         ctx.synchronize()
         if dist:
             dist.barrier()
-        qs.append(_max_over_ranks(dist, dev, time.perf_counter() - t))
+        q_el = _max_over_ranks(dist, dev, time.perf_counter() - t)
+        if not prof:
+            qs.append(q_el)
         if rank == 0:
+            if prof:
+                ctx.profile_reset()
+                ctx.profile(True)
             t = time.perf_counter()
             U, pst_proof, mipp = pl.open(S.PoseidonTranscript(), comms, pt, T)
-            opens.append(time.perf_counter() - t)
+            o_el = time.perf_counter() - t
+            if prof:
+                ctx.profile(False)
+                spans = _stage_ms(ctx)
+            else:
+                opens.append(o_el)
     if dist:
         dist.barrier()
     if rank != 0:
         return None
     ok = S.verify(ctx, S.PoseidonTranscript(), U, pt, v, pst_proof, mipp, T)
     _PST_LAST[log_n] = {"comms": comms, "T": T, "U": U, "comms_t": mipp.comms_t}
-    c, o = min(commits[1:]), min(opens[1:])
-    return {"log_n": log_n, "commit_s": round(c, 4), "open_s": round(o, 4), "commit_plus_open_s": round(c + o, 4),
-            **_wire_sizes(ctx, nv, pst_proof, mipp),
-            "first_call": {"commit_s": round(commits[0], 4), "open_s": round(opens[0], 4)},
-            "q_eval_s": round(min(qs[1:]), 4),
-            "ranks": world, "rows_per_rank": r1 - r0, "verified": ok,
-            "h2d_s_rank0": round(h2d_s, 4), "srs_setup_s": round(setup_s, 3),
-            "exchange": ("per-rank column-block upload; %s all_gather of [96-B row commitments | 576-B Miller "
-                         "partial] device buffers, FE on rank 0; %s all_gather of [z_q share | c_u share], mod-r / "
-                         "G1 sum on rank 0, open from q on rank 0"
-                         % ((("RCCL" if dist.get_backend() == "nccl" else "gloo"),) * 2)) if dist else "none"}
+    warm = list(zip(commits[1:], opens[1:]))
+    c, o = _median([w[0] for w in warm]), _median([w[1] for w in warm])
+    co = _median([w[0] + w[1] for w in warm])
+    res = {"log_n": log_n, "commit_s": round(c, 4), "open_s": round(o, 4), "commit_plus_open_s": round(co, 4),
+           "reps": reps, "timing": "median of the warm reps (commit: max over ranks)",
+           "h2d_s": round(h2d_s, 4), "commit_open_incl_h2d_s": round(co + h2d_s, 4),
+           "device_commit_rank0_s": round(k1.get("sqrt_commit", 0.0) * 1e-3, 5) if world == 1 else None,
+           "device_open_s": round(spans.get("sqrt_open", 0.0) * 1e-3, 5),
+           "stages_ms": {**{k: k1[k] for k in ("comm_list", "ipp", "sqrt_commit", "batch_sort", "bucket_acc")
+                            if k in k1},
+                         **{k: spans[k] for k in ("msm", "mipp_prove", "pst_open", "sqrt_open") if k in spans}},
+           **_wire_sizes(ctx, nv, pst_proof, mipp),
+           "first_call": {"commit_s": round(commits[0], 4), "open_s": round(opens[0], 4)},
+           "q_eval_s": round(_median(qs[1:]), 4),
+           "ranks": world, "rows_per_rank": r1 - r0, "verified": ok, "srs_setup_s": round(setup_s, 3),
+           "exchange": ("per-rank column-block upload; %s all_gather of [96-B row commitments | 576-B Miller "
+                        "partial] device buffers, FE on rank 0; %s all_gather of [z_q share | c_u share], mod-r / "
+                        "G1 sum on rank 0, open from q on rank 0"
+                        % ((("RCCL" if dist.get_backend() == "nccl" else "gloo"),) * 2)) if dist else "none"}
+    if "bucket_acc" in k1:  # K1 (k_bucket_acc_chunk + fixup) over this rank's rows
+        rows = r1 - r0
+        npts = 1 << (log_n - log_n // 2)
+        alg = rows * npts * 32 + npts * 96 + rows * 96  # scalars + bases once + row outputs
+        acc_s = k1["bucket_acc"] * 1e-3
+        pmc = None
+        if os.path.exists(PMC_FILE_K1):
+            try:
+                pmc = json.load(open(PMC_FILE_K1))
+            except ValueError:
+                pmc = None
+        res["roofline_k1"] = {"bound": "valu-int32 / random gathers", "kernel": "k_bucket_acc_chunk<Fq> + fixup",
+                              "achieved": round(alg / acc_s / 1e9, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(alg / acc_s / 1e9 / HBM_PEAK_GBS, 6), "alg_bytes_per_launch": alg,
+                              "kernel_ms": round(k1["bucket_acc"], 4),
+                              "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                              "traffic_source": os.path.relpath(PMC_FILE_K1, ROOT) if pmc else None,
+                              "gather_bytes_per_launch": pmc.get("gather_bytes_per_launch") if pmc else None}
+    return res
+
+
+def split_msm_leg(ctx, n, dist, dev, steps, warmup, ref_out):
+    """Strong scaling of ONE 2^log_n G1 MSM (sqrt_pst.rs:198 / mipp.rs:393):
+    rank g takes points [g n/N, (g+1) n/N) of rank 0's inputs, computes its
+    share as a raw XYZZ sum, one all-gather moves the 192-B shares and rank 0
+    sums them on the device (testudo_amd/distributed.py sharded_msm).  Timed
+    like the headline: barrier + synchronize around `steps` MSMs, max over
+    ranks; checked against rank 0's single-GPU MSM of the same inputs."""
+    import torch
+    from testudo_amd import sqrt_pst as S
+    from testudo_amd.distributed import shard_rows, sharded_msm
+    from testudo_amd.sqrt_pst import fr_stream
+    world, rank = dist.get_world_size(), dist.get_rank()
+    i0, i1 = shard_rows(n, world, rank)
+    sc, _ = fr_stream(SEED, n)  # rank 0's inputs (bench.py main: SEED + 17 * 0)
+    bk, _ = fr_stream(SEED + 1000, n)
+    d_s = torch.from_numpy(sc[i0:i1].view(np.int64).copy()).to(dev)
+    d_k = torch.from_numpy(bk[i0:i1].view(np.int64).copy()).to(dev)
+    d_b = torch.empty((i1 - i0) * 12, dtype=torch.int64, device=dev)
+    ctx.torch_to_lib()
+    ctx.g1_mul_generator_dev(d_k.data_ptr(), i1 - i0, d_b.data_ptr())
+    ctx.synchronize()
+
+    def step():
+        return sharded_msm(n, lambda a, b, o: S.g1_msm_partial_into(ctx, d_b.data_ptr(), d_s.data_ptr(), 0, b - a, o),
+                           lambda got: S.g1_xyzz_combine(ctx, got), dist, dev)
+
+    for _ in range(warmup):
+        step()
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        res = step()
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = _max_over_ranks(dist, dev, time.perf_counter() - t0)
+    if rank != 0:
+        return None
+    return {"value": round(n * steps / el / 1e6, 3), "unit": "Mscalar/s", "scaling": "strong",
+            "ms_per_msm": round(el / steps * 1e3, 4), "n_points": n, "ranks": world, "points_per_rank": i1 - i0,
+            "parity_ok": bool(np.array_equal(res.cpu().numpy().view(np.uint64), ref_out)),
+            "exchange": "%s all_gather of the 192-B XYZZ shares, device sum on rank 0" % (
+                "RCCL" if dist.get_backend() == "nccl" else "gloo")}
 
 
 def cpu_leg(ctx, bk, sc, gpu_out, result):

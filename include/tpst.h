@@ -52,6 +52,16 @@ const char* tpst_last_error(const tpst_ctx* ctx);
 /* hipStream_t of the context, for callers that order their own work */
 void* tpst_stream(tpst_ctx* ctx);
 int tpst_synchronize(tpst_ctx* ctx);
+/* Ordering against a caller's stream (e.g. the framework stream that wrote a
+ * device buffer handed to a _dev call, or will read one a _dev call fills).
+ * The library's stream is non-blocking, so without these the two streams are
+ * unordered.  tpst_wait_stream: work the library queues from now on starts
+ * after everything queued on `stream` so far.  tpst_join_stream: work queued
+ * on `stream` from now on starts after everything the library queued so far.
+ * Both are asynchronous (one event each); stream == NULL is the legacy
+ * default stream. */
+int tpst_wait_stream(tpst_ctx* ctx, void* stream);
+int tpst_join_stream(tpst_ctx* ctx, void* stream);
 
 /* ---- K2: variable-base MSM ---------------------------------------------
  * sum_i scalars[i] * bases[i] over min(n_bases, n_scalars) terms.
@@ -65,6 +75,13 @@ int tpst_g2_msm(tpst_ctx* ctx, const uint64_t* bases, size_t n_bases, const uint
 /* device-resident form: d_bases Montgomery affine (24 u32 each), d_scalars
  * canonical Fr (8 u32 each), d_out one canonical affine G1 */
 int tpst_g1_msm_dev(tpst_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, void* d_out);
+/* One MSM split over ranks (sqrt_pst.rs:198 / mipp.rs:393 at 1/2/4/8 GPUs):
+ * each rank's share of the points as the raw XYZZ sum (192 B: X, Y, ZZ, ZZZ,
+ * Montgomery u64 limbs; no per-rank affine inversion), gathered as bytes,
+ * then summed on one device to one canonical affine G1 (k shares, stride_bytes
+ * apart in d_parts). */
+int tpst_g1_msm_xyzz_dev(tpst_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, void* d_out_xyzz);
+int tpst_g1_xyzz_sum_dev(tpst_ctx* ctx, const void* d_parts, size_t k, size_t stride_bytes, void* d_out);
 
 /* Length-checked form: mipp.rs:385-394 `multiexponentiation` returns
  * Err(InvalidIPVectorLength) when the lengths differ -> TPST_E_ARG here. */

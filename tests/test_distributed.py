@@ -6,6 +6,8 @@
   gathered commitment list and T must equal the single-process commit bit for
   bit -- and the sharded opening inputs (C3: per-rank shares of get_q's z_q and
   of c_u, summed on rank 0) against the single-process q and U;
+* the split (strong-scaled) MSM: shares of equal point ranges, one
+  all-gather, the combine on rank 0, against the oracle MSM of all points;
 * bench.py's timing aggregation (barrier + max over ranks).
 """
 import os
@@ -126,6 +128,54 @@ def test_sharded_commit_gloo_world2(n):
         assert p.exitcode == 0
     res = [r for r in res if r is not None]
     assert res == [(True, True, True, True)]  # comm_list, T, combined z_q, combined c_u
+
+
+def _msm_worker(rank, world, port, n, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle", "cpu"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import orc
+        from testudo_amd.distributed import sharded_msm
+        k, _ = orc.fr_stream(0x7E57D6, n)
+        s, _ = orc.fr_stream(0x7E57D5, n)
+        bases = orc.g1_mul_gen(k)
+
+        def partial_into(i0, i1, out):  # the oracle stands in for tpst_g1_msm_xyzz_dev
+            share = np.zeros(24, dtype=np.uint64)
+            share[:12] = orc.g1_msm(bases[i0:i1], s[i0:i1])
+            out.copy_(torch.from_numpy(share.view(np.int64)))
+
+        def combine(got):
+            pts = got.numpy().view(np.uint64)[:, :12]
+            ones = np.zeros((len(pts), 4), dtype=np.uint64)
+            ones[:, 0] = 1
+            return orc.g1_msm(np.ascontiguousarray(pts), ones)
+
+        out = sharded_msm(n, partial_into, combine, dist, torch.device("cpu"))
+        q.put(bool(np.array_equal(out, orc.g1_msm(bases, s))) if rank == 0 else None)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_msm_gloo_world2():
+    """Strong-scaled MSM orchestration: two ranks take halves of the points,
+    one all-gather of the shares, the combine on rank 0 equals the oracle MSM
+    of all points."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_msm_worker, args=(r, 2, port, 1000, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r for r in res if r is not None] == [True]
 
 
 def _timing_worker(rank, world, port, q):

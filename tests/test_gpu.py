@@ -96,7 +96,7 @@ def test_g1_msm_linearity_full_size(ctx, lg):
     assert np.array_equal(got, orc.g1_mul_gen(fr_array([tot]))[0])
 
 
-@pytest.mark.parametrize("case", ["uniform", "clustered", "short"])
+@pytest.mark.parametrize("case", ["uniform", "clustered", "short", "boolean"])
 def test_g1_msm_window_groups_vs_oracle(ctx, case):
     """n >= 2^17 takes the window-grouped pipeline (msm.hip msm_groups: per-group
     accumulation launches, group reductions + doubling chains on aux streams).
@@ -104,13 +104,19 @@ def test_g1_msm_window_groups_vs_oracle(ctx, case):
     many chunks and the chunks straddling two window groups; its sort bins
     overflow the bin sort's LDS stage (k_sort_bin's direct-scatter path).
     'short' scalars (< 2^70) leave the top windows all zero digits: one large
-    sentinel bin, and the lower windows' GLV digits skewed."""
+    sentinel bin, and the lower windows' GLV digits skewed.  'boolean' puts
+    half the points into one bucket (the long-bucket fixup)."""
     n = (1 << 17) + 37
     k, _ = orc.fr_stream(71, n)
     bases = ctx.g1_mul_generator(k)
     if case == "uniform":
         s, _ = orc.fr_stream(72, n)
-    elif case == "short":
+    elif case == "boolean":
+        # 0/1 scalars (witness bits): one bucket of ~65 K entries in window 0,
+        # finished by k_bucket_fixup_long; every other window is sentinel
+        rng = np.random.default_rng(74)
+        s = np.zeros((n, 4), dtype=np.uint64)
+        s[:, 0] = rng.integers(0, 2, n, dtype=np.uint64)
         s, _ = orc.fr_stream(73, n)
         s[:, 1] &= np.uint64(0x3f)
         s[:, 2:] = 0
@@ -119,6 +125,73 @@ def test_g1_msm_window_groups_vs_oracle(ctx, case):
         s = fr_array([vals[(i // 1000) % len(vals)] for i in range(n)])
         bases[100:3000] = bases[7]     # repeated bases inside the big buckets
     assert np.array_equal(ctx.g1_msm(bases, s), orc.g1_msm(bases, s, parallel=True))
+
+
+@pytest.mark.parametrize("g2", [False, True])
+def test_msm_long_buckets_small_n(ctx, g2):
+    """Below 2^17 points (one window group, the quad / pair fixups): all-ones
+    scalars put every point into one bucket of window 0 -- n / 32 chunk pieces,
+    summed by k_bucket_fixup_long -- and every other entry is a zero digit."""
+    n = 20000
+    k, _ = orc.fr_stream(75, n)
+    bases = orc.g2_mul_gen(k[:2000]) if g2 else ctx.g1_mul_generator(k)
+    if g2:
+        bases = np.concatenate([bases] * (n // 2000))
+    s = np.zeros((n, 4), dtype=np.uint64)
+    s[:, 0] = 1
+    s[::7, 0] = 2  # a second long bucket
+    got = ctx.g2_msm(bases, s) if g2 else ctx.g1_msm(bases, s)
+    ref = (orc.g2_msm if g2 else orc.g1_msm)(bases, s)
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_split_msm_shares_combine(ctx, world):
+    """Strong-scaled MSM pieces: the XYZZ shares of `world`
+    equal point ranges (tpst_g1_msm_xyzz_dev), summed on the device
+    (tpst_g1_xyzz_sum_dev), equal the oracle MSM of all points."""
+    import torch
+    from testudo_amd import sqrt_pst as S
+    n = 1 << 16
+    k, _ = orc.fr_stream(76, n)
+    s, _ = orc.fr_stream(77, n)
+    dev = torch.device("cuda", 0)
+    d_k = torch.from_numpy(k.view(np.int64)).to(dev)
+    d_s = torch.from_numpy(s.view(np.int64)).to(dev)
+    d_b = torch.empty(n * 12, dtype=torch.int64, device=dev)
+    ctx.torch_to_lib()
+    ctx.g1_mul_generator_dev(d_k.data_ptr(), n, d_b.data_ptr())
+    ctx.lib_to_torch()
+    parts = torch.empty((world, 24), dtype=torch.int64, device=dev)
+    R = n // world
+    for g in range(world):
+        S.g1_msm_partial_into(ctx, d_b.data_ptr(), d_s.data_ptr(), g * R, (g + 1) * R, parts[g])
+    # a strided view of the shares (every other row of a wider buffer)
+    wide = torch.zeros((2 * world, 24), dtype=torch.int64, device=dev)
+    wide[::2] = parts
+    out = S.g1_xyzz_combine(ctx, parts).cpu().numpy().view(np.uint64)
+    out2 = S.g1_xyzz_combine(ctx, wide[::2]).cpu().numpy().view(np.uint64)
+    ref = orc.g1_msm(orc.g1_mul_gen(k), s, parallel=True)
+    assert np.array_equal(out, ref) and np.array_equal(out2, ref)
+
+
+def test_fr_sum_non_contiguous_gathered_view(ctx):
+    """The C3 combine reads a torch-produced buffer on the library stream:
+    a non-contiguous slice of a gathered tensor (the RCCL path's got[:, :N*4])
+    is made contiguous on torch's stream and must be complete before
+    tpst_fr_sum_dev reads it (tpst_wait_stream)."""
+    import torch
+    from testudo_amd import sqrt_pst as S
+    k, w = 4, 1 << 14
+    a, _ = orc.fr_stream(78, k * w)
+    dev = torch.device("cuda", 0)
+    for _ in range(3):
+        big = torch.from_numpy(np.concatenate([a.reshape(k, -1), np.zeros((k, 12), np.uint64)], axis=1)
+                               .view(np.int64)).to(dev)
+        got = S.fr_sum(ctx, big[:, :w * 4]).cpu().numpy().view(np.uint64).reshape(-1, 4)
+        ai = a.reshape(k, w, 4).astype(object)
+        tot = sum(ai[:, :, t] << (64 * t) for t in range(4)).sum(axis=0) % O.R
+        assert [limbs_to_int(x) for x in got] == list(tot)
 
 
 def test_generator_muls_vs_oracle(ctx):

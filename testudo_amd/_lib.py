@@ -24,9 +24,13 @@ PROTOTYPES = [
     ("tpst_last_error", C.c_char_p, [_vp]),
     ("tpst_stream", _vp, [_vp]),
     ("tpst_synchronize", C.c_int, [_vp]),
+    ("tpst_wait_stream", C.c_int, [_vp, _vp]),
+    ("tpst_join_stream", C.c_int, [_vp, _vp]),
     ("tpst_g1_msm", C.c_int, [_vp, _u64p, _sz, _u64p, _sz, _u64p]),
     ("tpst_g2_msm", C.c_int, [_vp, _u64p, _sz, _u64p, _sz, _u64p]),
     ("tpst_g1_msm_dev", C.c_int, [_vp, _vp, _vp, _sz, _vp]),
+    ("tpst_g1_msm_xyzz_dev", C.c_int, [_vp, _vp, _vp, _sz, _vp]),
+    ("tpst_g1_xyzz_sum_dev", C.c_int, [_vp, _vp, _sz, _sz, _vp]),
     ("tpst_g1_multiexp", C.c_int, [_vp, _u64p, _sz, _u64p, _sz, _u64p]),
     ("tpst_g2_multiexp", C.c_int, [_vp, _u64p, _sz, _u64p, _sz, _u64p]),
     ("tpst_gens_load", C.c_int, [_vp, _u64p, _sz, _u64p, C.POINTER(_vp)]),

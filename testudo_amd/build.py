@@ -21,9 +21,21 @@ BUILD = os.path.join(HERE, "build")
 LIB = os.path.join(HERE, "libtpst.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("TPST_ARCH", "gfx950")
-FLAGS = ["-std=c++17", "-O3", "--offload-arch=" + ARCH, "-fPIC", "-Wno-unused-result",
-         "-Xarch_host", "-march=x86-64-v3", "-Xarch_host", "-madx",
-         "-I" + CSRC, "-I" + os.path.join(ROOT, "include")]
+
+
+def _host_isa_flags() -> list:
+    """x86-64-v3 + ADX for the host code (the Poseidon transcript's 768-bit
+    products between MIPP rounds) only when TPST_HOST_ISA=v3 asks for it: the
+    library then needs AVX2 / BMI2 / ADX on every machine that loads it.  The
+    default is the baseline ISA, which runs anywhere (the __int128 code is
+    correct without those extensions)."""
+    if os.environ.get("TPST_HOST_ISA", "") == "v3":
+        return ["-Xarch_host", "-march=x86-64-v3", "-Xarch_host", "-madx"]
+    return []
+
+
+FLAGS = (["-std=c++17", "-O3", "--offload-arch=" + ARCH, "-fPIC", "-Wno-unused-result"] + _host_isa_flags() +
+         ["-I" + CSRC, "-I" + os.path.join(ROOT, "include")])
 
 
 def _includes(path: str, seen: set) -> None:
@@ -66,7 +78,8 @@ def build(verbose: bool = True) -> str:
         objs = list(ex.map(_compile, srcs))
     newest = max(os.path.getmtime(o) for o in objs)
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < newest:
-        cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", LIB + ".tmp"] + objs
+        cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", LIB + ".tmp"] + objs + [
+            "-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed:\n" + r.stderr[-4000:])

@@ -68,6 +68,8 @@ extern "C" void tpst_destroy(tpst_ctx* ctx) {
     ctx->arena_side[i].release();
   }
   for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
+  if (ctx->ev_wait) (void)hipEventDestroy(ctx->ev_wait);
+  if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   tpst_release_pst_state(ctx);
   (void)hipStreamDestroy(ctx->stream);
@@ -82,6 +84,29 @@ extern "C" int tpst_synchronize(tpst_ctx* ctx) {
   if (!ctx) return TPST_E_ARG;
   TPST_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return TPST_OK;
+}
+
+// one event per direction, re-recorded per call (a stream wait captures the
+// event's state at the time of the wait call, so re-use is safe)
+static int order_streams(tpst_ctx* ctx, hipStream_t before, hipStream_t after, hipEvent_t& ev) {
+  if (!ev) TPST_HIP(ctx, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  TPST_HIP(ctx, hipEventRecord(ev, before));
+  TPST_HIP(ctx, hipStreamWaitEvent(after, ev, 0));
+  return TPST_OK;
+}
+
+extern "C" int tpst_wait_stream(tpst_ctx* ctx, void* stream) {
+  if (!ctx) return TPST_E_ARG;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  return order_streams(ctx, (hipStream_t)stream, ctx->stream, ctx->ev_wait);
+}
+
+extern "C" int tpst_join_stream(tpst_ctx* ctx, void* stream) {
+  if (!ctx) return TPST_E_ARG;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  return order_streams(ctx, ctx->stream, (hipStream_t)stream, ctx->ev_join);
 }
 
 // ---------------------------------------------------------------- MSM ----
@@ -194,6 +219,41 @@ extern "C" int tpst_g1_msm_dev(tpst_ctx* ctx, const void* d_bases, const void* d
   TPST_HIP(ctx, ctx->io.reserve(Arena::need(1, sizeof(Xyzz<Fq>)) + 256));
   Xyzz<Fq>* d_r = ctx->io.take<Xyzz<Fq>>(1);
   TPST_HIP(ctx, msm_var<Fq>(ctx->arena, ctx->stream, (const uint32_t*)d_bases, (const uint32_t*)d_scalars, n, d_r));
+  TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(ctx->stream, d_r, (uint32_t*)d_out, 1));
+  return TPST_OK;
+}
+
+// strong-scaled MSM pieces: one rank's share as the raw XYZZ sum (no affine
+// inversion per rank), and the combine of the gathered shares on one device
+extern "C" int tpst_g1_msm_xyzz_dev(tpst_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n,
+                                    void* d_out_xyzz) {
+  if (!ctx || !d_out_xyzz || (n && (!d_bases || !d_scalars))) return fail(ctx, TPST_E_ARG, "null argument");
+  if (n > MSM_MAX_POINTS) return fail(ctx, TPST_E_ARG, "MSM longer than 2^27 points: split it");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  TPST_HIP(ctx, msm_var<Fq>(ctx->arena, ctx->stream, (const uint32_t*)d_bases, (const uint32_t*)d_scalars, n,
+                            (Xyzz<Fq>*)d_out_xyzz));
+  return TPST_OK;
+}
+
+static __global__ void __launch_bounds__(64) k_xyzz_sum(const uint8_t* __restrict__ parts, size_t k, size_t stride,
+                                                        Xyzz<Fq>* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  Xyzz<Fq> acc = Xyzz<Fq>::inf();
+  for (size_t i = 0; i < k; i++) acc = add(acc, load_xyzz(reinterpret_cast<const Xyzz<Fq>*>(parts + i * stride), 0));
+  store_xyzz(out, 0, acc);
+}
+
+extern "C" int tpst_g1_xyzz_sum_dev(tpst_ctx* ctx, const void* d_parts, size_t k, size_t stride_bytes, void* d_out) {
+  if (!ctx || !d_out || (k && !d_parts)) return fail(ctx, TPST_E_ARG, "null argument");
+  if (k && (stride_bytes < sizeof(Xyzz<Fq>) || stride_bytes % 4)) return fail(ctx, TPST_E_ARG, "bad stride");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  ctx->io.reset();
+  TPST_HIP(ctx, ctx->io.reserve(Arena::need(1, sizeof(Xyzz<Fq>)) + 256));
+  Xyzz<Fq>* d_r = ctx->io.take<Xyzz<Fq>>(1);
+  k_xyzz_sum<<<1, 64, 0, ctx->stream>>>((const uint8_t*)d_parts, k, stride_bytes, d_r);
+  TPST_HIP(ctx, hipGetLastError());
   TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(ctx->stream, d_r, (uint32_t*)d_out, 1));
   return TPST_OK;
 }

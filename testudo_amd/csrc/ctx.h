@@ -21,6 +21,8 @@ struct tpst_ctx {
   hipStream_t side[3] = {nullptr, nullptr, nullptr};
   tpst::Arena arena_side[3];
   std::vector<hipEvent_t> events;  // timing-free event pool of the opening
+  hipEvent_t ev_wait = nullptr;    // tpst_wait_stream / tpst_join_stream
+  hipEvent_t ev_join = nullptr;
   void* pinned = nullptr;          // pinned host staging of the opening
   size_t pinned_cap = 0;
 };

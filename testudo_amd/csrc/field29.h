@@ -1,0 +1,243 @@
+// Reduced-radix Fq for the throughput kernels (MSM bucket accumulation):
+// 13 limbs of 29 bits (377 bits), Montgomery R = 2^377, values canonical
+// (< p) in every limb representation handed between functions.
+//
+// Why: field.h's Fq product spends one v_mad_u64_u32 AND one v_addc per limb
+// product (a 32 x 32-bit product into a 64-bit column needs the carry-out),
+// 276 of each for 12 x 32-bit limbs.  With 29-bit limbs a limb product is
+// < 2^58 and a column of up to 26 of them stays below 2^63, so each limb
+// product is a single v_mad_u64_u32 into a 64-bit accumulator and the carry
+// moves once per column: 169 + 156 multiply-adds (p_0 = 1: the reduction
+// word of a column is m = -t mod 2^29 and m * p_0 is an add), no v_addc.
+// Chip issue, measured (profiles/r02/s11/mb_wave.log): v_mad_u64_u32 takes
+// two issue slots of a v_add_u32, so the product drops from ~993 to ~790
+// slots.
+//
+// Conversions: field.h keeps arkworks' layout (12 x u32, R = 2^384).
+//   from_std: V = x 2^384 -> x 2^377 = (V + k p) / 2^7, k = -V mod 2^7
+//             (p = 1 mod 2^46), then the bits regrouped -- no product;
+//   to_std:   Y = x 2^377 -> Montgomery product by 2^384 mod p (one product;
+//             used only where a bucket or piece leaves the kernel).
+#pragma once
+#include "field.h"
+
+namespace tpst {
+
+namespace r29 {
+constexpr int N = 13;
+constexpr uint32_t M = (1u << 29) - 1;
+// p in radix 2^29 (p_0 = 1)
+static constexpr uint32_t P[N] = {0x00000001u, 0x08460000u, 0x00000021u, 0x16ba8860u, 0x14800170u,
+                                  0x1117dd04u, 0x0e3c7bcdu, 0x1e601ea2u, 0x1b1a22d9u, 0x03650a49u,
+                                  0x118ec170u, 0x0f8a21d5u, 0x1ae3a461u};
+// 2^377 mod p (Montgomery one)
+static constexpr uint32_t ONE[N] = {0x1fffffffu, 0x17b9ffffu, 0x1fffffdeu, 0x0945779fu, 0x0b7ffe8fu,
+                                    0x0ee822fbu, 0x11c38432u, 0x019fe15du, 0x04e5dd26u, 0x1c9af5b6u,
+                                    0x0e713e8fu, 0x1075de2au, 0x051c5b9eu};
+// 2^384 mod p in radix 2^29, plain (the to_std multiplier: Y * C / 2^377 = Y 2^7)
+static constexpr uint32_t TO_STD[N] = {0x1fffff68u, 0x166fffffu, 0x1fffec40u, 0x013f06ffu, 0x13ff2514u,
+                                       0x19d4c53eu, 0x0c167df6u, 0x16edcf8cu, 0x087b4e97u, 0x1c01e427u,
+                                       0x133d256fu, 0x05fbe934u, 0x08d6661eu};
+}  // namespace r29
+
+struct Fq29 {
+  uint32_t v[r29::N];
+  static TPST_HD Fq29 zero() {
+    Fq29 r;
+#pragma unroll
+    for (int i = 0; i < r29::N; i++) r.v[i] = 0;
+    return r;
+  }
+  static TPST_HD Fq29 one() {
+    Fq29 r;
+#pragma unroll
+    for (int i = 0; i < r29::N; i++) r.v[i] = r29::ONE[i];
+    return r;
+  }
+};
+
+TPST_HD bool is_zero(const Fq29& a) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < r29::N; i++) acc |= a.v[i];
+  return acc == 0;
+}
+
+TPST_HD bool eq(const Fq29& a, const Fq29& b) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < r29::N; i++) acc |= a.v[i] ^ b.v[i];
+  return acc == 0;
+}
+
+// t - p if t >= p (t < 2p, limbs normalised except the top one, < 2^30)
+TPST_HD void reduce_once(Fq29& t) {
+  uint32_t s[r29::N];
+  int32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < r29::N; i++) {
+    const int32_t d = (int32_t)t.v[i] - (int32_t)r29::P[i] + br;
+    s[i] = (uint32_t)d & r29::M;
+    br = d >> 29;  // 0 or -1
+  }
+  const bool take = br == 0;
+#pragma unroll
+  for (int i = 0; i < r29::N; i++) t.v[i] = take ? s[i] : t.v[i];
+}
+
+TPST_HD Fq29 add(const Fq29& a, const Fq29& b) {
+  Fq29 r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < r29::N; i++) {
+    const uint32_t s = a.v[i] + b.v[i] + c;
+    r.v[i] = i < r29::N - 1 ? (s & r29::M) : s;
+    c = s >> 29;
+  }
+  reduce_once(r);
+  return r;
+}
+
+TPST_HD Fq29 dbl(const Fq29& a) { return add(a, a); }
+
+TPST_HD Fq29 sub(const Fq29& a, const Fq29& b) {
+  Fq29 r;
+  int32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < r29::N; i++) {
+    const int32_t d = (int32_t)a.v[i] - (int32_t)b.v[i] + br;
+    r.v[i] = (uint32_t)d & r29::M;
+    br = d >> 29;
+  }
+  const uint32_t mask = (uint32_t)br;  // all ones if a < b: add p back
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < r29::N; i++) {
+    const uint32_t s = r.v[i] + (r29::P[i] & mask) + c;
+    r.v[i] = s & r29::M;
+    c = s >> 29;
+  }
+  return r;
+}
+
+TPST_HD Fq29 neg(const Fq29& a) { return sub(Fq29::zero(), a); }
+TPST_HD Fq29 mul3(const Fq29& a) { return add(dbl(a), a); }
+
+// Montgomery product a b 2^-377 mod p, product scanning: column k gathers its
+// a_i b_j and m_i p_j (i < k) in one 64-bit accumulator (<= 26 terms < 2^58
+// each), then the reduction word m_k = -acc mod 2^29 (p_0 = 1) for k < 13 or
+// the output limb, and the carry acc >> 29 moves to the next column.
+TPST_HD Fq29 mul(const Fq29& a, const Fq29& b) {
+  constexpr int N = r29::N;
+  uint32_t m[N], t[N];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; k++) {
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < N) acc += (uint64_t)a.v[i] * b.v[j];
+    }
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      const int j = k - i;
+      if (i < k && j >= 1 && j < N) acc += (uint64_t)m[i] * r29::P[j];
+    }
+    if (k < N) {
+      m[k] = (0u - (uint32_t)acc) & r29::M;
+      acc += m[k];
+    } else {
+      t[k - N] = (uint32_t)acc & r29::M;
+    }
+    acc >>= 29;
+  }
+  t[N - 1] = (uint32_t)acc;  // < 2^30: t < 2p
+  Fq29 r;
+#pragma unroll
+  for (int i = 0; i < N; i++) r.v[i] = t[i];
+  reduce_once(r);
+  return r;
+}
+
+// square: cross products a_i a_j (i < j) once, doubled per column
+TPST_HD Fq29 sqr(const Fq29& a) {
+  constexpr int N = r29::N;
+  uint32_t m[N], t[N];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; k++) {
+    uint64_t cr = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      const int j = k - i;
+      if (i < j && j < N) cr += (uint64_t)a.v[i] * a.v[j];
+    }
+    acc += cr << 1;  // <= 13 cross terms < 2^58: doubled < 2^63
+    if ((k & 1) == 0 && (k >> 1) < N) acc += (uint64_t)a.v[k >> 1] * a.v[k >> 1];
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      const int j = k - i;
+      if (i < k && j >= 1 && j < N) acc += (uint64_t)m[i] * r29::P[j];
+    }
+    if (k < N) {
+      m[k] = (0u - (uint32_t)acc) & r29::M;
+      acc += m[k];
+    } else {
+      t[k - N] = (uint32_t)acc & r29::M;
+    }
+    acc >>= 29;
+  }
+  t[N - 1] = (uint32_t)acc;
+  Fq29 r;
+#pragma unroll
+  for (int i = 0; i < N; i++) r.v[i] = t[i];
+  reduce_once(r);
+  return r;
+}
+
+// bits [s, s + 29) of a 12-word little-endian value (s + 29 <= 416)
+TPST_HD uint32_t bits29(const uint32_t* w, int s) {
+  const int q = s >> 5, o = s & 31;
+  const uint64_t lo = q < 12 ? w[q] : 0u;
+  const uint64_t hi = q + 1 < 12 ? w[q + 1] : 0u;
+  return (uint32_t)(((hi << 32) | lo) >> o) & r29::M;
+}
+
+// field.h Montgomery (x 2^384, 12 x u32, < p) -> x 2^377 in radix 2^29
+TPST_HD Fq29 from_std(const Fq& a) {
+  const uint32_t k = (0u - a.v[0]) & 127u;  // (a + k p) = 0 mod 2^7
+  uint32_t w[12];
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    c += (uint64_t)k * params::FQ_P[i] + a.v[i];
+    w[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  // a + k p < 128 p < 2^384: no carry out
+  Fq29 r;
+#pragma unroll
+  for (int j = 0; j < r29::N; j++) r.v[j] = bits29(w, 29 * j + 7);
+  return r;  // (a + k p) / 2^7 < p
+}
+
+// x 2^377 (radix 2^29, < p) -> field.h Montgomery x 2^384
+TPST_HD Fq to_std(const Fq29& a) {
+  Fq29 c;
+#pragma unroll
+  for (int i = 0; i < r29::N; i++) c.v[i] = r29::TO_STD[i];
+  const Fq29 y = mul(a, c);  // a 2^384 / 2^377 = a 2^7, canonical
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    // bits [32 i, 32 i + 32) of the 29-bit limbs
+    const int s = 32 * i, j = s / 29, o = s % 29;
+    uint64_t v = (uint64_t)y.v[j] >> o;
+    if (j + 1 < r29::N) v |= (uint64_t)y.v[j + 1] << (29 - o);
+    if (j + 2 < r29::N) v |= (uint64_t)y.v[j + 2] << (58 - o);
+    r.v[i] = (uint32_t)v;
+  }
+  return r;
+}
+
+}  // namespace tpst

@@ -5,6 +5,7 @@
 #include "ctx.h"
 #include "device_util.h"
 #include "wave_tower.h"
+#include "field29.h"
 
 using namespace tpst;
 
@@ -184,6 +185,31 @@ __global__ void k_mb_fqmul_v(int variant, int iters, uint32_t* out) {
   store_f<Fq>(out + 12 * (size_t)t, a);
 }
 
+// radix-2^29 field (field29.h): product / square chains and the XYZZ mixed
+// add over it, same shapes as kinds 0 and 1 (kinds 12, 14, 13)
+__global__ void k_mb_fq29(int sq, int iters, uint32_t* out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  Fq29 a = Fq29::one(), b = Fq29::one();
+  a.v[0] ^= t & 0xffffu;
+  b.v[1] ^= (t * 7u + 1) & 0xffffu;
+  if (sq)
+    for (int i = 0; i < iters; i++) a = sqr(a);
+  else
+    for (int i = 0; i < iters; i++) a = mul(a, b);
+#pragma unroll
+  for (int i = 0; i < 12; i++) out[12 * (size_t)t + i] = a.v[i] ^ (i == 0 ? a.v[12] : 0u);
+}
+
+__global__ void k_mb_madd29(int iters, uint32_t* out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const Affine<Fq29> g = {from_std(Fq::from_limbs(params::G1_GEN_X)), from_std(Fq::from_limbs(params::G1_GEN_Y))};
+  Xyzz<Fq29> acc = dbl_affine(g);
+  acc.X.v[0] ^= (t & 1);
+  for (int i = 0; i < iters; i++) acc = add_affine(acc, g);
+  const Fq x = to_std(acc.X);
+  store_f<Fq>(out + 12 * (size_t)t, x);
+}
+
 __global__ void k_mb_dbl(int iters, uint32_t* out) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   G1A g = {Fq::from_limbs(params::G1_GEN_X), Fq::from_limbs(params::G1_GEN_Y)};
@@ -352,6 +378,10 @@ extern "C" int tpst_microbench(tpst_ctx* ctx, int kind, size_t threads, int iter
     k_mb_insn<10><<<grid, bs, 0, ctx->stream>>>(iters, d);
   else if (kind == 11)
     k_mb_insn<11><<<grid, bs, 0, ctx->stream>>>(iters, d);
+  else if (kind == 12 || kind == 14)
+    k_mb_fq29<<<grid, bs, 0, ctx->stream>>>(kind == 14, iters, d);
+  else if (kind == 13)
+    k_mb_madd29<<<grid, bs, 0, ctx->stream>>>(iters, d);
   else if (kind >= 16 && kind < 16 + wave::N_OPS) {
     const int op = kind - 16;
     const size_t lds = (((wave::OP_LEN[op] + 3) & ~3u) + (size_t)(wave::N_CONSTS + 64 + 4 * 48) * wave::SLOT) * 4;

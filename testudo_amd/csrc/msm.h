@@ -24,7 +24,16 @@ namespace tpst {
 
 // Optional per-stage HIP-event timing of the MSM pipeline (the bench's
 // roofline needs the dominant kernel's own duration on the stream it runs on).
-enum MsmStage { ST_DECOMPOSE = 0, ST_SORT, ST_BOUNDS, ST_BUCKET_ACC, ST_REDUCE, ST_COMBINE, ST_BATCH_SORT, N_STAGES };
+// The sqrt-PST stages carry the reference's Timer labels (sqrt_pst.rs:33-262):
+// build_q, sqrt_commit = comm_list + ipp, sqrt_open = msm (U) + mipp_prove +
+// pst_open; their device spans (first command to last, across the opening's
+// streams) are recorded here, and the same names are roctx host ranges
+// (trace.h) for rocprofv3 --marker-trace.
+enum MsmStage {
+  ST_DECOMPOSE = 0, ST_SORT, ST_BOUNDS, ST_BUCKET_ACC, ST_REDUCE, ST_COMBINE, ST_BATCH_SORT,
+  ST_BUILD_Q, ST_SQRT_COMMIT, ST_COMM_LIST, ST_IPP, ST_SQRT_OPEN, ST_MSM_U, ST_MIPP_PROVE, ST_PST_OPEN,
+  N_STAGES
+};
 
 struct Profiler {
   bool on = false;

@@ -6,6 +6,7 @@
 #include "msm.h"
 #include "pair_fq2.h"
 #include "glv.h"
+#include "field29.h"
 #include <type_traits>
 
 namespace tpst {
@@ -421,10 +422,20 @@ static __global__ void __launch_bounds__(SORTB_THREADS)
   uint32_t* sval = sm + 2 * D;  // staged values
   const uint32_t b = blockIdx.x, t = threadIdx.x;
   const uint32_t s = start[b], len = start[b + 1] - s;
+  if ((b << lo) >= sent) {
+    // the sentinel bin (zero digits; sent = W nb is a multiple of 2^lo when
+    // lo <= c - 1): nothing reads entries past range[W] -- the short chunks
+    // stop at range[whi], the long-chunk pass at range[W] -- so a bin that can
+    // hold most of m entries (small or boolean scalars) costs nothing here
+    if (t == 0 && (b << lo) == sent) range[W] = s;
+    return;
+  }
   for (uint32_t d = t; d < D; d += SORTB_THREADS) off[d] = 0;
   __syncthreads();
   const bool fits = len <= (uint32_t)SORTB_CAP;
   uint32_t kk[SORTB_IT], vv[SORTB_IT];
+  // sentinel entries of a mixed last bin (lo > c - 1: small MSMs) are not
+  // counted: they fill the bin's tail [nz, len) after the sorted entries
   if (fits) {
 #pragma unroll
     for (int k = 0; k < SORTB_IT; k++) {
@@ -436,9 +447,12 @@ static __global__ void __launch_bounds__(SORTB_THREADS)
     }
 #pragma unroll
     for (int k = 0; k < SORTB_IT; k++)
-      if (k * SORTB_THREADS + t < len) atomicAdd(&off[kk[k] & mask], 1u);
+      if (k * SORTB_THREADS + t < len && kk[k] < sent) atomicAdd(&off[kk[k] & mask], 1u);
   } else {
-    for (uint32_t p = t; p < len; p += SORTB_THREADS) atomicAdd(&off[keys2[s + p] & mask], 1u);
+    for (uint32_t p = t; p < len; p += SORTB_THREADS) {
+      const uint32_t key = keys2[s + p];
+      if (key < sent) atomicAdd(&off[key & mask], 1u);
+    }
   }
   __syncthreads();
   // exclusive scan of the counts: per-thread runs, wave scan, wave totals
@@ -455,8 +469,11 @@ static __global__ void __launch_bounds__(SORTB_THREADS)
   }
   if ((t & 63) == 63) wsum[t >> 6] = incl;
   __syncthreads();
-  uint32_t acc = incl - sum;
-  for (uint32_t w = 0; w < (t >> 6); w++) acc += wsum[w];
+  uint32_t acc = incl - sum, nz = 0;
+  for (uint32_t w = 0; w < SORTB_THREADS / 64; w++) {
+    if (w < (t >> 6)) acc += wsum[w];
+    nz += wsum[w];  // entries with a bucket key
+  }
   for (uint32_t k = 0; k < per; k++) {
     const uint32_t d = d0 + k;
     if (d >= D) break;
@@ -481,9 +498,9 @@ static __global__ void __launch_bounds__(SORTB_THREADS)
   if (fits) {
 #pragma unroll
     for (int k = 0; k < SORTB_IT; k++)
-      if (k * SORTB_THREADS + t < len) sval[atomicAdd(&cur[kk[k] & mask], 1u)] = vv[k];
+      if (k * SORTB_THREADS + t < len && kk[k] < sent) sval[atomicAdd(&cur[kk[k] & mask], 1u)] = vv[k];
     __syncthreads();
-    for (uint32_t p = t; p < len; p += SORTB_THREADS) {
+    for (uint32_t p = t; p < nz; p += SORTB_THREADS) {
       uint32_t a = 0, z = D;  // first bucket offset > p
       while (a < z) {
         const uint32_t mid = (a + z) >> 1;
@@ -498,12 +515,39 @@ static __global__ void __launch_bounds__(SORTB_THREADS)
   } else {
     for (uint32_t p = t; p < len; p += SORTB_THREADS) {
       const uint32_t key = keys2[s + p];
+      if (key >= sent) continue;
       const uint32_t pos = s + atomicAdd(&cur[key & mask], 1u);
       keys[pos] = key;
       vals[pos] = vals2[s + p];
     }
   }
+  for (uint32_t p = nz + t; p < len; p += SORTB_THREADS) keys[s + p] = sent;
 }
+
+// Compute field of the G1 bucket accumulation: the radix-2^29 Fq of
+// field29.h (one v_mad_u64_u32 per limb product, no carry chain); points are
+// converted as they are gathered and bucket pieces as they are stored, so
+// everything outside the accumulation kernels keeps field.h's layout.  G2
+// (Fq2) accumulates in its own field.  TPST_ACC29=0 selects field.h for A/B.
+template <class F>
+struct AccField {
+  using T = F;
+  static __device__ __forceinline__ Affine<T> in(const Affine<F>& a) { return a; }
+  static __device__ __forceinline__ Xyzz<F> out(const Xyzz<T>& a) { return a; }
+};
+#ifndef TPST_ACC29
+#define TPST_ACC29 1
+#endif
+#if TPST_ACC29
+template <>
+struct AccField<Fq> {
+  using T = Fq29;
+  static __device__ __forceinline__ Affine<T> in(const Affine<Fq>& a) { return {from_std(a.x), from_std(a.y)}; }
+  static __device__ __forceinline__ Xyzz<Fq> out(const Xyzz<T>& a) {
+    return {to_std(a.X), to_std(a.Y), to_std(a.ZZ), to_std(a.ZZZ)};
+  }
+};
+#endif
 
 template <class F>
 __device__ __forceinline__ Affine<F> fetch_point(const uint32_t* bases, const uint32_t* phib, uint32_t nbase,
@@ -527,27 +571,31 @@ __device__ __forceinline__ Affine<F> fetch_point(const uint32_t* bases, const ui
 // the current mixed add runs (software prefetch).
 template <class F>
 __global__ void __launch_bounds__(ACC_BLOCK, (sizeof(F) > 48 ? 1 : 2))
-    k_bucket_acc_chunk(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals, size_t m,
-                       uint32_t sent, const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend,
+    k_bucket_acc_chunk(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals, size_t m_all,
+                       const uint32_t* __restrict__ mend, uint32_t sent, const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend,
                        const uint32_t* __restrict__ bases, const uint32_t* __restrict__ phib, uint32_t nbase,
                        int lg, Xyzz<F>* __restrict__ buckets, Xyzz<F>* __restrict__ part,
                        Xyzz<F>* __restrict__ bpart) {
   const size_t t = (size_t)blockIdx.x * ACC_BLOCK + threadIdx.x;
   const size_t c0 = t << lg;
+  // entries with a bucket key: range[W] for msm_var (its sentinel tail is never sorted)
+  const size_t m = mend ? (size_t)*mend : m_all;
   uint32_t tail_key = sent;
   Xyzz<F> tail = Xyzz<F>::inf();
   if (c0 < m) {
+    using A = AccField<F>;
+    using C = typename A::T;
     const size_t c1 = (c0 + ((size_t)1 << lg) < m) ? c0 + ((size_t)1 << lg) : m;
     uint32_t key = keys[c0];
-    Affine<F> pt;
-    if (key < sent) pt = fetch_point<F>(bases, phib, nbase, vals[c0]);
-    Xyzz<F> acc = Xyzz<F>::inf();
+    Affine<C> pt;
+    if (key < sent) pt = A::in(fetch_point<F>(bases, phib, nbase, vals[c0]));
+    Xyzz<C> acc = Xyzz<C>::inf();
     for (size_t e = c0; e < c1; e++) {
       uint32_t key_n = sent;
-      Affine<F> pt_n;
+      Affine<C> pt_n;
       if (e + 1 < c1) {
         key_n = keys[e + 1];
-        if (key_n < sent) pt_n = fetch_point<F>(bases, phib, nbase, vals[e + 1]);
+        if (key_n < sent) pt_n = A::in(fetch_point<F>(bases, phib, nbase, vals[e + 1]));
       }
       if (key < sent) {
         acc = add_affine(acc, pt);
@@ -555,14 +603,14 @@ __global__ void __launch_bounds__(ACC_BLOCK, (sizeof(F) > 48 ? 1 : 2))
           const bool starts = bstart[key] >= c0;
           const bool ends = bend[key] <= c1;
           if (starts && ends) {
-            store_xyzz(buckets, key, acc);
+            store_xyzz(buckets, key, A::out(acc));
           } else if (starts) {  // only the chunk's last segment can continue
-            tail = acc;
+            tail = A::out(acc);
             tail_key = key;
           } else {  // only the chunk's first segment can have begun earlier
-            store_xyzz(part, t, acc);
+            store_xyzz(part, t, A::out(acc));
           }
-          acc = Xyzz<F>::inf();
+          acc = Xyzz<C>::inf();
         }
       }
       key = key_n;
@@ -587,14 +635,15 @@ __global__ void __launch_bounds__(ACC_BLOCK, (sizeof(F) > 48 ? 1 : 2))
 // plus the leading pieces of the chunks after B up to the bucket's last one
 template <class F>
 __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
-    k_bucket_fixup(const uint32_t* __restrict__ keys, size_t m, uint32_t sent, const uint32_t* __restrict__ bstart,
-                   const uint32_t* __restrict__ bend, int lg, size_t nblk, const Xyzz<F>* __restrict__ part,
-                   const Xyzz<F>* __restrict__ bpart, Xyzz<F>* __restrict__ buckets) {
+    k_bucket_fixup(const uint32_t* __restrict__ keys, size_t m_all, const uint32_t* __restrict__ mend, uint32_t sent,
+                   const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend, int lg, size_t nblk,
+                   const Xyzz<F>* __restrict__ part, const Xyzz<F>* __restrict__ bpart,
+                   Xyzz<F>* __restrict__ buckets) {
   const size_t B = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (B + 1 >= nblk) return;
   const int lb = lg + ACC_BLOCK_LG;
   const size_t e = (B + 1) << lb;  // first entry of workgroup B + 1
-  if (e >= m) return;
+  if (e >= (mend ? (size_t)*mend : m_all)) return;
   const uint32_t key = keys[e];
   if (key >= sent || keys[e - 1] != key || ((size_t)bstart[key] >> lb) != B) return;
   const size_t t1 = ((size_t)bend[key] - 1) >> lg;
@@ -625,16 +674,18 @@ __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
   if (c0 >= e_hi) return;
   const size_t c1 = (c0 + ((size_t)1 << lg) < e_hi) ? c0 + ((size_t)1 << lg) : e_hi;
   if (c0 < e_lo) c0 = e_lo;
+  using A = AccField<F>;
+  using C = typename A::T;
   uint32_t key = keys[c0];
-  Affine<F> pt;
-  if (key < sent) pt = fetch_point<F>(bases, phib, nbase, vals[c0]);
-  Xyzz<F> acc = Xyzz<F>::inf();
+  Affine<C> pt;
+  if (key < sent) pt = A::in(fetch_point<F>(bases, phib, nbase, vals[c0]));
+  Xyzz<C> acc = Xyzz<C>::inf();
   for (size_t e = c0; e < c1; e++) {
     uint32_t key_n = sent;
-    Affine<F> pt_n;
+    Affine<C> pt_n;
     if (e + 1 < c1) {
       key_n = keys[e + 1];
-      if (key_n < sent) pt_n = fetch_point<F>(bases, phib, nbase, vals[e + 1]);
+      if (key_n < sent) pt_n = A::in(fetch_point<F>(bases, phib, nbase, vals[e + 1]));
     }
     if (key < sent) {
       acc = add_affine(acc, pt);
@@ -642,10 +693,10 @@ __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
         const bool starts = bstart[key] >= c0;
         const bool ends = bend[key] <= c1;
         if (starts && ends)
-          store_xyzz(buckets, key, acc);
+          store_xyzz(buckets, key, A::out(acc));
         else
-          store_xyzz(part, 2 * t + (starts ? 1 : 0), acc);
-        acc = Xyzz<F>::inf();
+          store_xyzz(part, 2 * t + (starts ? 1 : 0), A::out(acc));
+        acc = Xyzz<C>::inf();
       }
     }
     key = key_n;
@@ -704,12 +755,56 @@ static __global__ void __launch_bounds__(64, 2)
   }
 }
 
+// Buckets spanning more than LONG_PARTS chunks (many equal digits: small or
+// boolean scalars put most entries of a window into one bucket) are not
+// walked by one lane of the fixups below -- 2^20 entries of one bucket would
+// be a 32 768-add serial chain -- but appended to a per-group list and summed
+// by k_bucket_fixup_long, one workgroup per bucket (strided partial sums, then
+// a tree in LDS).  cap bounds the list: every listed bucket covers more than
+// LONG_PARTS whole chunks of its group's entries.
+constexpr uint32_t LONG_PARTS = 64;
+constexpr int LONG_THREADS = 256;
+constexpr unsigned LONG_GRID = 32;
+struct LongList {
+  uint32_t* cnt;
+  uint32_t* list;
+  uint32_t cap;
+  __device__ __forceinline__ void push(uint32_t b) const {
+    const uint32_t i = atomicAdd(cnt, 1u);
+    if (i < cap) list[i] = b;
+  }
+};
+
+template <class F>
+__global__ void __launch_bounds__(LONG_THREADS) k_bucket_fixup_long(const uint32_t* __restrict__ bstart,
+                                                                    const uint32_t* __restrict__ bend, int lg,
+                                                                    const Xyzz<F>* __restrict__ part,
+                                                                    Xyzz<F>* __restrict__ buckets, LongList ll) {
+  __shared__ Xyzz<F> sh[LONG_THREADS];
+  const uint32_t n = *ll.cnt < ll.cap ? *ll.cnt : ll.cap;
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint32_t b = ll.list[i];
+    const size_t t0 = (size_t)bstart[b] >> lg, t1 = (size_t)(bend[b] - 1) >> lg;
+    Xyzz<F> acc = tid == 0 ? load_xyzz(part, 2 * t0 + 1) : Xyzz<F>::inf();
+    for (size_t t = t0 + 1 + tid; t <= t1; t += LONG_THREADS) acc = add(acc, load_xyzz(part, 2 * t));
+    sh[tid] = acc;
+    __syncthreads();
+    for (uint32_t h = LONG_THREADS / 2; h > 0; h >>= 1) {
+      if (tid < h) sh[tid] = add(sh[tid], sh[tid + h]);
+      __syncthreads();
+    }
+    if (tid == 0) store_xyzz(buckets, b, sh[0]);
+    __syncthreads();
+  }
+}
+
 // k_bucket_fixup_short over G2 with pair-distributed Fq2: lanes 2b, 2b+1
 // finish bucket b0 + b together
 static __global__ void __launch_bounds__(64, 2)
     k_bucket_fixup_short_pair(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend, size_t b0,
                               size_t b1, int lg, const Xyzz<Fq2>* __restrict__ part, Xyzz<Fq2>* __restrict__ buckets,
-                              int prio) {
+                              int prio, LongList ll) {
   set_wave_prio(prio);
   const size_t b = b0 + (((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 1);
   if (b >= b1) return;
@@ -717,6 +812,10 @@ static __global__ void __launch_bounds__(64, 2)
   if (e <= s) return;
   const size_t t0 = (size_t)s >> lg, t1 = (size_t)(e - 1) >> lg;
   if (t0 == t1) return;
+  if (t1 - t0 > LONG_PARTS) {
+    if (!(threadIdx.x & 1)) ll.push((uint32_t)b);
+    return;
+  }
   Xyzz<Fq2P> acc = load_xyzz_pair(part, 2 * t0 + 1);
   for (size_t t = t0 + 1; t <= t1; t++) acc = add(acc, load_xyzz_pair(part, 2 * t));
   store_xyzz_pair(buckets, b, acc);
@@ -728,7 +827,7 @@ template <class F>
 __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
     k_bucket_fixup_short(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend, size_t b0,
                          size_t b1, int lg, const Xyzz<F>* __restrict__ part, Xyzz<F>* __restrict__ buckets,
-                         int prio) {
+                         int prio, LongList ll) {
   set_wave_prio(prio);
   const size_t b = b0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= b1) return;
@@ -736,6 +835,10 @@ __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
   if (e <= s) return;
   const size_t t0 = (size_t)s >> lg, t1 = (size_t)(e - 1) >> lg;
   if (t0 == t1) return;
+  if (t1 - t0 > LONG_PARTS) {
+    ll.push((uint32_t)b);
+    return;
+  }
   Xyzz<F> acc = load_xyzz(part, 2 * t0 + 1);
   for (size_t t = t0 + 1; t <= t1; t++) acc = add(acc, load_xyzz(part, 2 * t));
   store_xyzz(buckets, b, acc);
@@ -748,7 +851,7 @@ template <class F>
 __global__ void __launch_bounds__(64) k_bucket_fixup_quad(const uint32_t* __restrict__ bstart,
                                                           const uint32_t* __restrict__ bend, size_t b0, size_t b1,
                                                           int lg, const Xyzz<F>* __restrict__ part,
-                                                          Xyzz<F>* __restrict__ buckets) {
+                                                          Xyzz<F>* __restrict__ buckets, LongList ll) {
   const size_t b = b0 + (((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2);
   const int qi = threadIdx.x & 3;
   if (b >= b1) return;  // quad-uniform
@@ -756,6 +859,10 @@ __global__ void __launch_bounds__(64) k_bucket_fixup_quad(const uint32_t* __rest
   if (e <= s) return;
   const size_t t0 = (size_t)s >> lg, t1 = (size_t)(e - 1) >> lg;
   if (t0 == t1) return;
+  if (t1 - t0 > LONG_PARTS) {
+    if (qi == 0) ll.push((uint32_t)b);
+    return;
+  }
   Xyzz<F> acc = load_xyzz(part, 2 * t0 + 1);
   for (size_t t = t0 + 1; t <= t1; t++) acc = add_quad(acc, load_xyzz(part, 2 * t), qi);
   if (qi == 0) store_xyzz(buckets, b, acc);
@@ -1186,7 +1293,8 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
                 Arena::need(2 * nchunk, sizeof(Xyzz<F>)) + Arena::need(nblk, sizeof(Xyzz<F>)) + red_need +
                 Arena::need(W, sizeof(Xyzz<F>)) + Arena::need(NG, sizeof(Xyzz<F>)) + Arena::need(W + 1, 4) +
                 Arena::need(glv ? n * PW : 1, 4) + Arena::need((size_t)sp.ntile * sp.nbins, 4) +
-                Arena::need(sp.nbins, 4) + Arena::need(sp.nbins + 1, 4) + 8192;
+                Arena::need(sp.nbins, 4) + Arena::need(sp.nbins + 1, 4) + Arena::need(NG, 4) +
+                Arena::need((size_t)NG * ((m >> (lg + 6)) + 1), 4) + 8192;
   ar.reset();
   TPST_TRY(ar.reserve(need));
   uint32_t* keys = ar.take<uint32_t>(m);
@@ -1205,11 +1313,15 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   uint32_t* tab = ar.take<uint32_t>((size_t)sp.ntile * sp.nbins);
   uint32_t* btot = ar.take<uint32_t>(sp.nbins);
   uint32_t* bin0 = ar.take<uint32_t>(sp.nbins + 1);
+  const uint32_t lcap = (uint32_t)(m >> (lg + 6)) + 1;  // LONG_PARTS = 2^6 whole chunks per listed bucket
+  uint32_t* lcnt = ar.take<uint32_t>(NG);
+  uint32_t* llist = ar.take<uint32_t>((size_t)NG * lcap);
 
   Profiler* pf = ar.prof;
   Profiler dummy;
   if (!pf) pf = &dummy;
   pf->begin(ST_DECOMPOSE, s);
+  if (short_chunks) TPST_TRY(hipMemsetAsync(lcnt, 0, NG * sizeof(uint32_t), s));
   k_decompose_hist<F><<<sp.ntile, SORT_THREADS, sp.nbins * 4, s>>>(d_scalars, n, c, W, glv ? 1 : 0, sent, sp.lo,
                                                                   sp.nbins, sp.tile, keys, vals, tab, d_bases, phib);
   TPST_TRY(hipGetLastError());
@@ -1244,10 +1356,10 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   pf->end(ST_SORT, s);
   if (!short_chunks) {  // one launch, long chunks (more than ~2^21 points)
     pf->begin(ST_BUCKET_ACC, s);
-    k_bucket_acc_chunk<F><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys, vals, m, sent, bstart, bend, d_bases, phib,
-                                                                (uint32_t)n, lg, buckets, part, bpart);
+    k_bucket_acc_chunk<F><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys, vals, m, range + W, sent, bstart, bend,
+                                                                d_bases, phib, (uint32_t)n, lg, buckets, part, bpart);
     TPST_TRY(hipGetLastError());
-    k_bucket_fixup<F><<<grid_for(nblk, 64), 64, 0, s>>>(keys, m, sent, bstart, bend, lg, nblk, part, bpart,
+    k_bucket_fixup<F><<<grid_for(nblk, 64), 64, 0, s>>>(keys, m, range + W, sent, bstart, bend, lg, nblk, part, bpart,
                                                         buckets);
     TPST_TRY(hipGetLastError());
     pf->end(ST_BUCKET_ACC, s);
@@ -1285,14 +1397,17 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
       TPST_TRY(hipEventRecord(ar.aux_ev[2 * g], bulk));
       TPST_TRY(hipStreamWaitEvent(a, ar.aux_ev[2 * g], 0));
     }
+    const LongList ll{lcnt + g, llist + (size_t)g * lcap, lcap};
     if constexpr (std::is_same<F, Fq2>::value)
       k_bucket_fixup_short_pair<<<grid_for(2 * (b1 - b0), 64), 64, 0, a>>>(bstart, bend, b0, b1, lg, part, buckets,
-                                                                          g ? red_prio() : 0);
+                                                                          g ? red_prio() : 0, ll);
     else if (g < fixup_quad_groups())
-      k_bucket_fixup_quad<F><<<grid_for(4 * (b1 - b0), 64), 64, 0, a>>>(bstart, bend, b0, b1, lg, part, buckets);
+      k_bucket_fixup_quad<F><<<grid_for(4 * (b1 - b0), 64), 64, 0, a>>>(bstart, bend, b0, b1, lg, part, buckets, ll);
     else
       k_bucket_fixup_short<F><<<grid_for(b1 - b0, 64), 64, 0, a>>>(bstart, bend, b0, b1, lg, part, buckets,
-                                                                    g ? red_prio() : 0);
+                                                                    g ? red_prio() : 0, ll);
+    TPST_TRY(hipGetLastError());
+    k_bucket_fixup_long<F><<<LONG_GRID, LONG_THREADS, 0, a>>>(bstart, bend, lg, part, buckets, ll);
     TPST_TRY(hipGetLastError());
     if (g == 0) break;
     if (red2_mode() >= 1 && red2_ok(nb))
@@ -1717,12 +1832,12 @@ hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint3
   TPST_TRY(hipGetLastError());
   pf->end(ST_BATCH_SORT, s);
   pf->begin(ST_BUCKET_ACC, s);
-  k_bucket_acc_chunk<Fq><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys, entries, m, (uint32_t)nbk, bstart, bend,
-                                                               t.d_table, nullptr, 0x7fffffffu, lg, buckets, part,
-                                                               bpart);
+  k_bucket_acc_chunk<Fq><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys, entries, m, nullptr, (uint32_t)nbk, bstart,
+                                                               bend, t.d_table, nullptr, 0x7fffffffu, lg, buckets,
+                                                               part, bpart);
   TPST_TRY(hipGetLastError());
-  k_bucket_fixup<Fq><<<grid_for(nblk, 64), 64, 0, s>>>(keys, m, (uint32_t)nbk, bstart, bend, lg, nblk, part, bpart,
-                                                       buckets);
+  k_bucket_fixup<Fq><<<grid_for(nblk, 64), 64, 0, s>>>(keys, m, nullptr, (uint32_t)nbk, bstart, bend, lg, nblk,
+                                                       part, bpart, buckets);
   TPST_TRY(hipGetLastError());
   pf->end(ST_BUCKET_ACC, s);
   pf->begin(ST_REDUCE, s);

@@ -643,7 +643,7 @@ hipError_t multi_pairing(Arena& ar, hipStream_t s, const uint32_t* d_g1, const u
 // the cyclotomic subgroup (order Phi12(p), so cyclotomic squaring applies),
 // and then f^p == f^x puts it in GT, because gcd(p - x, Phi12(p)) = r for
 // BLS12-377 (tests/test_kat_ref.py checks it).  ok[i] = 1 iff f_i is in GT
-// (out[i] is only meaningful then).
+// (out[i] is only meaningful then); f = 0 is rejected first.
 constexpr int GP_REGS = 20;  // R0 scratch, T1..T15 subset table, ACC, TMP, X1, X2
 constexpr size_t GP_LDS = (size_t)(FW_PROG + (wave::N_CONSTS + 64 + 12 * GP_REGS) * wave::SLOT) * 4;
 static_assert(GP_LDS <= 65536, "GT pow kernel LDS");
@@ -678,7 +678,12 @@ __global__ void __launch_bounds__(64) k_gt_pow_wave(const Fq12* __restrict__ bas
   wave::load_f12(vals, R(1), base + i);
   const bool check = ok != nullptr;
   bool good = true;
-  if (check) {  // cyclotomic subgroup: f^(p^4) f == f^(p^2)
+  if (check) {
+    // f = 0 passes both equations below but is not in GT (Validate::Yes rejects it)
+    const int ln = threadIdx.x & 63;
+    good = __any((ln < 12 && !is_zero(wave::get_slot(vals, R(1) + ln))) ? 1 : 0) != 0;
+  }
+  if (check && good) {  // cyclotomic subgroup: f^(p^4) f == f^(p^2)
     wave::run(e, P + FE_SET.off[FE_FROB2], R(1), 0, X1);
     wave::run(e, P + FE_SET.off[FE_FROB2], X1, 0, X2);
     wave::run(e, P + FE_SET.off[FE_MUL], X2, R(1), R(0));

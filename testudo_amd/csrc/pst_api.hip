@@ -16,6 +16,7 @@
 #include "host_curve.h"
 #include "device_util.h"
 #include "pst_kernels.h"
+#include "trace.h"
 
 using namespace tpst;
 
@@ -809,7 +810,9 @@ extern "C" void tpst_poly_free(tpst_poly* p) { delete p; }
 
 // get_q (sqrt_pst.rs:81-101): chis over b = point[m_row..], q = Z^T chis
 static int poly_get_q(tpst_ctx* ctx, tpst_poly* p, const uint64_t* point) {
+  TraceRange tr("build_q");
   hipStream_t s = ctx->stream;
+  ctx->prof.begin(ST_BUILD_Q, s);
   DevBuf b;
   TPST_HIP(ctx, b.alloc((size_t)(p->m_col ? p->m_col : 1) * 32));
   if (p->m_col) {
@@ -820,6 +823,7 @@ static int poly_get_q(tpst_ctx* ctx, tpst_poly* p, const uint64_t* point) {
   TPST_HIP(ctx, p->q.alloc(((size_t)1 << p->m_row) * 32));
   TPST_HIP(ctx, chi_table(s, b.u(), p->m_col, p->chis.u()));
   TPST_HIP(ctx, get_q(s, p->d_Z, p->m_col, p->m_row, p->chis.u(), p->q.u()));
+  ctx->prof.end(ST_BUILD_Q, s);
   TPST_HIP(ctx, hipStreamSynchronize(s));
   p->has_q = true;
   return TPST_OK;
@@ -859,17 +863,31 @@ static int poly_commit_dev(tpst_ctx* ctx, tpst_poly* p, uint32_t* d_comms_mont, 
   ctx->arena2.reset();
   TPST_HIP(ctx, ctx->arena2.reserve(Arena::need(C, sizeof(Xyzz<Fq>)) + 256));
   Xyzz<Fq>* rows = ctx->arena2.take<Xyzz<Fq>>(C);
-  TPST_HIP(ctx, msm_batch(ctx->arena, s, st->tables, p->d_Z, C, 1, C, rows));
-  TPST_HIP(ctx, xyzz_to_affine_mont<Fq>(s, rows, d_comms_mont, C));
-  const LineCoeff* hp = (const LineCoeff*)st->hprep[p->odd].p;
-  ctx->arena.reset();
-  TPST_HIP(ctx, ctx->arena.reserve(multi_pairing_scratch(1, C)));
-  TPST_HIP(ctx, multi_pairing_prepared(ctx->arena, s, d_comms_mont, st->ph[p->odd]->u(), hp, 1, C, d_T));
+  Profiler& pf = ctx->prof;
+  pf.begin(ST_SQRT_COMMIT, s);
+  {
+    TraceRange tr("comm_list");  // sqrt_pst.rs:119-126
+    pf.begin(ST_COMM_LIST, s);
+    TPST_HIP(ctx, msm_batch(ctx->arena, s, st->tables, p->d_Z, C, 1, C, rows));
+    TPST_HIP(ctx, xyzz_to_affine_mont<Fq>(s, rows, d_comms_mont, C));
+    pf.end(ST_COMM_LIST, s);
+  }
+  {
+    TraceRange tr("ipp");  // sqrt_pst.rs:131-144
+    pf.begin(ST_IPP, s);
+    const LineCoeff* hp = (const LineCoeff*)st->hprep[p->odd].p;
+    ctx->arena.reset();
+    TPST_HIP(ctx, ctx->arena.reserve(multi_pairing_scratch(1, C)));
+    TPST_HIP(ctx, multi_pairing_prepared(ctx->arena, s, d_comms_mont, st->ph[p->odd]->u(), hp, 1, C, d_T));
+    pf.end(ST_IPP, s);
+  }
+  pf.end(ST_SQRT_COMMIT, s);
   return TPST_OK;
 }
 
 extern "C" int tpst_poly_commit(tpst_ctx* ctx, tpst_poly* p, uint64_t* comms, uint64_t* T) {
   if (!ctx || !p || !comms || !T) return fail(ctx, TPST_E_ARG, "null argument");
+  TraceRange tr("sqrt_commit");
   std::lock_guard<std::mutex> lk(ctx->mu);
   if (int rc = poly_need_full(ctx, p)) return rc;
   TPST_HIP(ctx, hipSetDevice(ctx->device));
@@ -1342,10 +1360,13 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   if (st->nv != p->m_row) return fail(ctx, TPST_E_ARG, "SRS num_vars != ceil(n/2)");
   for (size_t i = 0; i < ((size_t)2 << p->m_col); i++)
     if (!fq_ok(comms + 6 * i)) return fail(ctx, TPST_E_ARG, "comm_list coordinate >= p");
-  if (!p->has_q) {
+  if (!p->has_q) {  // before the reference's open timer (sqrt_pst.rs:177-183)
     int rc = poly_get_q(ctx, p, point);
     if (rc) return rc;
   }
+  TraceRange trace_open("sqrt_open");
+  Profiler& pf = ctx->prof;
+  pf.begin(ST_SQRT_OPEN, ctx->stream);
   {
     int rc = srs_fbt(ctx, st, p->odd);
     if (rc) return rc;
@@ -1457,6 +1478,8 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   TPST_HIP(ctx, fr_from_mont(sA, p->chis.u(), chiC.u(), C));
   TPST_HIP(ctx, hipEventRecord(ev[EV_PRE], sA));
   for (hipStream_t s2 : {sB, sLA[0], sLA[1]}) TPST_HIP(ctx, hipStreamWaitEvent(s2, ev[EV_PRE], 0));
+  pf.begin(ST_MIPP_PROVE, sA);  // mipp.rs:38-149 (sqrt_pst.rs:211-214)
+  TraceRange trace_mipp("mipp_prove");
 
   // ---- look-ahead stream 1 (idle until round 1): the fold table over comm_list
   TPST_HIP(ctx, fbt_build<Fq>(*arLA[1], sLA[1], A.u(), C, st->t_A.u(), true));
@@ -1468,17 +1491,22 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     TPST_HIP(ctx, hipEventRecord(ev[EV_U], sB));
   } else {
     TPST_HIP(ctx, hipStreamWaitEvent(sB, ev[EV_TABLE], 0));
+    TraceRange trace_msm("msm");  // sqrt_pst.rs:188-199
+    pf.begin(ST_MSM_U, sB);
     FbGroups gu;
     gu.members = C;
     gu.L = gu.D = C;
     gu.glv = true;
     TPST_HIP(ctx, fbt_msm<Fq>(arB, sB, tA, chiC.u(), gu, (Xyzz<Fq>*)xd.p));
     TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(sB, (Xyzz<Fq>*)xd.p, canD.u(), 1));
+    pf.end(ST_MSM_U, sB);
     TPST_HIP(ctx, hipMemcpyAsync(pin + dn_U, canD.p, 96, hipMemcpyDeviceToHost, sB));
     TPST_HIP(ctx, hipEventRecord(ev[EV_U], sB));
   }
   // PST proof of q at a_rev (stream B, after round 0's cross terms)
   auto pst_q = [&]() -> int {
+    TraceRange trace_pst("pst_open");  // sqrt_pst.rs:216-226
+    pf.begin(ST_PST_OPEN, sB);
     const size_t a_off = up_off[m] + (2 + m) * 32;
     TPST_HIP(ctx, hipMemcpyAsync(dup(a_off), pin + a_off, (size_t)k * 32, hipMemcpyHostToDevice, sB));
     TPST_HIP(ctx, fr_to_mont(sB, dup(a_off), dup(a_off), k));
@@ -1487,6 +1515,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     TPST_HIP(ctx, xyzz_to_affine_canonical<Fq2>(sB, x2, canD.u() + 24, k));
     TPST_HIP(ctx, hipMemcpyAsync(pin + dn_final + 96 + 192 + (size_t)m * 96, canD.u() + 24, (size_t)k * 192,
                                  hipMemcpyDeviceToHost, sB));
+    pf.end(ST_PST_OPEN, sB);
     return TPST_OK;
   };
   if (m == 0)
@@ -1718,6 +1747,14 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
                                  sB));
   }
   TPST_HIP(ctx, hipEventRecord(ev[EV_B_DONE], sB));
+  if (pf.on) {  // device spans end when every stream of the opening has drained
+    TPST_HIP(ctx, hipEventRecord(ev[EV_D_DONE], sLA[0]));
+    TPST_HIP(ctx, hipEventRecord(ev[EV_A_DONE], sLA[1]));
+    for (int e : {(int)EV_B_DONE, (int)EV_C_DONE, (int)EV_D_DONE, (int)EV_A_DONE})
+      TPST_HIP(ctx, hipStreamWaitEvent(sA, ev[e], 0));
+    pf.end(ST_MIPP_PROVE, sA);
+    pf.end(ST_SQRT_OPEN, sA);
+  }
   for (hipStream_t s2 : {sA, sB, sLA[0], sLA[1]}) TPST_HIP(ctx, hipStreamSynchronize(s2));
   memcpy(proof->final_a, pin + dn_final, 96);
   memcpy(proof->final_h, pin + dn_final + 96, 192);
@@ -2044,11 +2081,18 @@ extern "C" int tpst_pst_verify(tpst_ctx* ctx, tpst_transcript* tr, int n, const 
   // T check, device side first (side stream): t_l^{c_inv}, t_r^{c} for every
   // round after a GT membership test of each (mipp.rs:263-283)
   const size_t k = 2 * (size_t)m;
-  if (int rc = open_streams(ctx, 8, 0)) return rc;
+  if (int rc = open_streams(ctx, 8, k * (sizeof(Fq12) + 4))) return rc;
   hipStream_t s2 = ctx->side[0];
   DevBuf db, de, dout, dok;
-  std::vector<Fq12> pw(k);
-  std::vector<uint32_t> okv(k);
+  // the powers and flags come back into the context's pinned staging (a true
+  // async copy); every return path below drains s2 first (the guard is
+  // destroyed before the device buffers the copies read)
+  Fq12* pw = reinterpret_cast<Fq12*>(ctx->pinned);
+  uint32_t* okv = reinterpret_cast<uint32_t*>(pw + k);
+  struct Drain {
+    hipStream_t s;
+    ~Drain() { (void)hipStreamSynchronize(s); }
+  } drain{s2};
   if (k) {
     std::vector<uint32_t> bases;
     std::vector<uint64_t> dg(4 * k);
@@ -2071,8 +2115,8 @@ extern "C" int tpst_pst_verify(tpst_ctx* ctx, tpst_transcript* tr, int n, const 
     TPST_HIP(ctx, hipMemcpyAsync(db.p, bases.data(), k * sizeof(Fq12), hipMemcpyHostToDevice, s2));
     TPST_HIP(ctx, hipMemcpyAsync(de.p, dg.data(), k * 32, hipMemcpyHostToDevice, s2));
     TPST_HIP(ctx, gt_pow_wave(s2, (const Fq12*)db.p, (const uint64_t*)de.p, k, (Fq12*)dout.p, dok.u()));
-    TPST_HIP(ctx, hipMemcpyAsync(pw.data(), dout.p, k * sizeof(Fq12), hipMemcpyDeviceToHost, s2));
-    TPST_HIP(ctx, hipMemcpyAsync(okv.data(), dok.p, k * 4, hipMemcpyDeviceToHost, s2));
+    TPST_HIP(ctx, hipMemcpyAsync(pw, dout.p, k * sizeof(Fq12), hipMemcpyDeviceToHost, s2));
+    TPST_HIP(ctx, hipMemcpyAsync(okv, dok.p, k * 4, hipMemcpyDeviceToHost, s2));
   }
   // host threads meanwhile: the U check's terms and the check / check_2 pairs
   // U check: uc = U + sum(c_inv u_l + c u_r) == final_y * final_a (mipp.rs:239-251)
@@ -2108,15 +2152,15 @@ extern "C" int tpst_pst_verify(tpst_ctx* ctx, tpst_transcript* tr, int n, const 
   std::vector<uint64_t> gts;
   if (int rc = pairing_groups(ctx, {&fin, &chk2, &chk}, gts)) return rc;
   TPST_HIP(ctx, hipStreamSynchronize(s2));
-  for (uint32_t o : okv)
-    if (!o) return fail(ctx, TPST_E_VERIFY, "comms_t element outside GT");
+  for (size_t i = 0; i < k; i++)
+    if (!okv[i]) return fail(ctx, TPST_E_VERIFY, "comms_t element outside GT");
   // T * prod t_l^{c_inv} t_r^{c} == e(final_a, final_h)
   Fq12 acc;
   {
     Fq* c = reinterpret_cast<Fq*>(&acc);
     for (int q = 0; q < 12; q++) c[q] = fq_canon(T + 6 * q);
   }
-  for (auto& x : pw) acc = mul(acc, x);
+  for (size_t i = 0; i < k; i++) acc = mul(acc, pw[i]);
   {
     const Fq* c = reinterpret_cast<const Fq*>(&acc);
     for (int q = 0; q < 12; q++) {

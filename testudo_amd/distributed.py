@@ -23,6 +23,13 @@ q and U, and rank 0 opens from q alone (no rank holds the whole Z).  The MIPP
 rounds, the PST proof of q and the final folds are transcript-sequential and
 KB-sized: they stay on rank 0.
 
+Split MSM (strong scaling): one variable-base MSM (sqrt_pst.rs:198,
+mipp.rs:393) over n points is cut into equal contiguous point ranges; each
+rank computes its range's sum as a raw XYZZ point (192 B, no per-rank affine
+inversion), one all-gather moves the shares as bytes and one device sums them
+(tpst_g1_xyzz_sum_dev) -- the "single reduce of partial bucket sums", done as
+a gather because RCCL has no elliptic-curve reduction.
+
 The per-rank compute and the combines are injected, so the orchestration is
 testable on CPU with the C++ oracle standing in for the GPU
 (tests/test_distributed.py).
@@ -109,3 +116,19 @@ def sharded_open_inputs(n: int, q_partial_into: Callable, cu_partial: Callable, 
     zq = combine_q(got[:, :N * 4].contiguous())
     U = combine_cu(got[:, N * 4:].cpu().numpy().view(np.uint64).copy())
     return zq, np.ascontiguousarray(U, dtype=np.uint64).reshape(12)
+
+
+def sharded_msm(n: int, msm_partial_into: Callable, combine: Callable, dist, device):
+    """Strong-scaled MSM over n points split evenly across the ranks.
+
+    msm_partial_into(i0, i1, out) fills the int64 tensor ``out`` (24 words on
+    the rank's device) with the XYZZ sum of points [i0, i1);
+    combine(gathered (world, 24) tensor) -> (12,) canonical affine, run on
+    rank 0.  Returns the MSM on rank 0, None elsewhere."""
+    import torch
+    dev = _device(dist, device)
+    i0, i1 = shard_rows(n, dist.get_world_size(), dist.get_rank())
+    buf = torch.empty(24, dtype=torch.int64, device=dev)
+    msm_partial_into(i0, i1, buf)
+    got = _all_gather(dist, buf)
+    return combine(got) if dist.get_rank() == 0 else None

@@ -107,7 +107,9 @@ class Context:
         return out
 
     # ------------------------------------------------------- profiling ---
-    STAGES = ("decompose", "sort", "bounds", "bucket_acc", "reduce", "combine", "batch_sort")
+    STAGES = ("decompose", "sort", "bounds", "bucket_acc", "reduce", "combine", "batch_sort",
+              # sqrt-PST stages under the reference's Timer labels (sqrt_pst.rs:33-262), device spans
+              "build_q", "sqrt_commit", "comm_list", "ipp", "sqrt_open", "msm", "mipp_prove", "pst_open")
 
     def profile(self, on: bool):
         self.check(self.lib.tpst_profile_enable(self.h, 1 if on else 0), "tpst_profile_enable")
@@ -126,9 +128,37 @@ class Context:
     def synchronize(self):
         self.check(self.lib.tpst_synchronize(self.h), "tpst_synchronize")
 
+    # ------------------------------------------- ordering against torch ---
+    # The library runs on its own non-blocking stream.  A device buffer that
+    # torch produced (all-gather output, a .contiguous() copy, torch.empty from
+    # the caching allocator) is handed to a _dev call only after torch_to_lib();
+    # a buffer the library filled is used by torch only after lib_to_torch().
+    @staticmethod
+    def _torch_stream(device):
+        import torch
+        return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+    def torch_to_lib(self):
+        """Library work queued from now on waits for torch's current stream."""
+        self.check(self.lib.tpst_wait_stream(self.h, self._torch_stream(self.device)), "tpst_wait_stream")
+
+    def lib_to_torch(self):
+        """Torch work queued from now on (current stream) waits for the library."""
+        self.check(self.lib.tpst_join_stream(self.h, self._torch_stream(self.device)), "tpst_join_stream")
+
     def g1_msm_dev(self, d_bases: int, d_scalars: int, n: int, d_out: int):
         self.check(self.lib.tpst_g1_msm_dev(self.h, C.c_void_p(d_bases), C.c_void_p(d_scalars), n,
                                             C.c_void_p(d_out)), "tpst_g1_msm_dev")
+
+    def g1_msm_xyzz_dev(self, d_bases: int, d_scalars: int, n: int, d_out: int):
+        """One rank's share of a split MSM: the raw XYZZ sum (24 u64, Montgomery) at d_out."""
+        self.check(self.lib.tpst_g1_msm_xyzz_dev(self.h, C.c_void_p(d_bases), C.c_void_p(d_scalars), n,
+                                                 C.c_void_p(d_out)), "tpst_g1_msm_xyzz_dev")
+
+    def g1_xyzz_sum_dev(self, d_parts: int, k: int, stride_bytes: int, d_out: int):
+        """Sum of k XYZZ shares (stride_bytes apart) -> one canonical affine G1 (12 u64) at d_out."""
+        self.check(self.lib.tpst_g1_xyzz_sum_dev(self.h, C.c_void_p(d_parts), k, stride_bytes, C.c_void_p(d_out)),
+                   "tpst_g1_xyzz_sum_dev")
 
     def g1_mul_generator_dev(self, d_scalars: int, n: int, d_out: int):
         self.check(self.lib.tpst_g1_mul_generator_dev(self.h, C.c_void_p(d_scalars), n, C.c_void_p(d_out)),

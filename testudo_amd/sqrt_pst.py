@@ -22,6 +22,15 @@ from .encoding import ptr
 from .engine import Context, TpstError
 
 
+def _torch_ready() -> bool:
+    """True when torch is importable with a GPU (stream ordering applies)."""
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except ImportError:
+        return False
+
+
 def _u64(a, shape=None):
     a = np.ascontiguousarray(a, dtype=np.uint64)
     return a if shape is None else a.reshape(shape)
@@ -208,6 +217,8 @@ class Polynomial:
     @classmethod
     def from_device(cls, ctx: Context, d_ptr: int, n: int, keep=None) -> "Polynomial":
         h = C.c_void_p()
+        if _torch_ready():
+            ctx.torch_to_lib()  # d_ptr may be a torch tensor written on torch's stream
         ctx.check(ctx.lib.tpst_poly_from_evaluations_dev(ctx.h, C.c_void_p(d_ptr), n, C.byref(h)),
                   "from_evaluations_dev")
         return cls(ctx, h, n, keep)
@@ -254,9 +265,11 @@ class Polynomial:
         72 words, [comms | Miller partial]): straight from device memory when
         ``out`` is a GPU tensor (the RCCL all-gather buffer), else via host."""
         if out.is_cuda:
+            self.ctx.torch_to_lib()  # `out` may come from torch's caching allocator
             self.ctx.check(self.ctx.lib.tpst_poly_commit_rows_partial_dev(self.ctx.h, self.h, r0, r1,
                                                                           C.c_void_p(out.data_ptr())),
                            "commit_rows_partial_dev")
+            self.ctx.lib_to_torch()  # the all-gather reads it on torch's stream
             return
         import torch
         cm, ml = self.commit_rows_partial(r0, r1)
@@ -274,9 +287,11 @@ class Polynomial:
         """get_q_partial into the int64 tensor ``out`` (device-side when it is a GPU tensor)."""
         if out.is_cuda:
             point = _u64(point, (self.n, 4))
+            self.ctx.torch_to_lib()
             self.ctx.check(self.ctx.lib.tpst_poly_get_q_partial_dev(self.ctx.h, self.h, ptr(point), r0, r1,
                                                                     C.c_void_p(out.data_ptr())),
                            "get_q_partial_dev")
+            self.ctx.lib_to_torch()
             return
         import torch
         out.copy_(torch.from_numpy(self.get_q_partial(point, r0, r1).reshape(-1).view(np.int64)))
@@ -291,6 +306,7 @@ class Polynomial:
         if not zq.is_cuda:
             zq = zq.to(torch.device("cuda", ctx.device))
         zq = zq.contiguous()
+        ctx.torch_to_lib()  # zq was produced on torch's stream
         Up = ptr(_u64(U, (12,))) if U is not None else None
         h = C.c_void_p()
         ctx.check(ctx.lib.tpst_poly_from_q_dev(ctx.h, n, ptr(point), C.c_void_p(zq.data_ptr()), Up, C.byref(h)),
@@ -349,6 +365,7 @@ def gt_final_exp_product_gathered(ctx: Context, gathered, R: int) -> np.ndarray:
     if not gathered.is_cuda:
         gathered = gathered.to(torch.device("cuda", ctx.device))
     gathered = gathered.contiguous()
+    ctx.torch_to_lib()  # the all-gather / copy wrote it on torch's stream
     k, w = gathered.shape
     T = np.zeros(72, dtype=np.uint64)
     ctx.check(ctx.lib.tpst_gt_final_exp_product_dev(ctx.h, C.c_void_p(gathered.data_ptr() + 96 * R), 8 * w, k,
@@ -365,8 +382,10 @@ def fr_sum(ctx: Context, gathered):
     gathered = gathered.contiguous()
     k, w = gathered.shape
     out = torch.empty(w, dtype=torch.int64, device=gathered.device)
+    ctx.torch_to_lib()  # gathered (all-gather / stack / contiguous) and out's previous users
     ctx.check(ctx.lib.tpst_fr_sum_dev(ctx.h, C.c_void_p(gathered.data_ptr()), k, w // 4, C.c_void_p(out.data_ptr())),
               "fr_sum_dev")
+    ctx.lib_to_torch()
     return out
 
 
@@ -406,3 +425,30 @@ def verify(ctx: Context, transcript: PoseidonTranscript, U, point, v, pst_proof,
         return False
     ctx.check(rc, "verify")
     return True
+
+
+def g1_msm_partial_into(ctx: Context, d_bases: int, d_scalars: int, i0: int, i1: int, out) -> None:
+    """Points [i0, i1) of a device-resident MSM (Montgomery bases, canonical Fr
+    scalars) summed into the int64 tensor ``out`` (24 words, raw XYZZ; a host
+    tensor -- the gloo path -- is filled through a device staging tensor)."""
+    import torch
+    dst = out if out.is_cuda else torch.empty(24, dtype=torch.int64, device=torch.device("cuda", ctx.device))
+    ctx.torch_to_lib()
+    ctx.g1_msm_xyzz_dev(d_bases + 96 * i0, d_scalars + 32 * i0, i1 - i0, dst.data_ptr())
+    ctx.lib_to_torch()
+    if dst is not out:
+        out.copy_(dst.cpu())
+
+
+def g1_xyzz_combine(ctx: Context, gathered):
+    """Sum of a gathered (k, 24) int64 tensor of XYZZ shares on the device ->
+    (12,) canonical affine G1 as an int64 tensor."""
+    import torch
+    if not gathered.is_cuda:
+        gathered = gathered.to(torch.device("cuda", ctx.device))
+    gathered = gathered.contiguous()
+    out = torch.empty(12, dtype=torch.int64, device=gathered.device)
+    ctx.torch_to_lib()
+    ctx.g1_xyzz_sum_dev(gathered.data_ptr(), gathered.shape[0], 8 * gathered.shape[1], out.data_ptr())
+    ctx.lib_to_torch()
+    return out
