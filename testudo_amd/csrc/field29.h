@@ -221,8 +221,46 @@ TPST_HD Fq29 from_std(const Fq& a) {
   return r;  // (a + k p) / 2^7 < p
 }
 
-// x 2^377 (radix 2^29, < p) -> field.h Montgomery x 2^384
+// x 2^377 (radix 2^29, < p) -> field.h Montgomery x 2^384 = Y 2^7 mod p
+// without a product: W = Y 2^7 < 128 p < 2^384 in 32-bit words, q from a
+// floating-point estimate of W / p biased low (q or q - 1), W - q p < 2p,
+// one conditional subtraction
 TPST_HD Fq to_std(const Fq29& a) {
+  uint32_t w[12];
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    // bits [32 i - 7, 32 i + 25) of the 29-bit limbs
+    const int s = 32 * i - 7;
+    uint64_t v = 0;
+#pragma unroll
+    for (int j = 0; j < r29::N; j++) {
+      const int sh = 29 * j - s;  // position of limb j relative to bit s
+      if (sh > -29 && sh < 32) v |= sh >= 0 ? ((uint64_t)a.v[j] << sh) : ((uint64_t)a.v[j] >> (-sh));
+    }
+    w[i] = (uint32_t)v;
+  }
+  const double top = (double)w[11] * 4294967296.0 + (double)w[10];
+  const double pt = (double)params::FQ_P[11] * 4294967296.0 + (double)params::FQ_P[10];
+  const double qd = top / pt - 1e-6;
+  const uint32_t q = qd > 0.0 ? (uint32_t)qd : 0u;
+  Fq r;
+  uint64_t c = 0;
+  int64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    const uint64_t t = (uint64_t)q * params::FQ_P[i] + c;
+    c = t >> 32;
+    const int64_t d = (int64_t)w[i] - (int64_t)(uint32_t)t + br;
+    r.v[i] = (uint32_t)d;
+    br = d >> 32;
+  }
+  reduce_once(r);
+  return r;
+}
+
+// the same conversion as one Montgomery product by 2^384 mod p (reference
+// form of to_std, kept for the host tests)
+TPST_HD Fq to_std_mul(const Fq29& a) {
   Fq29 c;
 #pragma unroll
   for (int i = 0; i < r29::N; i++) c.v[i] = r29::TO_STD[i];

@@ -533,6 +533,7 @@ template <class F>
 struct AccField {
   using T = F;
   static __device__ __forceinline__ Affine<T> in(const Affine<F>& a) { return a; }
+  static __device__ __forceinline__ Xyzz<T> in(const Xyzz<F>& a) { return a; }
   static __device__ __forceinline__ Xyzz<F> out(const Xyzz<T>& a) { return a; }
 };
 #ifndef TPST_ACC29
@@ -543,16 +544,41 @@ template <>
 struct AccField<Fq> {
   using T = Fq29;
   static __device__ __forceinline__ Affine<T> in(const Affine<Fq>& a) { return {from_std(a.x), from_std(a.y)}; }
+  static __device__ __forceinline__ Xyzz<T> in(const Xyzz<Fq>& a) {
+    return {from_std(a.X), from_std(a.Y), from_std(a.ZZ), from_std(a.ZZZ)};
+  }
   static __device__ __forceinline__ Xyzz<Fq> out(const Xyzz<T>& a) {
     return {to_std(a.X), to_std(a.Y), to_std(a.ZZ), to_std(a.ZZZ)};
   }
 };
 #endif
 
+template <>
+struct Words<Fq29> {
+  static constexpr int n = 13;
+};
+// bucket / piece / segment values live in memory in field.h's layout; the
+// tail kernels (fixups, weighted reductions, window chains) compute in the
+// accumulation field too: 45 % lower lone-lane product latency (0.91 vs
+// 1.65 us, tools/mb_fq29.py) on their serial chains
+template <class F>
+__device__ __forceinline__ Xyzz<typename AccField<F>::T> load_acc(const Xyzz<F>* p, size_t i) {
+  return AccField<F>::in(load_xyzz(p, i));
+}
+template <class F>
+__device__ __forceinline__ void store_acc(Xyzz<F>* p, size_t i, const Xyzz<typename AccField<F>::T>& v) {
+  store_xyzz(p, i, AccField<F>::out(v));
+}
+
+// TPST_GATHER_MASK=<bits> (timing experiments only, wrong sums): every
+// gathered point index is masked to its low bits, so the same random access
+// pattern hits a cache-resident slice of the bases / table
+static __device__ uint32_t g_gather_mask = 0x7fffffffu;
+
 template <class F>
 __device__ __forceinline__ Affine<F> fetch_point(const uint32_t* bases, const uint32_t* phib, uint32_t nbase,
                                                 uint32_t v) {
-  const uint32_t idx = v & 0x7fffffffu;
+  const uint32_t idx = v & g_gather_mask;
   Affine<F> p = (idx < nbase) ? load_affine<F>(bases, idx) : load_affine<F>(phib, idx - nbase);
   if (v >> 31) p.y = neg(p.y);
   return p;
@@ -569,8 +595,8 @@ __device__ __forceinline__ Affine<F> fetch_point(const uint32_t* bases, const ui
 // (its owner's partial goes to bpart[workgroup]), so the fixup runs one thread
 // per workgroup instead of one per bucket.  The next point is loaded before
 // the current mixed add runs (software prefetch).
-template <class F>
-__global__ void __launch_bounds__(ACC_BLOCK, (sizeof(F) > 48 ? 1 : 2))
+template <class F, int MINW = (sizeof(F) > 48 ? 1 : 2)>
+__global__ void __launch_bounds__(ACC_BLOCK, MINW)
     k_bucket_acc_chunk(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals, size_t m_all,
                        const uint32_t* __restrict__ mend, uint32_t sent, const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend,
                        const uint32_t* __restrict__ bases, const uint32_t* __restrict__ phib, uint32_t nbase,
@@ -639,6 +665,7 @@ __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
                    const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend, int lg, size_t nblk,
                    const Xyzz<F>* __restrict__ part, const Xyzz<F>* __restrict__ bpart,
                    Xyzz<F>* __restrict__ buckets) {
+  using C = typename AccField<F>::T;
   const size_t B = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (B + 1 >= nblk) return;
   const int lb = lg + ACC_BLOCK_LG;
@@ -647,9 +674,9 @@ __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
   const uint32_t key = keys[e];
   if (key >= sent || keys[e - 1] != key || ((size_t)bstart[key] >> lb) != B) return;
   const size_t t1 = ((size_t)bend[key] - 1) >> lg;
-  Xyzz<F> acc = load_xyzz(bpart, B);
-  for (size_t u = (B + 1) << ACC_BLOCK_LG; u <= t1; u++) acc = add(acc, load_xyzz(part, u));
-  store_xyzz(buckets, key, acc);
+  Xyzz<C> acc = load_acc(bpart, B);
+  for (size_t u = (B + 1) << ACC_BLOCK_LG; u <= t1; u++) acc = add(acc, load_acc(part, u));
+  store_acc(buckets, key, acc);
 }
 
 // Short-chunk accumulation for the variable-base MSM (32-entry chunks over
@@ -661,8 +688,8 @@ __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
 // (range[w] = first sorted entry of window w, device-side): chunk indices stay
 // global (t = entry >> lg) so a chunk straddling two window groups is split
 // between their launches without sharing a part[] slot.
-template <class F>
-__global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
+template <class F, int MINW = (sizeof(F) > 48 ? 1 : 2)>
+__global__ void __launch_bounds__(64, MINW)
     k_bucket_acc_short(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
                        const uint32_t* __restrict__ range, int wlo, int whi, uint32_t sent,
                        const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend,
@@ -780,21 +807,22 @@ __global__ void __launch_bounds__(LONG_THREADS) k_bucket_fixup_long(const uint32
                                                                     const uint32_t* __restrict__ bend, int lg,
                                                                     const Xyzz<F>* __restrict__ part,
                                                                     Xyzz<F>* __restrict__ buckets, LongList ll) {
-  __shared__ Xyzz<F> sh[LONG_THREADS];
+  using C = typename AccField<F>::T;
+  __shared__ Xyzz<C> sh[LONG_THREADS];
   const uint32_t n = *ll.cnt < ll.cap ? *ll.cnt : ll.cap;
   const uint32_t tid = threadIdx.x;
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
     const uint32_t b = ll.list[i];
     const size_t t0 = (size_t)bstart[b] >> lg, t1 = (size_t)(bend[b] - 1) >> lg;
-    Xyzz<F> acc = tid == 0 ? load_xyzz(part, 2 * t0 + 1) : Xyzz<F>::inf();
-    for (size_t t = t0 + 1 + tid; t <= t1; t += LONG_THREADS) acc = add(acc, load_xyzz(part, 2 * t));
+    Xyzz<C> acc = tid == 0 ? load_acc(part, 2 * t0 + 1) : Xyzz<C>::inf();
+    for (size_t t = t0 + 1 + tid; t <= t1; t += LONG_THREADS) acc = add(acc, load_acc(part, 2 * t));
     sh[tid] = acc;
     __syncthreads();
     for (uint32_t h = LONG_THREADS / 2; h > 0; h >>= 1) {
       if (tid < h) sh[tid] = add(sh[tid], sh[tid + h]);
       __syncthreads();
     }
-    if (tid == 0) store_xyzz(buckets, b, sh[0]);
+    if (tid == 0) store_acc(buckets, b, sh[0]);
     __syncthreads();
   }
 }
@@ -828,6 +856,7 @@ __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
     k_bucket_fixup_short(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend, size_t b0,
                          size_t b1, int lg, const Xyzz<F>* __restrict__ part, Xyzz<F>* __restrict__ buckets,
                          int prio, LongList ll) {
+  using C = typename AccField<F>::T;
   set_wave_prio(prio);
   const size_t b = b0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= b1) return;
@@ -839,9 +868,9 @@ __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
     ll.push((uint32_t)b);
     return;
   }
-  Xyzz<F> acc = load_xyzz(part, 2 * t0 + 1);
-  for (size_t t = t0 + 1; t <= t1; t++) acc = add(acc, load_xyzz(part, 2 * t));
-  store_xyzz(buckets, b, acc);
+  Xyzz<C> acc = load_acc(part, 2 * t0 + 1);
+  for (size_t t = t0 + 1; t <= t1; t++) acc = add(acc, load_acc(part, 2 * t));
+  store_acc(buckets, b, acc);
 }
 
 // the same fixup, one quad of lanes per bucket (coop.h: 4 product latencies
@@ -852,6 +881,7 @@ __global__ void __launch_bounds__(64) k_bucket_fixup_quad(const uint32_t* __rest
                                                           const uint32_t* __restrict__ bend, size_t b0, size_t b1,
                                                           int lg, const Xyzz<F>* __restrict__ part,
                                                           Xyzz<F>* __restrict__ buckets, LongList ll) {
+  using C = typename AccField<F>::T;
   const size_t b = b0 + (((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2);
   const int qi = threadIdx.x & 3;
   if (b >= b1) return;  // quad-uniform
@@ -863,9 +893,9 @@ __global__ void __launch_bounds__(64) k_bucket_fixup_quad(const uint32_t* __rest
     if (qi == 0) ll.push((uint32_t)b);
     return;
   }
-  Xyzz<F> acc = load_xyzz(part, 2 * t0 + 1);
-  for (size_t t = t0 + 1; t <= t1; t++) acc = add_quad(acc, load_xyzz(part, 2 * t), qi);
-  if (qi == 0) store_xyzz(buckets, b, acc);
+  Xyzz<C> acc = load_acc(part, 2 * t0 + 1);
+  for (size_t t = t0 + 1; t <= t1; t++) acc = add_quad(acc, load_acc(part, 2 * t), qi);
+  if (qi == 0) store_acc(buckets, b, acc);
 }
 
 // segment t of group g: sum_{b in seg} (b+1) * S_b with b the bucket index
@@ -875,6 +905,7 @@ __global__ void __launch_bounds__(64) k_bucket_fixup_quad(const uint32_t* __rest
 template <class F>
 __global__ void __launch_bounds__(64) k_seg_reduce_quad(const Xyzz<F>* __restrict__ buckets, uint32_t nb, uint32_t L,
                                                         size_t nseg, Xyzz<F>* __restrict__ seg_out, int prio = 0) {
+  using C = typename AccField<F>::T;
   set_wave_prio(prio);
   const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
   const int qi = threadIdx.x & 3;
@@ -883,14 +914,14 @@ __global__ void __launch_bounds__(64) k_seg_reduce_quad(const Xyzz<F>* __restric
   const size_t g = t / S;
   const uint32_t k = (uint32_t)(t % S);
   const size_t base = g * nb + (size_t)k * L;
-  Xyzz<F> acc = Xyzz<F>::inf(), sum = Xyzz<F>::inf();
+  Xyzz<C> acc = Xyzz<C>::inf(), sum = Xyzz<C>::inf();
   for (int b = (int)L - 1; b >= 0; b--) {
-    acc = add_quad(acc, load_xyzz(buckets, base + b), qi);
+    acc = add_quad(acc, load_acc(buckets, base + b), qi);
     sum = add_quad(sum, acc, qi);
   }
   const uint32_t s0 = k * L;
   if (s0 != 0 && !is_inf(acc)) sum = add_quad(sum, scalar_mul_quad(acc, s0, 32 - __builtin_clz(s0), qi), qi);
-  if (qi == 0) store_xyzz(seg_out, t, sum);
+  if (qi == 0) store_acc(seg_out, t, sum);
 }
 
 // the same segment sums, one lane per segment: for reductions with enough
@@ -900,43 +931,45 @@ __global__ void __launch_bounds__(64) k_seg_reduce_quad(const Xyzz<F>* __restric
 template <class F>
 __global__ void __launch_bounds__(64) k_seg_reduce_lane(const Xyzz<F>* __restrict__ buckets, uint32_t nb, uint32_t L,
                                                         size_t nseg, Xyzz<F>* __restrict__ seg_out) {
+  using C = typename AccField<F>::T;
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nseg) return;
   const uint32_t S = nb / L;
   const size_t g = t / S;
   const uint32_t k = (uint32_t)(t % S);
   const size_t base = g * nb + (size_t)k * L;
-  Xyzz<F> acc = Xyzz<F>::inf(), sum = Xyzz<F>::inf();
+  Xyzz<C> acc = Xyzz<C>::inf(), sum = Xyzz<C>::inf();
   for (int b = (int)L - 1; b >= 0; b--) {
-    acc = add(acc, load_xyzz(buckets, base + b));
+    acc = add(acc, load_acc(buckets, base + b));
     sum = add(sum, acc);
   }
   const uint32_t s0 = k * L;
   if (s0 != 0 && !is_inf(acc)) sum = add(sum, scalar_mul_xyzz(acc, &s0, 32 - __builtin_clz(s0)));
-  store_xyzz(seg_out, t, sum);
+  store_acc(seg_out, t, sum);
 }
 
 // one workgroup of BS / 4 quads per group: sum its S partial points
 template <class F, int BS>
 __global__ void __launch_bounds__(BS) k_group_reduce_quad(const Xyzz<F>* __restrict__ seg, uint32_t S,
                                                           Xyzz<F>* __restrict__ out, int prio = 0) {
+  using C = typename AccField<F>::T;
   set_wave_prio(prio);
   constexpr int Q = BS / 4;
-  __shared__ Xyzz<F> sh[Q];
+  __shared__ Xyzz<C> sh[Q];
   const size_t g = blockIdx.x;
   const int quad = threadIdx.x >> 2, qi = threadIdx.x & 3;
-  Xyzz<F> acc = Xyzz<F>::inf();
-  for (uint32_t k = quad; k < S; k += Q) acc = add_quad(acc, load_xyzz(seg, g * S + k), qi);
+  Xyzz<C> acc = Xyzz<C>::inf();
+  for (uint32_t k = quad; k < S; k += Q) acc = add_quad(acc, load_acc(seg, g * S + k), qi);
   if (qi == 0) sh[quad] = acc;
   __syncthreads();
   for (int h = Q / 2; h > 0; h >>= 1) {
     if (quad < h) {  // a quad reads its two operands before its lane 0 writes (one wave, in order)
-      const Xyzz<F> v = add_quad(sh[quad], sh[quad + h], qi);
+      const Xyzz<C> v = add_quad(sh[quad], sh[quad + h], qi);
       if (qi == 0) sh[quad] = v;
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) store_xyzz(out, g, sh[0]);
+  if (threadIdx.x == 0) store_acc(out, g, sh[0]);
 }
 
 // Contribution of the window group [wlo, whi) on one wave:
@@ -948,17 +981,18 @@ template <class F>
 static __global__ void __launch_bounds__(64, 1) k_window_chain(const Xyzz<F>* __restrict__ win, int wlo, int whi,
                                                               int c, const Xyzz<F>* __restrict__ extra, int nextra,
                                                               Xyzz<F>* __restrict__ out) {
+  using C = typename AccField<F>::T;
   if (blockIdx.x != 0) return;
   __builtin_amdgcn_s_setprio(3);  // a lone latency chain beside accumulation waves
   const int qi = threadIdx.x & 3;
-  Xyzz<F> acc = load_xyzz(win, whi - 1);
+  Xyzz<C> acc = load_acc(win, whi - 1);
   for (int w = whi - 2; w >= wlo; w--) {
     for (int i = 0; i < c; i++) acc = dbl_quad(acc, qi);
-    acc = add_quad(acc, load_xyzz(win, w), qi);
+    acc = add_quad(acc, load_acc(win, w), qi);
   }
   for (int i = 0; i < c * wlo; i++) acc = dbl_quad(acc, qi);
-  for (int k = 0; k < nextra; k++) acc = add_quad(acc, load_xyzz(extra, k), qi);
-  if (threadIdx.x == 0) store_xyzz(out, 0, acc);
+  for (int k = 0; k < nextra; k++) acc = add_quad(acc, load_acc(extra, k), qi);
+  if (threadIdx.x == 0) store_acc(out, 0, acc);
 }
 
 template <class F>
@@ -1068,6 +1102,7 @@ template <class F>
 __global__ void __launch_bounds__(64) k_seg_run_quad(const Xyzz<F>* __restrict__ buckets, uint32_t nb, uint32_t L,
                                                      size_t nseg, Xyzz<F>* __restrict__ S_out,
                                                      Xyzz<F>* __restrict__ Tn, int prio = 0) {
+  using C = typename AccField<F>::T;
   set_wave_prio(prio);
   const size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
   const int qi = threadIdx.x & 3;
@@ -1076,14 +1111,14 @@ __global__ void __launch_bounds__(64) k_seg_run_quad(const Xyzz<F>* __restrict__
   const size_t g = t / S;
   const uint32_t k = (uint32_t)(t % S);
   const size_t base = g * nb + (size_t)k * L;
-  Xyzz<F> acc = Xyzz<F>::inf(), sum = Xyzz<F>::inf();
+  Xyzz<C> acc = Xyzz<C>::inf(), sum = Xyzz<C>::inf();
   for (int b = (int)L - 1; b >= 0; b--) {
-    acc = add_quad(acc, load_xyzz(buckets, base + b), qi);
+    acc = add_quad(acc, load_acc(buckets, base + b), qi);
     sum = add_quad(sum, acc, qi);
   }
   if (qi == 0) {
-    store_xyzz(S_out, t, sum);
-    store_xyzz(Tn, g * S + (k ? k - 1 : S - 1), k ? acc : Xyzz<F>::inf());
+    store_acc(S_out, t, sum);
+    store_acc(Tn, g * S + (k ? k - 1 : S - 1), k ? acc : Xyzz<C>::inf());
   }
 }
 
@@ -1092,14 +1127,15 @@ template <class F>
 __global__ void __launch_bounds__(64) k_lift_add_quad(const Xyzz<F>* __restrict__ a, const Xyzz<F>* __restrict__ b,
                                                       int lg, size_t groups, Xyzz<F>* __restrict__ out,
                                                       int prio = 0) {
+  using C = typename AccField<F>::T;
   set_wave_prio(prio);
   const size_t g = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
   const int qi = threadIdx.x & 3;
   if (g >= groups) return;
-  Xyzz<F> r = load_xyzz(b, g);
+  Xyzz<C> r = load_acc(b, g);
   for (int i = 0; i < lg; i++) r = dbl_quad(r, qi);
-  r = add_quad(r, load_xyzz(a, g), qi);
-  if (qi == 0) store_xyzz(out, g, r);
+  r = add_quad(r, load_acc(a, g), qi);
+  if (qi == 0) store_acc(out, g, r);
 }
 
 // sum of S points per group (tree passes of k_group_reduce_quad)
@@ -1235,9 +1271,20 @@ static int g2_window_bits(int c) {
   return (env >= 4 && env <= 16) ? env : c;
 }
 
+static hipError_t gather_mask_init() {
+  static const hipError_t e = [] {
+    const char* v = getenv("TPST_GATHER_MASK");
+    if (!v) return hipSuccess;
+    const uint32_t mask = (1u << atoi(v)) - 1u;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_gather_mask), &mask, 4);
+  }();
+  return e;
+}
+
 template <class F>
 hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint32_t* d_scalars, size_t n,
                    Xyzz<F>* d_out) {
+  TPST_TRY(gather_mask_init());
   if (n == 0) {
     Xyzz<F> inf = Xyzz<F>::inf();
     return hipMemcpyAsync(d_out, &inf, sizeof(inf), hipMemcpyHostToDevice, s);
@@ -1385,9 +1432,21 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
                                                                           bstart, bend, d_bases, phib, (uint32_t)n,
                                                                           lg, buckets, part);
     } else {
-      k_bucket_acc_short<F><<<grid_for(gchunks, 64), 64, 0, bulk>>>(keys, vals, range, wlo, whi, sent, bstart,
-                                                                     bend, d_bases, phib, (uint32_t)n, lg, buckets,
-                                                                     part);
+      // waves per SIMD the register budget must allow (TPST_ACC_MINW, sweeps)
+      static const int minw = [] {
+        const char* e = getenv("TPST_ACC_MINW");
+        return e ? atoi(e) : 2;  // 3 and 4 spill (32 / 111 VGPRs) and measured slower
+      }();
+      const unsigned grid = grid_for(gchunks, 64);
+      if (minw >= 4)
+        k_bucket_acc_short<F, 4><<<grid, 64, 0, bulk>>>(keys, vals, range, wlo, whi, sent, bstart, bend, d_bases,
+                                                         phib, (uint32_t)n, lg, buckets, part);
+      else if (minw == 3)
+        k_bucket_acc_short<F, 3><<<grid, 64, 0, bulk>>>(keys, vals, range, wlo, whi, sent, bstart, bend, d_bases,
+                                                         phib, (uint32_t)n, lg, buckets, part);
+      else
+        k_bucket_acc_short<F><<<grid, 64, 0, bulk>>>(keys, vals, range, wlo, whi, sent, bstart, bend, d_bases, phib,
+                                                      (uint32_t)n, lg, buckets, part);
     }
     TPST_TRY(hipGetLastError());
     if (g == 0) pf->end(ST_BUCKET_ACC, bulk);
@@ -1796,6 +1855,7 @@ __global__ void __launch_bounds__(SB_THREADS) k_batch_sort_staged(const uint32_t
 hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint32_t* d_scalars, size_t rows,
                      size_t row_stride, size_t col_stride, Xyzz<Fq>* d_out) {
   if (rows == 0) return hipSuccess;
+  TPST_TRY(gather_mask_init());
   const int c = t.c, W = t.W;
   const size_t N = t.N;
   const uint32_t nb = 1u << (c - 1);
@@ -1832,9 +1892,18 @@ hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint3
   TPST_TRY(hipGetLastError());
   pf->end(ST_BATCH_SORT, s);
   pf->begin(ST_BUCKET_ACC, s);
-  k_bucket_acc_chunk<Fq><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys, entries, m, nullptr, (uint32_t)nbk, bstart,
-                                                               bend, t.d_table, nullptr, 0x7fffffffu, lg, buckets,
-                                                               part, bpart);
+  static const int minw = [] {  // TPST_K1_MINW: waves per SIMD the register budget allows (sweeps)
+    const char* e = getenv("TPST_K1_MINW");
+    return e ? atoi(e) : 2;
+  }();
+  if (minw >= 3)
+    k_bucket_acc_chunk<Fq, 3><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys, entries, m, nullptr, (uint32_t)nbk, bstart,
+                                                                    bend, t.d_table, nullptr, 0x7fffffffu, lg,
+                                                                    buckets, part, bpart);
+  else
+    k_bucket_acc_chunk<Fq><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys, entries, m, nullptr, (uint32_t)nbk, bstart,
+                                                                 bend, t.d_table, nullptr, 0x7fffffffu, lg, buckets,
+                                                                 part, bpart);
   TPST_TRY(hipGetLastError());
   k_bucket_fixup<Fq><<<grid_for(nblk, 64), 64, 0, s>>>(keys, m, nullptr, (uint32_t)nbk, bstart, bend, lg, nblk,
                                                        part, bpart, buckets);
