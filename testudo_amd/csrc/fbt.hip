@@ -1,4 +1,5 @@
 // Fixed-base lookup tables + grouped fixed-base MSM (see fbt.h).
+#include "acc_field.h"
 #include "coop.h"
 #include "fbt.h"
 #include "glv.h"
@@ -36,12 +37,13 @@ __global__ void __launch_bounds__(64) k_fbt_pow(const uint32_t* __restrict__ bas
 template <class F>
 __global__ void __launch_bounds__(64) k_fbt_pow_quad(const uint32_t* __restrict__ bases, size_t n, int nw,
                                                      Xyzz<F>* __restrict__ tmp) {
+  using A = AccField<F>;
   const size_t k = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
   const int qi = threadIdx.x & 3;
   if (k >= n) return;  // quad-uniform
-  Xyzz<F> p = to_xyzz(load_affine<F>(bases, k));
+  Xyzz<typename A::T> p = to_xyzz(A::in(load_affine<F>(bases, k)));
   for (int w = 0; w < nw; w++) {
-    if (qi == 0) store_xyzz(tmp, k * nw + w, p);
+    if (qi == 0) store_acc(tmp, k * nw + w, p);
     if (w + 1 < nw) {
       p = dbl_quad(p, qi);
       p = dbl_quad(p, qi);
@@ -158,7 +160,9 @@ __global__ void __launch_bounds__(64) k_fbt_partial_quad(const uint32_t* __restr
   } else {
     k = (m / gr.D) * gr.L + g * gr.D + m % gr.D;
   }
-  Xyzz<F> acc = Xyzz<F>::inf();
+  using A = AccField<F>;
+  using C = typename A::T;
+  Xyzz<C> acc = Xyzz<C>::inf();
   if (valid) {
     uint32_t s[8];
     const uint4* sp = reinterpret_cast<const uint4*>(scal + 8 * (k + q * gr.set_stride));
@@ -189,16 +193,17 @@ __global__ void __launch_bounds__(64) k_fbt_partial_quad(const uint32_t* __restr
       const int w = wb + j;
       const int d = fbt_digit(s, w, carry);
       if (d) {
-        Affine<F> t = load_affine<F>(table, (k * nw + w) * FBT_M + (d < 0 ? -d : d) - 1);
+        Affine<F> ts = load_affine<F>(table, (k * nw + w) * FBT_M + (d < 0 ? -d : d) - 1);
         if constexpr (sizeof(F) == sizeof(Fq)) {
-          if (phi) t.x = mul(t.x, Fq::from_limbs(params::G1_BETA));
+          if (phi) ts.x = mul(ts.x, Fq::from_limbs(params::G1_BETA));
         }
+        Affine<C> t = A::in(ts);
         if (d < 0) t = neg(t);
         acc = add_affine_quad(acc, t, qi);
       }
     }
   }
-  if (qi == 0) store_xyzz(partial, i, acc);
+  if (qi == 0) store_acc(partial, i, acc);
 }
 
 // out[seg * parts + part] = sum of in[seg * seg_len + part * per .. + per),
@@ -206,23 +211,24 @@ __global__ void __launch_bounds__(64) k_fbt_partial_quad(const uint32_t* __restr
 template <class F, int BS>
 __global__ void __launch_bounds__(BS) k_seg_sum_quad(const Xyzz<F>* __restrict__ in, size_t seg_len, size_t per,
                                                      size_t parts, Xyzz<F>* __restrict__ out) {
+  using C = typename AccField<F>::T;
   constexpr int Q = BS / 4;
-  __shared__ Xyzz<F> sh[Q];
+  __shared__ Xyzz<C> sh[Q];
   const int quad = threadIdx.x >> 2, qi = threadIdx.x & 3;
   const size_t seg = blockIdx.x / parts, part = blockIdx.x % parts;
   const size_t lo = part * per, hi = lo + per < seg_len ? lo + per : seg_len;
-  Xyzz<F> acc = Xyzz<F>::inf();
-  for (size_t j = lo + quad; j < hi; j += Q) acc = add_quad(acc, load_xyzz(in, seg * seg_len + j), qi);
+  Xyzz<C> acc = Xyzz<C>::inf();
+  for (size_t j = lo + quad; j < hi; j += Q) acc = add_quad(acc, load_acc(in, seg * seg_len + j), qi);
   if (qi == 0) sh[quad] = acc;
   __syncthreads();
   for (int h = Q / 2; h > 0; h >>= 1) {
     if (quad < h) {
-      const Xyzz<F> v = add_quad(sh[quad], sh[quad + h], qi);
+      const Xyzz<C> v = add_quad(sh[quad], sh[quad + h], qi);
       if (qi == 0) sh[quad] = v;
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) store_xyzz(out, blockIdx.x, sh[0]);
+  if (threadIdx.x == 0) store_acc(out, blockIdx.x, sh[0]);
 }
 
 template <class F>

@@ -547,6 +547,21 @@ TPST_NI Fp<C> inv(const Fp<C>& y) {
   return limbs_is_one<C>(b) ? r : Fp<C>::zero();
 }
 
+// Fq's inverse: the radix-2^29 binary GCD of field29.h, ~3x fewer
+// instructions than the 32-bit-limb template above, which Fr keeps.
+// field29.h needs only the base field above and is included here; the
+// declaration covers a translation unit that includes field29.h first.
+#pragma GCC diagnostic push
+#pragma GCC diagnostic ignored "-Wattributes"
+TPST_NI Fq inv(const Fq& a);
+#pragma GCC diagnostic pop
+
+}  // namespace tpst
+
+#include "field29.h"
+
+namespace tpst {
+
 // small constant multiples
 template <class C>
 TPST_HD Fp<C> mul3(const Fp<C>& a) { return add(dbl(a), a); }
@@ -713,3 +728,4 @@ TPST_NI Fq12 frobenius(const Fq12& a, int k) {
 }
 
 }  // namespace tpst
+
