@@ -1,0 +1,44 @@
+// Host check of field29.h (radix-2^29 Fq, R = 2^377) against Python integers
+// (tests/test_field29.py): per input line "a b" (field.h Montgomery words,
+// 12 x u32 hex, possibly unreduced below 64 p) print
+//   mul, sqr, add, sub, to_std(from_std(a)), inv(a)        for reduced a, b
+//   the wave engine's stage product / square               for wide a, b
+#include <cstdio>
+#include <cstring>
+#include "field.h"
+
+using namespace tpst;
+
+static void put(const Fq& r) {
+  for (int i = 0; i < 12; i++) printf("%08x ", r.v[i]);
+  printf("\n");
+}
+
+int main() {
+  int n;
+  if (scanf("%d", &n) != 1) return 1;
+  for (int t = 0; t < n; t++) {
+    int wide;
+    Fq a, b;
+    if (scanf("%d", &wide) != 1) return 1;
+    for (int i = 0; i < 12; i++)
+      if (scanf("%x", &a.v[i]) != 1) return 1;
+    for (int i = 0; i < 12; i++)
+      if (scanf("%x", &b.v[i]) != 1) return 1;
+    const Fq29 x = from_std(a), y = from_std(b);
+    if (wide) {  // wave_tower.h stage_mul / stage_sqr
+      Fq29 m = mul(x, y);
+      reduce_once(m);
+      put(to_std(m));
+      put(to_std(sqr(x)));
+    } else {
+      put(to_std(mul(x, y)));
+      put(to_std(sqr(x)));
+      put(to_std(add(x, y)));
+      put(to_std(sub(x, y)));
+      put(to_std(x));
+      put(inv(a));
+    }
+  }
+  return 0;
+}

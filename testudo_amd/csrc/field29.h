@@ -200,18 +200,20 @@ TPST_HD Fq29 sqr(const Fq29& a) {
   return r;
 }
 
-// bits [s, s + 29) of a 12-word little-endian value (s + 29 <= 416)
+// bits [s, s + 29) of a 13-word little-endian value (s + 29 <= 416)
 TPST_HD uint32_t bits29(const uint32_t* w, int s) {
   const int q = s >> 5, o = s & 31;
-  const uint64_t lo = q < 12 ? w[q] : 0u;
-  const uint64_t hi = q + 1 < 12 ? w[q + 1] : 0u;
+  const uint64_t lo = q < 13 ? w[q] : 0u;
+  const uint64_t hi = q + 1 < 13 ? w[q + 1] : 0u;
   return (uint32_t)(((hi << 32) | lo) >> o) & r29::M;
 }
 
-// field.h Montgomery (x 2^384, 12 x u32, < p) -> x 2^377 in radix 2^29
+// field.h Montgomery (x 2^384, 12 x u32) -> x 2^377 in radix 2^29:
+// (a + k p) / 2^7 < p for a < p; for an unreduced a < 64 p (a wave-engine
+// form) the sum carries into a 13th word and the result is < 1.5 p < 2^377
 TPST_HD Fq29 from_std(const Fq& a) {
   const uint32_t k = (0u - a.v[0]) & 127u;  // (a + k p) = 0 mod 2^7
-  uint32_t w[12];
+  uint32_t w[13];
   uint64_t c = 0;
 #pragma unroll
   for (int i = 0; i < 12; i++) {
@@ -219,11 +221,14 @@ TPST_HD Fq29 from_std(const Fq& a) {
     w[i] = (uint32_t)c;
     c >>= 32;
   }
-  // a + k p < 128 p < 2^384: no carry out
+  w[12] = (uint32_t)c;
   Fq29 r;
 #pragma unroll
-  for (int j = 0; j < r29::N; j++) r.v[j] = bits29(w, 29 * j + 7);
-  return r;  // (a + k p) / 2^7 < p
+  for (int j = 0; j < r29::N - 1; j++) r.v[j] = bits29(w, 29 * j + 7);
+  // the top limb keeps every remaining bit: (a + k p) / 2^7 may reach 2^377
+  // for a wide operand (< 1.5 p); mul's columns stay below 2^63 with a 30-bit top limb
+  r.v[r29::N - 1] = (w[11] >> 3) | (w[12] << 29);  // bits 355.. (29 * 12 + 7)
+  return r;
 }
 
 // x 2^377 (radix 2^29, < p) -> field.h Montgomery x 2^384 = Y 2^7 mod p

@@ -307,7 +307,7 @@ __global__ void __launch_bounds__(64) k_mb_wave_prof(int op, int iters, unsigned
       }
     }
     unsigned long long t1 = clock64();
-    if (lane < np) pr = sq ? sqr(x) : mul(x, y);
+    if (lane < np) pr = sq ? wave::stage_sqr(x) : wave::stage_mul(x, y);
     unsigned long long t2 = clock64();
     if (lane < np) wave::put_slot(vals, base + lane, pr);
     wave::wave_sync();

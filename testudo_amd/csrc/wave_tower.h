@@ -153,6 +153,34 @@ __device__ __forceinline__ Fq reduce_wide(const uint32_t v[13]) {
   return r;
 }
 
+// The stage's Fq product runs in field29.h's radix 2^29 (0.91 vs 1.65 us
+// lone-wave latency): operands converted on the way in -- a form left
+// unreduced is < 64 p, so (x + k p) / 2^7 < 1.5 p stays in 13 x 29 bits --
+// and the product (reduced below p) back to
+// field.h's canonical form on the way out.  TPST_WAVE29=0 keeps field.h's
+// product (A/B).
+#ifndef TPST_WAVE29
+#define TPST_WAVE29 1
+#endif
+__device__ __forceinline__ Fq stage_mul(const Fq& x, const Fq& y) {
+#if TPST_WAVE29
+  // one operand up to 64 p (the other < p): the product is < 2.26 p before
+  // mul's conditional subtraction, so one more brings it below p for to_std
+  Fq29 r = mul(from_std(x), from_std(y));
+  reduce_once(r);
+  return to_std(r);
+#else
+  return mul(x, y);
+#endif
+}
+__device__ __forceinline__ Fq stage_sqr(const Fq& x) {
+#if TPST_WAVE29
+  return to_std(sqr(from_std(x)));
+#else
+  return sqr(x);
+#endif
+}
+
 // one stage: C/D = op(A, B).
 // block: [hdr0 = np | no << 8 | red << 16 | sq << 17 | nc << 24, hdr1 = TX | TY << 8 | TC << 16,
 //         X terms (TX x np, term-major), Y terms (TY x np), chunk terms (TC x nc),
@@ -185,7 +213,7 @@ __device__ __forceinline__ void run(const Eng& e, const lds_t* blk, int a, int b
       for (int i = 0; i < 12; i++) x.v[i] = xw[i];
     }
     if (sq) {
-      put_slot(e.lds, e.prod + lane, sqr(x));
+      put_slot(e.lds, e.prod + lane, stage_sqr(x));
     } else {
       uint32_t yw[13];
       form(e, Y + lane, np, ty, bases, yw);
@@ -196,7 +224,7 @@ __device__ __forceinline__ void run(const Eng& e, const lds_t* blk, int a, int b
 #pragma unroll
         for (int i = 0; i < 12; i++) y.v[i] = yw[i];
       }
-      put_slot(e.lds, e.prod + lane, mul(x, y));
+      put_slot(e.lds, e.prod + lane, stage_mul(x, y));
     }
   }
   wave_sync();
