@@ -51,7 +51,10 @@ METRIC = "PST commit+open sec, 2^20-var poly BLS12-377; G1 MSM Mscalar/s at 1/2/
 LOG_N = 20
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
 BYTES_PER_PAIR = 128           # 32 B scalar + 96 B affine base
-LIMB_PRODUCTS_PER_FQ_MUL = 276  # 12 x 12 a*b + 11 x 12 m*p limb products (v_mad_u64_u32 each, field.h mul)
+# the accumulation's Fq product (field29.h, 13 x 29-bit limbs): 13 x 13 a*b + 12 x 13 m*p limb
+# products, one v_mad_u64_u32 each (p_0 = 1 makes the m_k * p_0 terms adds)
+LIMB_PRODUCTS_PER_FQ_MUL = 325
+MB_FQMUL_KIND = 12  # tpst_microbench kind of that product (kind 0: field.h's 12 x 32-bit product)
 SEED = 0x7E57D0
 PMC_FILE = os.path.join(ROOT, "profiles", "r04", "pmc_bucket_acc_short.json")
 PMC_FILE_K1 = os.path.join(ROOT, "profiles", "r04", "pmc_bucket_acc_chunk_2p24.json")
@@ -297,15 +300,17 @@ def main():
             pmc = None
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     # compute roof, measured live on this GPU: the chip-wide issue rate of
-    # v_mad_u64_u32 (one limb product) prices an Fq product at its 276 limb
-    # products -- the multiply-issue roof; the Fq-product microbenchmark is the
-    # achieved-in-isolation rate; v_add_u32's rate is the VALU issue peak
+    # v_mad_u64_u32 (one limb product) prices the accumulation's Fq product
+    # at its 325 limb products -- the multiply-issue roof; the Fq-product
+    # microbenchmark (same product) is the achieved-in-isolation rate;
+    # v_add_u32's rate is the VALU issue peak
     rates = issue_rates(ctx)
     mad_roof_fqmul = rates["v_mad_u64_u32"] * 64 / LIMB_PRODUCTS_PER_FQ_MUL
     mb_threads = 256 * 16 * 64
     mb_iters = 200
-    ctx.microbench(0, mb_threads, 10)  # warm: first launch loads the code object
-    mb_fqmul = mb_threads * mb_iters / (min(ctx.microbench(0, mb_threads, mb_iters) for _ in range(3)) * 1e-3)
+    ctx.microbench(MB_FQMUL_KIND, mb_threads, 10)  # warm: first launch loads the code object
+    mb_fqmul = mb_threads * mb_iters / (min(ctx.microbench(MB_FQMUL_KIND, mb_threads, mb_iters)
+                                            for _ in range(3)) * 1e-3)
     c_bits = 16
     windows = 8  # GLV: two 127-bit halves, 8 signed 16-bit windows each
     madds = 2 * n * windows

@@ -685,6 +685,90 @@ __global__ void __launch_bounds__(64, MINW)
   }
 }
 
+// k_bucket_acc_short<Fq> with the next point staged through LDS instead of
+// registers: the wave issues six global_load_lds_dwordx4 for the 64 lanes'
+// next points (lane i's 16-byte piece j lands at stage[buf][j][i]; no VGPR
+// destination), runs the current mixed add meanwhile, and reads the staged
+// point back with six ds_read_b128.  Frees the prefetched point's VGPRs
+// (occupancy) and moves the gathers off the register file.  TPST_ACC_LDS=1.
+template <int MINW>
+__global__ void __launch_bounds__(64, MINW)
+    k_bucket_acc_short_lds(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                           const uint32_t* __restrict__ range, int wlo, int whi, uint32_t sent,
+                           const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend,
+                           const uint32_t* __restrict__ bases, const uint32_t* __restrict__ phib, uint32_t nbase,
+                           int lg, Xyzz<Fq>* __restrict__ buckets, Xyzz<Fq>* __restrict__ part) {
+  __shared__ uint4 stage[2][6][64];  // 12 KB: double-buffered 96-byte points, piece-major
+  using A = AccField<Fq>;
+  using C = typename A::T;
+  const int lane = threadIdx.x;
+  const size_t e_lo = range[wlo], e_hi = range[whi];
+  const size_t t = (e_lo >> lg) + (size_t)blockIdx.x * blockDim.x + lane;
+  size_t c0 = t << lg;
+  if ((e_lo >> lg) + (size_t)blockIdx.x * blockDim.x >= e_hi) return;  // wave-uniform: no lane has work
+  const bool active = c0 < e_hi;
+  const size_t c1 = active ? ((c0 + ((size_t)1 << lg) < e_hi) ? c0 + ((size_t)1 << lg) : e_hi) : c0;
+  if (c0 < e_lo) c0 = e_lo;
+  // every lane issues every staging load (the instruction is wave-wide);
+  // lanes without a point load bases[0]
+  auto stage_load = [&](int buf, uint32_t v, bool want) {
+    const uint32_t idx = v & g_gather_mask;
+    const uint32_t* src = want ? ((idx < nbase) ? bases + 24 * (size_t)idx : phib + 24 * (size_t)(idx - nbase)) : bases;
+#pragma unroll
+    for (int j = 0; j < 6; j++)
+      __builtin_amdgcn_global_load_lds((const void*)(src + 4 * j),
+                                       (__attribute__((address_space(3))) void*)&stage[buf][j][0], 16, 0, 0);
+  };
+  auto stage_read = [&](int buf, uint32_t v) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t w[24];
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+      const uint4 q = stage[buf][j][lane];
+      w[4 * j] = q.x;
+      w[4 * j + 1] = q.y;
+      w[4 * j + 2] = q.z;
+      w[4 * j + 3] = q.w;
+    }
+    Affine<Fq> p = {Fq::from_limbs(w), Fq::from_limbs(w + 12)};
+    if (v >> 31) p.y = neg(p.y);
+    return A::in(p);
+  };
+  uint32_t key = active ? keys[c0] : sent;
+  uint32_t val = active && key < sent ? vals[c0] : 0u;
+  stage_load(0, val, key < sent);
+  Xyzz<C> acc = Xyzz<C>::inf();
+  const size_t steps = c1 - c0;  // per lane; the loop runs to the wave's longest chunk
+  const size_t maxsteps = (size_t)1 << lg;
+  for (size_t s = 0; s < maxsteps; s++) {
+    const size_t e = c0 + s;
+    const bool live = s < steps;
+    uint32_t key_n = sent, val_n = 0;
+    if (s + 1 < steps) {
+      key_n = keys[e + 1];
+      if (key_n < sent) val_n = vals[e + 1];
+    }
+    const Affine<C> pt = stage_read((int)(s & 1), val);
+    stage_load((int)((s + 1) & 1), val_n, key_n < sent);
+    if (live && key < sent) {
+      acc = add_affine(acc, pt);
+      if (key_n != key) {
+        const bool starts = bstart[key] >= c0;
+        const bool ends = bend[key] <= c1;
+        if (starts && ends)
+          store_xyzz(buckets, key, A::out(acc));
+        else
+          store_xyzz(part, 2 * t + (starts ? 1 : 0), A::out(acc));
+        acc = Xyzz<C>::inf();
+      }
+    }
+    key = key_n;
+    val = val_n;
+    if (__all(s + 1 >= steps ? 1 : 0)) break;  // wave-uniform exit
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no staging load outstanding at exit
+}
+
 // k_bucket_acc_short over G2 with pair-distributed Fq2 (pair_fq2.h): lanes
 // 2t and 2t+1 run chunk t's bucket chain together, each holding one Fq
 // coordinate of every Fq2 value; same chunking, parking and bucket stores.
@@ -1391,8 +1475,18 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
         const char* e = getenv("TPST_ACC_MINW");
         return e ? atoi(e) : 2;  // 3 and 4 spill (32 / 111 VGPRs) and measured slower
       }();
+      static const bool lds = [] {
+        const char* e = getenv("TPST_ACC_LDS");
+        return e && atoi(e) != 0;
+      }();
       const unsigned grid = grid_for(gchunks, 64);
-      if (minw >= 4)
+      if (lds && minw >= 3)
+        k_bucket_acc_short_lds<3><<<grid, 64, 0, bulk>>>(keys, vals, range, wlo, whi, sent, bstart, bend, d_bases,
+                                                          phib, (uint32_t)n, lg, buckets, part);
+      else if (lds)
+        k_bucket_acc_short_lds<2><<<grid, 64, 0, bulk>>>(keys, vals, range, wlo, whi, sent, bstart, bend, d_bases,
+                                                          phib, (uint32_t)n, lg, buckets, part);
+      else if (minw >= 4)
         k_bucket_acc_short<F, 4><<<grid, 64, 0, bulk>>>(keys, vals, range, wlo, whi, sent, bstart, bend, d_bases,
                                                          phib, (uint32_t)n, lg, buckets, part);
       else if (minw == 3)

@@ -12,8 +12,6 @@
 //                     the r_A / r_B / r_C combination (r1csproof.rs:326-338) fused
 //   phase one         prove_cubic_with_additive_term (sumcheck.rs:67-148), comb tau (A B - C)
 //   phase two         prove_quad (sumcheck.rs:387-444), comb A B
-#include <hipcub/hipcub.hpp>
-
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -22,6 +20,7 @@
 #include "ctx.h"
 #include "device_util.h"
 #include "r1cs_state.h"
+#include "scan_sort.h"
 
 using namespace tpst;
 
@@ -343,10 +342,8 @@ static hipError_t build_compressed(hipStream_t s, const uint32_t* key, const uin
   TPST_TRY_HIP(hipMemsetAsync(cnt.p, 0, (nkeys + 1) * 4, s));
   if (nnz) k_count<<<grid_for(nnz, 256), 256, 0, s>>>(key, nnz, cnt.u());
   TPST_TRY_HIP(hipGetLastError());
-  size_t tb = 0;
-  TPST_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt.u(), ptr.u(), (int)(nkeys + 1), s));
-  TPST_TRY_HIP(tmp.alloc(tb));
-  TPST_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, cnt.u(), ptr.u(), (int)(nkeys + 1), s));
+  TPST_TRY_HIP(tmp.alloc(scan_sort::scan_scratch(nkeys + 1) * 4 + 4));
+  TPST_TRY_HIP(scan_sort::scan_excl_u32(s, cnt.u(), ptr.u(), nkeys + 1, tmp.u()));
   TPST_TRY_HIP(hipMemcpyAsync(cursor.p, ptr.p, (nkeys + 1) * 4, hipMemcpyDeviceToDevice, s));
   if (nnz) k_scatter<<<grid_for(nnz, 256), 256, 0, s>>>(key, other, val, nnz, cursor.u(), idx.u(), vout.u());
   TPST_TRY_HIP(hipGetLastError());
@@ -710,17 +707,14 @@ extern "C" int tpst_r1cs_commit(tpst_ctx* ctx, tpst_r1cs* R, const uint8_t* labe
     TPST_HIP(ctx, spos.alloc(M3 * 4));
     TPST_HIP(ctx, rts.alloc(M3 * 4));
     TPST_HIP(ctx, audit.alloc(cells * 4));
-    size_t sb = 0;
-    TPST_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, sb, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                                     (uint32_t*)nullptr, (uint32_t*)nullptr, (int)M3, 0, vmax + 1, s));
-    TPST_HIP(ctx, tmp.alloc(sb));
+    TPST_HIP(ctx, tmp.alloc(scan_sort::sort_scratch(M3) * 4));
     for (int rc = 0; rc < 2; rc++) {  // rows, then columns
       const Buf* o = rc ? R->ocol : R->orow;
       k_ops_addr<<<grid_for(M3, 256), 256, 0, s>>>(o[0].u(), o[1].u(), o[2].u(), (uint32_t)R->nnz[0],
                                                    (uint32_t)R->nnz[1], (uint32_t)R->nnz[2], N, addr.u(), pos.u());
       TPST_HIP(ctx, hipGetLastError());
-      TPST_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(tmp.p, sb, addr.u(), skey.u(), pos.u(), spos.u(), (int)M3, 0,
-                                                       vmax + 1, s));
+      // stable by address: equal addresses keep position order (the timestamps' rank)
+      TPST_HIP(ctx, scan_sort::stable_sort_pairs(s, addr.u(), pos.u(), skey.u(), spos.u(), M3, vmax + 1, tmp.u()));
       TPST_HIP(ctx, hipMemsetAsync(audit.p, 0, cells * 4, s));
       k_timestamps<<<grid_for(M3, 256), 256, 0, s>>>(skey.u(), spos.u(), M3, rts.u(), audit.u());
       TPST_HIP(ctx, hipGetLastError());

@@ -5,8 +5,8 @@ one launch per window group (msm.hip msm_groups), so the figures are per MSM
 reports half of the bytes of wide coalesced reads -> x2; WRITE_SIZE as is.
 FETCH/WRITE_SIZE are in KB (rocprofv3 derived metrics, 1024 B).
 
-The VALU pass also holds the bench's Fq-multiply microbenchmark (k_mb_fqmul,
-200 products per lane): its SQ_INSTS_VALU per wave-product against the
+The VALU pass also holds the bench's Fq-multiply microbenchmark (k_mb_fq29,
+the accumulation's radix-2^29 product, 200 per lane; k_mb_fqmul before round 4): its SQ_INSTS_VALU per wave-product against the
 accumulation's per wave-madd gives the mixed add's cost in Fq-product
 equivalents from counted instructions (bench.py's compute column).  With a
 kernel-trace directory of the same bench, the per-grid launch durations of the
@@ -37,7 +37,9 @@ def main():
     fetch = load(dfetch, "FETCH_SIZE")
     write = load(dwrite, "WRITE_SIZE")
     valu = load(dvalu, "SQ_INSTS_VALU")
-    mb = load(dvalu, "SQ_INSTS_VALU", "k_mb_fqmul")
+    mb = load(dvalu, "SQ_INSTS_VALU", "k_mb_fq29")  # the accumulation's product (field29.h, bench MB_FQMUL_KIND)
+    if not mb:
+        mb = load(dvalu, "SQ_INSTS_VALU", "k_mb_fqmul")
     avg = lambda v: sum(v) / len(v)  # noqa: E731
     n_msm = min(len(v) for v in fetch.values())
     per_msm = lambda d: sum(sum(v) for v in d.values()) / n_msm if d else None  # noqa: E731
