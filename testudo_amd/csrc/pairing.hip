@@ -7,6 +7,8 @@
 #include "device_util.h"
 #include "pairing_kernels.h"
 #include "wave_tower.h"
+#include "rns_engine.h"
+#include <cstdlib>
 
 namespace tpst {
 
@@ -518,6 +520,205 @@ __global__ void __launch_bounds__(128) k_chain_final(const Fq12* __restrict__ MB
   wave::store_f12(vals, r, out + g);
 }
 
+// ---- the same chain on the RNS engine (rns_engine.h) ------------------------
+// Two groups per workgroup (the two halves of every wave), twelve waves: one
+// per Fq12 output coefficient, so a stage is a dozen parallel RNS Montgomery
+// reductions instead of a wave's lone-lane product chain.  The Fq inversion of
+// the final exponentiation runs on lanes 0 / 32 of wave 0 between two stages.
+// TPST_CHAIN_RNS=0 keeps k_chain_final (A/B and fallback for the tests).
+#ifndef TPST_CHAIN_RNS
+#define TPST_CHAIN_RNS 1
+#endif
+constexpr int RC_WAVES = 12;
+constexpr int RC_SLOTS = rns::N_CONSTS + 36 + 10 * 12 + 24;
+static_assert((size_t)(RC_SLOTS * rns::SLOT + RC_WAVES * rns::XCH) * 4 <= 65536, "RNS chain LDS");
+
+__device__ int rc_exp_by_x(const rns::Eng& e, const rns::Lane& L, int src, int r1, int r2) {
+  int cur = src;
+  for (int b = X_BITS - 2; b >= 0; b--) {
+    int nxt = cur == r1 ? r2 : r1;
+    rns::stage<rns::OP_CYC_SQR>(e, L, cur, 0, nxt);
+    cur = nxt;
+    if ((params::BLS_X >> b) & 1) {
+      nxt = cur == r1 ? r2 : r1;
+      rns::stage<rns::OP_F12_MUL>(e, L, cur, src, nxt);
+      cur = nxt;
+    }
+  }
+  return cur;
+}
+
+// fe_final_exp on the RNS engine (same chain, eprint 2020/875)
+__device__ int rc_final_exp(const rns::Eng& e, const rns::Lane& L, int F, int regs, int I, Fq* sh_n) {
+  using namespace rns;
+#define R(i) (regs + 12 * (i))
+  stage<OP_INV1>(e, L, F, 0, I + 0);         // t = c0^2 - v c1^2
+  stage<OP_INV2>(e, L, I + 0, 0, I + 6);     // Fq6 adjugate c'
+  stage<OP_INV3>(e, L, I + 6, I + 0, I + 12);  // Fq6 norm t'
+  stage<OP_INV4>(e, L, I + 12, 0, I + 14);   // Fq2 norm n
+  store(e, L, I + 14, sh_n, sh_n + 1, 1);
+  const int lane = threadIdx.x & 63;
+  if (wave_id() == 0 && (lane & 31) == 0) sh_n[lane >> 5] = inv(sh_n[lane >> 5]);
+  __syncthreads();
+  load(e, L, sh_n, sh_n + 1, I + 15, 1);
+  stage<OP_INV5>(e, L, I + 12, I + 15, I + 16);  // t'^-1
+  stage<OP_INV6>(e, L, I + 6, I + 16, I + 18);   // t^-1
+  stage<OP_INV7>(e, L, F, I + 18, R(0));         // f^-1
+  // easy part
+  stage<OP_CONJ>(e, L, F, 0, R(1));
+  stage<OP_F12_MUL>(e, L, R(1), R(0), R(2));  // r = conj(f) f^-1
+  stage<OP_FROB2>(e, L, R(2), 0, R(1));
+  stage<OP_F12_MUL>(e, L, R(1), R(2), R(3));  // r = r^(p^2) r
+  // hard part
+  stage<OP_CYC_SQR>(e, L, R(3), 0, R(4));  // y0
+  int t = rc_exp_by_x(e, L, R(3), R(5), R(6));
+  stage<OP_CONJ>(e, L, R(3), 0, R(7));      // y2 = conj(r)
+  stage<OP_F12_MUL>(e, L, t, R(7), R(8));   // y1 = y1 y2
+  t = rc_exp_by_x(e, L, R(8), R(5), R(6));  // y2
+  stage<OP_CONJ>(e, L, R(8), 0, R(7));
+  stage<OP_F12_MUL>(e, L, R(7), t, R(9));   // y1 = conj(y1) y2
+  t = rc_exp_by_x(e, L, R(9), R(5), R(6));  // y2
+  stage<OP_FROB1>(e, L, R(9), 0, R(7));
+  stage<OP_F12_MUL>(e, L, R(7), t, R(8));   // y1 = frob(y1) y2
+  stage<OP_F12_MUL>(e, L, R(3), R(4), R(0));  // r = r y0
+  const int y0 = rc_exp_by_x(e, L, R(8), R(5), R(6));
+  const int y2 = rc_exp_by_x(e, L, y0, y0 == R(5) ? R(6) : R(5), R(1));
+  stage<OP_FROB2>(e, L, R(8), 0, R(2));  // y0 = frob2(y1)
+  stage<OP_CONJ>(e, L, R(8), 0, R(3));
+  stage<OP_F12_MUL>(e, L, R(3), y2, R(4));   // y1 = conj(y1) y2
+  stage<OP_F12_MUL>(e, L, R(4), R(2), R(7));  // y1 = y1 y0
+  stage<OP_F12_MUL>(e, L, R(0), R(7), R(9));  // r = r y1
+  return R(9);
+#undef R
+}
+
+// tree products on the RNS engine: out[g][j] = prod in[g][j*CH .. j*CH+CH),
+// two outputs per workgroup, the result in RNS form.  From field.h Fq12
+// (RES_IN false) the first factor is loaded with K_LOAD[CH] and the others
+// raw (no reduction), so a chunk costs CH - 1 stages; a short tail chunk is
+// padded with ones so both halves run the same stage sequence.
+template <bool RES_IN>
+__global__ void __launch_bounds__(64 * RC_WAVES) k_chunk_prod_rns(const void* __restrict__ in, size_t groups,
+                                                                  size_t n, size_t nout, uint32_t* __restrict__ out,
+                                                                  int chunk) {
+  __shared__ uint32_t s_slots[(rns::N_CONSTS + 36) * rns::SLOT];
+  __shared__ uint32_t s_xch[RC_WAVES * rns::XCH];
+  const size_t items = groups * nout;
+  const size_t o0 = 2 * (size_t)blockIdx.x, o1 = o0 + 1 < items ? o0 + 1 : o0;
+  rns::load_consts((rns::lds_t*)s_slots);
+  const rns::Lane L = rns::load_lane();
+  const rns::Eng e{(rns::lds_t*)s_slots, (rns::lds_t*)s_xch + rns::wave_id() * rns::XCH, 0};
+  __syncthreads();
+  int acc = rns::N_CONSTS, in_r = acc + 12, tmp = acc + 24;
+  const size_t k0a = (o0 % nout) * chunk, k0b = (o1 % nout) * chunk;
+  const size_t ba = (o0 / nout) * n, bb = (o1 / nout) * n;
+  for (int i = 0; i < chunk; i++) {
+    const bool va = k0a + i < n, vb = k0b + i < n;
+    const int dst = i == 0 ? acc : in_r;
+    if (RES_IN) {
+      const uint32_t* r = static_cast<const uint32_t*>(in);
+      rns::load_res(e, va ? r + (ba + k0a + i) * rns::RES_WORDS : nullptr,
+                    vb ? r + (bb + k0b + i) * rns::RES_WORDS : nullptr, dst, 12);
+    } else {
+      const Fq* f = static_cast<const Fq*>(in);
+      const Fq* fa = va ? f + 12 * (ba + k0a + i) : nullptr;
+      const Fq* fb = vb ? f + 12 * (bb + k0b + i) : nullptr;
+      if (i == 0)
+        rns::load(e, L, fa, fb, dst, 12, chunk);
+      else
+        rns::load_raw(e, L, fa, fb, dst, 12);
+    }
+    if (i > 0) {
+      rns::stage<rns::OP_F12_MUL>(e, L, acc, in_r, tmp);
+      const int t = acc;
+      acc = tmp;
+      tmp = t;
+    }
+  }
+  rns::store_res(e, acc, out + o0 * rns::RES_WORDS, out + o1 * rns::RES_WORDS, 12);
+}
+
+// block multipliers on the RNS engine: one workgroup per (block, pair of
+// groups) -- both halves of a wave must run the same stage sequence, so the
+// pair shares the block (and so its bit pattern).  Input: the per-bit line
+// products M (field.h Fq12, or RNS form from k_chunk_prod_rns); MB is left
+// in RNS form.
+template <bool RES_IN>
+__global__ void __launch_bounds__(64 * RC_WAVES) k_miller_blocks_rns(const void* __restrict__ M, size_t groups,
+                                                                     uint32_t* __restrict__ MBr) {
+  __shared__ uint32_t s_slots[(rns::N_CONSTS + 36) * rns::SLOT];
+  __shared__ uint32_t s_xch[RC_WAVES * rns::XCH];
+  const size_t pairs = (groups + 1) / 2;
+  const int blk = (int)(blockIdx.x / pairs);
+  const size_t g0 = 2 * (blockIdx.x % pairs), g1 = g0 + 1 < groups ? g0 + 1 : g0;
+  rns::load_consts((rns::lds_t*)s_slots);
+  const rns::Lane L = rns::load_lane();
+  const rns::Eng e{(rns::lds_t*)s_slots, (rns::lds_t*)s_xch + rns::wave_id() * rns::XCH, 0};
+  __syncthreads();
+  int acc = rns::N_CONSTS, in_r = acc + 12, tmp = acc + 24;
+  auto fetch = [&](int idx, int dst) {
+    if (RES_IN) {
+      const uint32_t* r = static_cast<const uint32_t*>(M);
+      rns::load_res(e, r + (g0 * N_LINE_COEFFS + idx) * rns::RES_WORDS,
+                    r + (g1 * N_LINE_COEFFS + idx) * rns::RES_WORDS, dst, 12);
+    } else {
+      const Fq* f = static_cast<const Fq*>(M);
+      rns::load(e, L, f + 12 * (g0 * N_LINE_COEFFS + idx), f + 12 * (g1 * N_LINE_COEFFS + idx), dst, 12);
+    }
+  };
+  const int lo = blk * LB, hi = (lo + LB < N_BITS ? lo + LB : N_BITS) - 1;
+  for (int b = hi; b >= lo; b--) {
+    const int idx = dbl_idx(b);
+    if (b == hi) {
+      fetch(idx, acc);
+    } else {
+      rns::stage<rns::OP_F12_SQR>(e, L, acc, 0, tmp);
+      fetch(idx, in_r);
+      rns::stage<rns::OP_F12_MUL>(e, L, tmp, in_r, acc);
+    }
+    if ((params::BLS_X >> b) & 1) {
+      fetch(idx + 1, in_r);
+      rns::stage<rns::OP_F12_MUL>(e, L, acc, in_r, tmp);
+      const int t = acc;
+      acc = tmp;
+      tmp = t;
+    }
+  }
+  rns::store_res(e, acc, MBr + (g0 * NBLK + blk) * rns::RES_WORDS, MBr + (g1 * NBLK + blk) * rns::RES_WORDS, 12);
+}
+
+__global__ void __launch_bounds__(64 * RC_WAVES) k_chain_final_rns(const uint32_t* __restrict__ MBr, size_t groups,
+                                                                   Fq12* __restrict__ out, int do_final) {
+  __shared__ uint32_t s_slots[RC_SLOTS * rns::SLOT];
+  __shared__ uint32_t s_xch[RC_WAVES * rns::XCH];
+  __shared__ Fq sh_n[2];
+  const size_t g0 = 2 * (size_t)blockIdx.x, g1 = g0 + 1 < groups ? g0 + 1 : g0;
+  rns::load_consts((rns::lds_t*)s_slots);
+  const rns::Lane L = rns::load_lane();
+  const rns::Eng e{(rns::lds_t*)s_slots, (rns::lds_t*)s_xch + rns::wave_id() * rns::XCH, 0};
+  __syncthreads();
+  int acc = rns::N_CONSTS, in_r = acc + 12, tmp = acc + 24;
+  const uint32_t* m0 = MBr + g0 * NBLK * rns::RES_WORDS;
+  const uint32_t* m1 = MBr + g1 * NBLK * rns::RES_WORDS;
+  rns::load_res(e, m0 + (NBLK - 1) * rns::RES_WORDS, m1 + (NBLK - 1) * rns::RES_WORDS, acc, 12);
+  for (int blk = NBLK - 2; blk >= 0; blk--) {
+    for (int i = 0; i < LB; i++) {
+      rns::stage<rns::OP_F12_SQR>(e, L, acc, 0, tmp);
+      const int t = acc;
+      acc = tmp;
+      tmp = t;
+    }
+    rns::load_res(e, m0 + blk * rns::RES_WORDS, m1 + blk * rns::RES_WORDS, in_r, 12);
+    rns::stage<rns::OP_F12_MUL>(e, L, acc, in_r, tmp);
+    const int t = acc;
+    acc = tmp;
+    tmp = t;
+  }
+  int r = acc;
+  if (do_final) r = rc_final_exp(e, L, acc, rns::N_CONSTS + 36, rns::N_CONSTS + 36 + 120, sh_n);
+  rns::store(e, L, r, reinterpret_cast<Fq*>(out + g0), reinterpret_cast<Fq*>(out + g1), 12);
+}
+
 static size_t line_tree_len(size_t n) {  // tree levels over n pairs, chunk TREE_CHUNK
   size_t tot = 0;
   while (n > 1) {
@@ -530,20 +731,57 @@ static size_t line_tree_len(size_t n) {  // tree levels over n pairs, chunk TREE
 size_t multi_pairing_scratch(size_t groups, size_t n) {
   const size_t G = groups * N_LINE_COEFFS;
   return Arena::need(G * (n ? n : 1), sizeof(Fq12)) + Arena::need(G * (line_tree_len(n) + 1), sizeof(Fq12)) +
-         Arena::need(groups * NBLK, sizeof(Fq12)) + Arena::need(groups * NBLK, sizeof(Fq)) + 4096 + 256 * 16;
+         Arena::need(groups * NBLK, sizeof(Fq12)) + Arena::need(groups * NBLK, sizeof(Fq)) +
+         Arena::need(groups * NBLK * rns::RES_WORDS, sizeof(uint32_t)) +
+         Arena::need(G * line_tree_len(n) * rns::RES_WORDS, sizeof(uint32_t)) + 4096 + 256 * 16;
 }
 
 // tree products of the lines, block multipliers, Horner chain (+ final exp)
 static hipError_t pairing_from_lines(Arena& ar, hipStream_t s, Fq12* lines, size_t groups, size_t n, Fq12* d_out,
                                      bool final_exp) {
   const size_t G = groups * N_LINE_COEFFS;
-  while (n > 1) {
+  static const bool use_rns = [] {
+    const char* v = getenv("TPST_CHAIN_RNS");
+    return v ? atoi(v) != 0 : TPST_CHAIN_RNS != 0;
+  }();
+  static const bool tree_rns = [] {  // TPST_TREE_RNS=0: radix-engine tree levels (A/B)
+    const char* v = getenv("TPST_TREE_RNS");
+    return v ? atoi(v) != 0 : true;
+  }();
+  while (n > 1 && !(use_rns && tree_rns)) {
     const size_t nout = (n + TREE_CHUNK - 1) / TREE_CHUNK;
     Fq12* nxt = ar.take<Fq12>(G * nout);
     k_f12_chunk_prod<<<grid_for(G * nout, RW), 64 * RW, RW_LDS, s>>>(lines, G, n, nout, nxt, TREE_CHUNK);
     TPST_TRY(hipGetLastError());
     lines = nxt;
     n = nout;
+  }
+  if (use_rns) {
+    // tree levels in RNS form (the first from the field.h line products)
+    const void* cur = lines;
+    bool res = false;
+    while (n > 1) {
+      const size_t nout = (n + TREE_CHUNK - 1) / TREE_CHUNK;
+      uint32_t* nxt = ar.take<uint32_t>(G * nout * rns::RES_WORDS);
+      const unsigned wg = (unsigned)((G * nout + 1) / 2);
+      if (res)
+        k_chunk_prod_rns<true><<<wg, 64 * RC_WAVES, 0, s>>>(cur, G, n, nout, nxt, TREE_CHUNK);
+      else
+        k_chunk_prod_rns<false><<<wg, 64 * RC_WAVES, 0, s>>>(cur, G, n, nout, nxt, TREE_CHUNK);
+      TPST_TRY(hipGetLastError());
+      cur = nxt;
+      res = true;
+      n = nout;
+    }
+    uint32_t* MBr = ar.take<uint32_t>(groups * NBLK * rns::RES_WORDS);
+    const unsigned pairs = (unsigned)((groups + 1) / 2);
+    if (res)
+      k_miller_blocks_rns<true><<<pairs * NBLK, 64 * RC_WAVES, 0, s>>>(cur, groups, MBr);
+    else
+      k_miller_blocks_rns<false><<<pairs * NBLK, 64 * RC_WAVES, 0, s>>>(cur, groups, MBr);
+    TPST_TRY(hipGetLastError());
+    k_chain_final_rns<<<pairs, 64 * RC_WAVES, 0, s>>>(MBr, groups, d_out, final_exp ? 1 : 0);
+    return hipGetLastError();
   }
   Fq12* MB = ar.take<Fq12>(groups * NBLK);
   Fq* MBn = final_exp ? ar.take<Fq>(groups * NBLK) : nullptr;
