@@ -5,6 +5,7 @@
 #include "ctx.h"
 #include "device_util.h"
 #include "wave_tower.h"
+#include "rns_engine.h"
 #include "field29.h"
 
 using namespace tpst;
@@ -328,6 +329,29 @@ __global__ void __launch_bounds__(64) k_mb_wave_prof(int op, int iters, unsigned
     for (int i = 0; i < 5; i++) out[i] = acc[i];
 }
 
+// RNS engine stages (rns_engine.h): each 12-wave workgroup (two chains) runs
+// `iters` dependent stages of OP; grid = threads / 768 workgroups, so one
+// workgroup measures the stage latency and a full grid the throughput
+template <int OP>
+__global__ void __launch_bounds__(768) k_mb_rns(int iters, uint32_t* __restrict__ sink) {
+  __shared__ uint32_t s_slots[(rns::N_CONSTS + 36) * rns::SLOT];
+  __shared__ uint32_t s_xch[12 * rns::XCH];
+  rns::load_consts((rns::lds_t*)s_slots);
+  const rns::Lane L = rns::load_lane();
+  const rns::Eng e{(rns::lds_t*)s_slots, (rns::lds_t*)s_xch + rns::wave_id() * rns::XCH, 0};
+  for (int i = threadIdx.x; i < 24 * rns::SLOT; i += blockDim.x)
+    s_slots[rns::N_CONSTS * rns::SLOT + i] = s_slots[((i / rns::SLOT) % rns::N_CONSTS) * rns::SLOT + (i % rns::SLOT)];
+  __syncthreads();
+  int acc = rns::N_CONSTS, in_r = acc + 12, tmp = acc + 24;
+  for (int it = 0; it < iters; it++) {
+    rns::stage<OP>(e, L, acc, in_r, tmp);
+    const int t = acc;
+    acc = tmp;
+    tmp = t;
+  }
+  rns::store_res(e, acc, sink + (size_t)blockIdx.x * 2 * rns::RES_WORDS, sink + ((size_t)blockIdx.x * 2 + 1) * rns::RES_WORDS, 12);
+}
+
 extern "C" int tpst_microbench_wave_phases(tpst_ctx* ctx, int op, int iters, uint64_t* cycles5) {
   if (!ctx || !cycles5 || op < 0 || op >= wave::N_OPS || iters <= 0) return fail(ctx, TPST_E_ARG, "bad argument");
   std::lock_guard<std::mutex> lk(ctx->mu);
@@ -347,7 +371,8 @@ extern "C" int tpst_microbench(tpst_ctx* ctx, int kind, size_t threads, int iter
   if (!ctx || !ms || threads == 0 || iters <= 0) return fail(ctx, TPST_E_ARG, "bad argument");
   std::lock_guard<std::mutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
-  const unsigned bs = threads < 256 ? (unsigned)threads : 256u;
+  const bool rnsk = kind >= 64 && kind < 64 + rns::N_OPS;
+  const unsigned bs = rnsk ? 768u : (threads < 256 ? (unsigned)threads : 256u);
   const unsigned grid = grid_for(threads, bs);
   ctx->io.reset();
   TPST_HIP(ctx, ctx->io.reserve(Arena::need((size_t)grid * bs * 12, 4)));
@@ -386,6 +411,12 @@ extern "C" int tpst_microbench(tpst_ctx* ctx, int kind, size_t threads, int iter
     const int op = kind - 16;
     const size_t lds = (((wave::OP_LEN[op] + 3) & ~3u) + (size_t)(wave::N_CONSTS + 64 + 4 * 48) * wave::SLOT) * 4;
     k_mb_wave<<<1, 64, lds, ctx->stream>>>(op, iters, d);
+  } else if (kind == 64 + rns::OP_F12_MUL) {
+    k_mb_rns<rns::OP_F12_MUL><<<grid, bs, 0, ctx->stream>>>(iters, d);
+  } else if (kind == 64 + rns::OP_F12_SQR) {
+    k_mb_rns<rns::OP_F12_SQR><<<grid, bs, 0, ctx->stream>>>(iters, d);
+  } else if (kind == 64 + rns::OP_CYC_SQR) {
+    k_mb_rns<rns::OP_CYC_SQR><<<grid, bs, 0, ctx->stream>>>(iters, d);
   } else
     return fail(ctx, TPST_E_ARG, "unknown microbench kind");
   TPST_HIP(ctx, hipGetLastError());

@@ -74,8 +74,94 @@ __global__ void __launch_bounds__(64 * PW) k_g2_prepare_wave(const uint32_t* __r
   }
 }
 
-hipError_t g2_prepare_batch(hipStream_t s, const uint32_t* d_g2, size_t n, LineCoeff* d_coeffs) {
+// ---- G2Prepared on the RNS engine ------------------------------------------
+// The same chain (one 44-slot region per point, the two halves of a
+// 12-wave workgroup holding two points): G2_DBL1-4 / G2_ADD1-4 as RNS stages,
+// each step's line (region slots 6..11) dumped in residue form, then
+// k_rns_to_fq converts every coefficient to field.h form in bulk -- ~280
+// stages of ~1 us against the radix engine's ~6 us stages.
+__global__ void __launch_bounds__(768) k_g2_prepare_rns(const uint32_t* __restrict__ g2, size_t n,
+                                                        uint32_t* __restrict__ lres) {
+  __shared__ uint32_t s_slots[(rns::N_CONSTS + 44) * rns::SLOT];
+  __shared__ uint32_t s_xch[12 * rns::XCH];
+  rns::load_consts((rns::lds_t*)s_slots);
+  const rns::Lane L = rns::load_lane();
+  const rns::Eng e{(rns::lds_t*)s_slots, (rns::lds_t*)s_xch + rns::wave_id() * rns::XCH, 0};
+  const int w = rns::wave_id(), lane = threadIdx.x & 63;
+  const size_t p0 = 2 * (size_t)blockIdx.x, p1 = p0 + 1 < n ? p0 + 1 : p0;
+  const int R = rns::N_CONSTS;
+  __syncthreads();
+  // x, y (and the copy of Q at 26..29); z = 1
+  const Fq* q0 = reinterpret_cast<const Fq*>(g2 + p0 * 48);
+  const Fq* q1 = reinterpret_cast<const Fq*>(g2 + p1 * 48);
+  rns::load(e, L, q0, q1, R, 4);
+  if (w < 4) e.slots[(R + 26 + w) * rns::SLOT + lane] = e.slots[(R + w) * rns::SLOT + lane];
+  if (w == 4) e.slots[(R + 4) * rns::SLOT + lane] = e.slots[e.kon * rns::SLOT + lane];
+  if (w == 5) e.slots[(R + 5) * rns::SLOT + lane] = 0;
+  __syncthreads();
+  const size_t p = (lane & 32) ? p1 : p0;
+  size_t idx = 0;
+  auto dump = [&]() {  // line (c0, c1, c2) of step idx
+    if (w < 6) lres[((idx * n + p) * 6 + w) * 32 + (lane & 31)] = e.slots[(R + 6 + w) * rns::SLOT + lane];
+    __syncthreads();
+    idx++;
+  };
+  for (int b = X_BITS - 2; b >= 0; b--) {
+    rns::stage<rns::OP_G2_DBL1, rns::OP_RW[rns::OP_G2_DBL1] != 0>(e, L, R, R, R);
+    rns::stage<rns::OP_G2_DBL2, rns::OP_RW[rns::OP_G2_DBL2] != 0>(e, L, R, R, R);
+    rns::stage<rns::OP_G2_DBL3, rns::OP_RW[rns::OP_G2_DBL3] != 0>(e, L, R, R, R);
+    rns::stage<rns::OP_G2_DBL4, rns::OP_RW[rns::OP_G2_DBL4] != 0>(e, L, R, R, R);
+    dump();
+    if ((params::BLS_X >> b) & 1) {
+      rns::stage<rns::OP_G2_ADD1, rns::OP_RW[rns::OP_G2_ADD1] != 0>(e, L, R, R, R);
+      rns::stage<rns::OP_G2_ADD2, rns::OP_RW[rns::OP_G2_ADD2] != 0>(e, L, R, R, R);
+      rns::stage<rns::OP_G2_ADD3, rns::OP_RW[rns::OP_G2_ADD3] != 0>(e, L, R, R, R);
+      rns::stage<rns::OP_G2_ADD4, rns::OP_RW[rns::OP_G2_ADD4] != 0>(e, L, R, R, R);
+      dump();
+    }
+  }
+}
+
+// count M-domain residue vectors (32 u32 each) -> field.h Montgomery Fq,
+// two per wave and pass
+__global__ void __launch_bounds__(256) k_rns_to_fq(const uint32_t* __restrict__ res, size_t count,
+                                                   Fq* __restrict__ out) {
+  __shared__ uint32_t s_slots[rns::N_CONSTS * rns::SLOT];
+  __shared__ uint32_t s_xch[4 * rns::XCH];
+  rns::load_consts((rns::lds_t*)s_slots);
+  const rns::Lane L = rns::load_lane();
+  const rns::Eng e{(rns::lds_t*)s_slots, (rns::lds_t*)s_xch + (threadIdx.x >> 6) * rns::XCH, 0};
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const size_t pairs = (count + 1) / 2;
+  for (size_t pw = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6); pw < pairs; pw += (size_t)gridDim.x * 4) {
+    const size_t v0 = 2 * pw, v1 = v0 + 1 < count ? v0 + 1 : v0;
+    const uint32_t x = res[((lane & 32) ? v1 : v0) * 32 + (lane & 31)];
+    rns::to_fq_wave(e, L, x, out + v0, out + v1);
+  }
+}
+
+size_t g2_prepare_scratch(size_t n) { return n * N_LINE_COEFFS * 6 * 32 * sizeof(uint32_t); }
+
+static bool g2_rns() {
+  static const bool on = [] {  // TPST_G2_RNS=0: the radix-engine preparation (A/B)
+    const char* v = getenv("TPST_G2_RNS");
+    return v ? atoi(v) != 0 : true;
+  }();
+  return on;
+}
+
+hipError_t g2_prepare_batch(hipStream_t s, const uint32_t* d_g2, size_t n, LineCoeff* d_coeffs, uint32_t* scratch) {
   if (!n) return hipSuccess;
+  if (scratch && g2_rns()) {
+    k_g2_prepare_rns<<<(unsigned)((n + 1) / 2), 768, 0, s>>>(d_g2, n, scratch);
+    TPST_TRY(hipGetLastError());
+    const size_t count = n * N_LINE_COEFFS * 6;
+    const size_t waves = (count + 1) / 2;
+    const unsigned grid = (unsigned)(waves / 4 < 2048 ? (waves + 3) / 4 : 2048);
+    k_rns_to_fq<<<grid, 256, 0, s>>>(scratch, count, reinterpret_cast<Fq*>(d_coeffs));
+    return hipGetLastError();
+  }
   k_g2_prepare_wave<<<grid_for(n, PW), 64 * PW, PW_LDS, s>>>(d_g2, n, d_coeffs);
   return hipGetLastError();
 }
@@ -597,45 +683,73 @@ __device__ int rc_final_exp(const rns::Eng& e, const rns::Lane& L, int F, int re
 // (RES_IN false) the first factor is loaded with K_LOAD[CH] and the others
 // raw (no reduction), so a chunk costs CH - 1 stages; a short tail chunk is
 // padded with ones so both halves run the same stage sequence.
-template <bool RES_IN>
+template <bool RES_IN, int CH>
 __global__ void __launch_bounds__(64 * RC_WAVES) k_chunk_prod_rns(const void* __restrict__ in, size_t groups,
-                                                                  size_t n, size_t nout, uint32_t* __restrict__ out,
-                                                                  int chunk) {
-  __shared__ uint32_t s_slots[(rns::N_CONSTS + 36) * rns::SLOT];
+                                                                  size_t n, size_t nout, uint32_t* __restrict__ out) {
+  __shared__ uint32_t s_slots[(rns::N_CONSTS + 12 * (CH + 1)) * rns::SLOT];
   __shared__ uint32_t s_xch[RC_WAVES * rns::XCH];
-  const size_t items = groups * nout;
-  const size_t o0 = 2 * (size_t)blockIdx.x, o1 = o0 + 1 < items ? o0 + 1 : o0;
+  const size_t items = groups * nout, pairs = (items + 1) / 2;
   rns::load_consts((rns::lds_t*)s_slots);
   const rns::Lane L = rns::load_lane();
   const rns::Eng e{(rns::lds_t*)s_slots, (rns::lds_t*)s_xch + rns::wave_id() * rns::XCH, 0};
+  const int w = rns::wave_id(), lane = threadIdx.x & 63;
+  const int X = rns::N_CONSTS;  // factor i in slots X + 12 i; the product ping-pongs with X + 12 CH
   __syncthreads();
-  int acc = rns::N_CONSTS, in_r = acc + 12, tmp = acc + 24;
-  const size_t k0a = (o0 % nout) * chunk, k0b = (o1 % nout) * chunk;
-  const size_t ba = (o0 / nout) * n, bb = (o1 / nout) * n;
-  for (int i = 0; i < chunk; i++) {
-    const bool va = k0a + i < n, vb = k0b + i < n;
-    const int dst = i == 0 ? acc : in_r;
-    if (RES_IN) {
-      const uint32_t* r = static_cast<const uint32_t*>(in);
-      rns::load_res(e, va ? r + (ba + k0a + i) * rns::RES_WORDS : nullptr,
-                    vb ? r + (bb + k0b + i) * rns::RES_WORDS : nullptr, dst, 12);
-    } else {
-      const Fq* f = static_cast<const Fq*>(in);
-      const Fq* fa = va ? f + 12 * (ba + k0a + i) : nullptr;
-      const Fq* fb = vb ? f + 12 * (bb + k0b + i) : nullptr;
-      if (i == 0)
-        rns::load(e, L, fa, fb, dst, 12, chunk);
-      else
-        rns::load_raw(e, L, fa, fb, dst, 12);
+  // persistent: a workgroup walks the output pairs (its setup amortized)
+  for (size_t pr = blockIdx.x; pr < pairs; pr += gridDim.x) {
+    const size_t o = (lane & 32) ? (2 * pr + 1 < items ? 2 * pr + 1 : 2 * pr) : 2 * pr;
+    const size_t k0 = (o % nout) * CH, base = (o / nout) * n;
+    // wave w fetches coefficient w of all CH factors at once (one memory
+    // latency per chunk, not one per factor)
+    uint32_t v[CH];
+#pragma unroll
+    for (int i = 0; i < CH; i++) {
+      const bool valid = k0 + i < n;
+      if (RES_IN) {
+        const uint32_t* r = static_cast<const uint32_t*>(in);
+        v[i] = valid ? r[(base + k0 + i) * rns::RES_WORDS + w * 32 + (lane & 31)]
+                     : (w == 0 ? e.slots[e.kon * rns::SLOT + lane] : 0u);
+      } else {
+        const Fq* f = static_cast<const Fq*>(in) + 12 * (base + k0 + i);
+        if (valid) {
+          v[i] = rns::residue(L, f[w].v);
+        } else {
+          uint32_t one[12];
+#pragma unroll
+          for (int k = 0; k < 12; k++) one[k] = w == 0 ? params::FQ_ONE[k] : 0u;
+          v[i] = rns::residue(L, one);
+        }
+      }
     }
-    if (i > 0) {
-      rns::stage<rns::OP_F12_MUL>(e, L, acc, in_r, tmp);
+    if (!RES_IN) {  // the first of CH raw factors carries the (M/R)^(CH-1) M correction
+      const uint32_t kin = e.slots[(e.kon + rns::K_LOAD[CH]) * rns::SLOT + lane];
+      v[0] = rns::mont(e, L, rns::red64((uint64_t)v[0] * kin, L));
+    }
+#pragma unroll
+    for (int i = 0; i < CH; i++) e.slots[(X + 12 * i + w) * rns::SLOT + lane] = v[i];
+    __syncthreads();
+    int acc = X, tmp = X + 12 * CH;
+#pragma unroll
+    for (int i = 1; i < CH; i++) {
+      rns::stage<rns::OP_F12_MUL>(e, L, acc, X + 12 * i, tmp);
       const int t = acc;
       acc = tmp;
       tmp = t;
     }
+    rns::store_res(e, acc, out + 2 * pr * rns::RES_WORDS,
+                   out + (2 * pr + 1 < items ? 2 * pr + 1 : 2 * pr) * rns::RES_WORDS, 12);
+    __syncthreads();  // the next chunk's factors overwrite these slots
   }
-  rns::store_res(e, acc, out + o0 * rns::RES_WORDS, out + o1 * rns::RES_WORDS, 12);
+}
+
+// workgroups for a persistent RNS kernel over `pairs` work items
+static unsigned rns_grid(size_t pairs) {
+  static const unsigned per_cu = [] {
+    const char* v = getenv("TPST_RNS_WG_PER_CU");
+    return v ? (unsigned)atoi(v) : 2u;
+  }();
+  const size_t cap = (size_t)256 * (per_cu ? per_cu : 1);
+  return (unsigned)(pairs < cap ? pairs : cap);
 }
 
 // block multipliers on the RNS engine: one workgroup per (block, pair of
@@ -643,10 +757,12 @@ __global__ void __launch_bounds__(64 * RC_WAVES) k_chunk_prod_rns(const void* __
 // pair shares the block (and so its bit pattern).  Input: the per-bit line
 // products M (field.h Fq12, or RNS form from k_chunk_prod_rns); MB is left
 // in RNS form.
+constexpr int MB_MAXV = 12;  // line products one block reads (LB doublings + its additions)
+
 template <bool RES_IN>
 __global__ void __launch_bounds__(64 * RC_WAVES) k_miller_blocks_rns(const void* __restrict__ M, size_t groups,
                                                                      uint32_t* __restrict__ MBr) {
-  __shared__ uint32_t s_slots[(rns::N_CONSTS + 36) * rns::SLOT];
+  __shared__ uint32_t s_slots[(rns::N_CONSTS + 24 + 12 * MB_MAXV) * rns::SLOT];
   __shared__ uint32_t s_xch[RC_WAVES * rns::XCH];
   const size_t pairs = (groups + 1) / 2;
   const int blk = (int)(blockIdx.x / pairs);
@@ -654,34 +770,41 @@ __global__ void __launch_bounds__(64 * RC_WAVES) k_miller_blocks_rns(const void*
   rns::load_consts((rns::lds_t*)s_slots);
   const rns::Lane L = rns::load_lane();
   const rns::Eng e{(rns::lds_t*)s_slots, (rns::lds_t*)s_xch + rns::wave_id() * rns::XCH, 0};
-  __syncthreads();
-  int acc = rns::N_CONSTS, in_r = acc + 12, tmp = acc + 24;
-  auto fetch = [&](int idx, int dst) {
-    if (RES_IN) {
-      const uint32_t* r = static_cast<const uint32_t*>(M);
-      rns::load_res(e, r + (g0 * N_LINE_COEFFS + idx) * rns::RES_WORDS,
-                    r + (g1 * N_LINE_COEFFS + idx) * rns::RES_WORDS, dst, 12);
-    } else {
-      const Fq* f = static_cast<const Fq*>(M);
-      rns::load(e, L, f + 12 * (g0 * N_LINE_COEFFS + idx), f + 12 * (g1 * N_LINE_COEFFS + idx), dst, 12);
-    }
-  };
+  const int w = rns::wave_id(), lane = threadIdx.x & 63;
+  const size_t g = (lane & 32) ? g1 : g0;
   const int lo = blk * LB, hi = (lo + LB < N_BITS ? lo + LB : N_BITS) - 1;
-  for (int b = hi; b >= lo; b--) {
-    const int idx = dbl_idx(b);
-    if (b == hi) {
-      fetch(idx, acc);
+  const int V = rns::N_CONSTS + 24;  // the block's line products, in reading order
+  // every line product of the block fetched at once: line index idx(hi) .. ,
+  // in the order the Horner below consumes them
+  const int idx_hi = dbl_idx(hi);
+  const int nv = dbl_idx(lo) + 1 + (int)((params::BLS_X >> lo) & 1) - idx_hi;
+  for (int v = 0; v < nv; v++) {
+    const size_t li = g * N_LINE_COEFFS + idx_hi + v;
+    uint32_t x;
+    if (RES_IN) {
+      x = static_cast<const uint32_t*>(M)[li * rns::RES_WORDS + w * 32 + (lane & 31)];
     } else {
-      rns::stage<rns::OP_F12_SQR>(e, L, acc, 0, tmp);
-      fetch(idx, in_r);
-      rns::stage<rns::OP_F12_MUL>(e, L, tmp, in_r, acc);
+      const uint32_t r = rns::residue(L, static_cast<const Fq*>(M)[12 * li + w].v);
+      x = rns::mont(e, L, rns::red64((uint64_t)r * e.slots[(e.kon + rns::K_IN) * rns::SLOT + lane], L));
+    }
+    e.slots[(V + 12 * v + w) * rns::SLOT + lane] = x;
+  }
+  __syncthreads();
+  // two work registers; other(x) is the one not holding x
+  const int W0 = rns::N_CONSTS, W1 = rns::N_CONSTS + 12;
+  auto other = [&](int x) { return x == W0 ? W1 : W0; };
+  int acc = V, v = 1;
+  for (int b = hi; b >= lo; b--) {
+    if (b != hi) {
+      const int t = other(acc);
+      rns::stage<rns::OP_F12_SQR>(e, L, acc, 0, t);
+      acc = other(t);
+      rns::stage<rns::OP_F12_MUL>(e, L, t, V + 12 * v++, acc);
     }
     if ((params::BLS_X >> b) & 1) {
-      fetch(idx + 1, in_r);
-      rns::stage<rns::OP_F12_MUL>(e, L, acc, in_r, tmp);
-      const int t = acc;
-      acc = tmp;
-      tmp = t;
+      const int t = other(acc);
+      rns::stage<rns::OP_F12_MUL>(e, L, acc, V + 12 * v++, t);
+      acc = t;
     }
   }
   rns::store_res(e, acc, MBr + (g0 * NBLK + blk) * rns::RES_WORDS, MBr + (g1 * NBLK + blk) * rns::RES_WORDS, 12);
@@ -763,11 +886,11 @@ static hipError_t pairing_from_lines(Arena& ar, hipStream_t s, Fq12* lines, size
     while (n > 1) {
       const size_t nout = (n + TREE_CHUNK - 1) / TREE_CHUNK;
       uint32_t* nxt = ar.take<uint32_t>(G * nout * rns::RES_WORDS);
-      const unsigned wg = (unsigned)((G * nout + 1) / 2);
+      const unsigned wg = rns_grid((G * nout + 1) / 2);
       if (res)
-        k_chunk_prod_rns<true><<<wg, 64 * RC_WAVES, 0, s>>>(cur, G, n, nout, nxt, TREE_CHUNK);
+        k_chunk_prod_rns<true, TREE_CHUNK><<<wg, 64 * RC_WAVES, 0, s>>>(cur, G, n, nout, nxt);
       else
-        k_chunk_prod_rns<false><<<wg, 64 * RC_WAVES, 0, s>>>(cur, G, n, nout, nxt, TREE_CHUNK);
+        k_chunk_prod_rns<false, TREE_CHUNK><<<wg, 64 * RC_WAVES, 0, s>>>(cur, G, n, nout, nxt);
       TPST_TRY(hipGetLastError());
       cur = nxt;
       res = true;
@@ -861,11 +984,13 @@ hipError_t gt_product_final(Arena& ar, hipStream_t s, const Fq12* d_partials, si
 hipError_t multi_pairing(Arena& ar, hipStream_t s, const uint32_t* d_g1, const uint32_t* d_g2, size_t groups,
                          size_t n, Fq12* d_out) {
   const size_t np = groups * n;
-  size_t need = Arena::need(np * N_LINE_COEFFS, sizeof(LineCoeff)) + multi_pairing_scratch(groups, n) + 4096;
+  size_t need = Arena::need(np * N_LINE_COEFFS, sizeof(LineCoeff)) + multi_pairing_scratch(groups, n) +
+                Arena::need(g2_prepare_scratch(np), 1) + 4096;
   ar.reset();
   TPST_TRY(ar.reserve(need));
   LineCoeff* coeffs = ar.take<LineCoeff>(np * N_LINE_COEFFS);
-  TPST_TRY(g2_prepare_batch(s, d_g2, np, coeffs));
+  uint32_t* prep = ar.take<uint32_t>(g2_prepare_scratch(np) / sizeof(uint32_t));
+  TPST_TRY(g2_prepare_batch(s, d_g2, np, coeffs, prep));
   return multi_pairing_prepared(ar, s, d_g1, d_g2, coeffs, groups, n, d_out);
 }
 
@@ -1128,17 +1253,177 @@ __global__ void __launch_bounds__(64 * TP_WAVES) k_gt_table_prod(const Fq12* __r
   wave::store_f12(vals, reg(r), G + tp.out[b] + i);
 }
 
+// ---- the same combination on the RNS engine ---------------------------------
+// Tables and partial products stay in RNS form (rns::RES_WORDS u32 per Fq12):
+//   k_gt_sq_table_rns   blocks 0, 1: two bases each (the two halves), 63
+//                       cyclotomic squarings, every power stored; block 2
+//                       converts the plain copies (A0 A3 B0 B3) into G
+//   k_gt_tab_prod1_rns  (base, digit, byte j): product of the 8 selected
+//                       powers 8j .. 8j+7 (ones where the digit bit is 0)
+//   k_gt_tab_prod2_rns  (base, digit): product of its 8 partials, then
+//                       frob^digit -- both halves share the digit index, so
+//                       they share the Frobenius stages
+//   k_gt_final_rns      t_l, t_r = product of the 10 factors of each group,
+//                       back to field.h Montgomery form
+// about 25 stages on the critical path after the challenge, against the
+// radix engine's ~17 slower stages and its table conversions.
+#ifndef TPST_GT_RNS
+#define TPST_GT_RNS 1
+#endif
+static bool gt_rns() {
+  static const bool on = [] {
+    const char* v = getenv("TPST_GT_RNS");
+    return v ? atoi(v) != 0 : TPST_GT_RNS != 0;
+  }();
+  return on;
+}
+
+__global__ void __launch_bounds__(64 * RC_WAVES) k_gt_sq_table_rns(const Fq12* __restrict__ src, SqPlan sp,
+                                                                   uint32_t* __restrict__ tab, CopyPlan cp,
+                                                                   uint32_t* __restrict__ G) {
+  __shared__ uint32_t s_slots[(rns::N_CONSTS + 24) * rns::SLOT];
+  __shared__ uint32_t s_xch[RC_WAVES * rns::XCH];
+  rns::load_consts((rns::lds_t*)s_slots);
+  const rns::Lane L = rns::load_lane();
+  const rns::Eng e{(rns::lds_t*)s_slots, (rns::lds_t*)s_xch + rns::wave_id() * rns::XCH, 0};
+  __syncthreads();
+  int cur = rns::N_CONSTS, nxt = cur + 12;
+  if (blockIdx.x < 2) {
+    const int b0 = 2 * blockIdx.x, b1 = b0 + 1;
+    rns::load(e, L, reinterpret_cast<const Fq*>(src + sp.sel[b0]), reinterpret_cast<const Fq*>(src + sp.sel[b1]),
+              cur, 12);
+    for (int k = 0; k < 64; k++) {
+      rns::store_res(e, cur, tab + (size_t)(b0 * 64 + k) * rns::RES_WORDS,
+                     tab + (size_t)(b1 * 64 + k) * rns::RES_WORDS, 12);
+      if (k == 63) break;
+      rns::stage<rns::OP_CYC_SQR>(e, L, cur, 0, nxt);
+      const int t = cur;
+      cur = nxt;
+      nxt = t;
+    }
+    return;
+  }
+  for (int j = 0; j < cp.n; j += 2) {
+    const int j1 = j + 1 < cp.n ? j + 1 : j;
+    rns::load(e, L, reinterpret_cast<const Fq*>(src + cp.src[j]), reinterpret_cast<const Fq*>(src + cp.src[j1]),
+              cur, 12);
+    rns::store_res(e, cur, G + (size_t)cp.dst[j] * rns::RES_WORDS, G + (size_t)cp.dst[j1] * rns::RES_WORDS, 12);
+    __syncthreads();
+  }
+}
+
+// product of CH factors already fetched into slots X + 12 i; returns the slot
+template <int CH>
+__device__ int rns_product(const rns::Eng& e, const rns::Lane& L, int X, int W) {
+  int acc = X, tmp = W;
+#pragma unroll
+  for (int i = 1; i < CH; i++) {
+    rns::stage<rns::OP_F12_MUL>(e, L, acc, X + 12 * i, tmp);
+    acc = tmp;
+    tmp = tmp == W ? W + 12 : W;
+  }
+  return acc;
+}
+
+__global__ void __launch_bounds__(64 * RC_WAVES) k_gt_tab_prod1_rns(const uint32_t* __restrict__ tab,
+                                                                    const uint64_t* __restrict__ digits, TpPlan tp,
+                                                                    uint32_t* __restrict__ L1) {
+  __shared__ uint32_t s_slots[(rns::N_CONSTS + 12 * 10) * rns::SLOT];
+  __shared__ uint32_t s_xch[RC_WAVES * rns::XCH];
+  rns::load_consts((rns::lds_t*)s_slots);
+  const rns::Lane L = rns::load_lane();
+  const rns::Eng e{(rns::lds_t*)s_slots, (rns::lds_t*)s_xch + rns::wave_id() * rns::XCH, 0};
+  const int w = rns::wave_id(), lane = threadIdx.x & 63;
+  const int q = 2 * blockIdx.x + (lane >> 5);  // (base, digit, byte) = (q / 32, q / 8 % 4, q % 8)
+  const int b = q >> 5, i = (q >> 3) & 3, j = q & 7;
+  const uint64_t ei = digits[4 * tp.dig[b] + i];
+  const uint32_t one = w == 0 ? e.slots[e.kon * rns::SLOT + lane] : 0u;
+  uint32_t v[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const int bit = 8 * j + k;
+    v[k] = ((ei >> bit) & 1) ? tab[(size_t)(b * 64 + bit) * rns::RES_WORDS + w * 32 + (lane & 31)] : one;
+  }
+  const int X = rns::N_CONSTS;
+#pragma unroll
+  for (int k = 0; k < 8; k++) e.slots[(X + 12 * k + w) * rns::SLOT + lane] = v[k];
+  __syncthreads();
+  const int r = rns_product<8>(e, L, X, X + 96);
+  rns::store_res(e, r, L1 + (size_t)(2 * blockIdx.x) * rns::RES_WORDS, L1 + (size_t)(2 * blockIdx.x + 1) * rns::RES_WORDS,
+                 12);
+}
+
+__global__ void __launch_bounds__(64 * RC_WAVES) k_gt_tab_prod2_rns(const uint32_t* __restrict__ L1, TpPlan tp,
+                                                                    uint32_t* __restrict__ G) {
+  __shared__ uint32_t s_slots[(rns::N_CONSTS + 12 * 10) * rns::SLOT];
+  __shared__ uint32_t s_xch[RC_WAVES * rns::XCH];
+  rns::load_consts((rns::lds_t*)s_slots);
+  const rns::Lane L = rns::load_lane();
+  const rns::Eng e{(rns::lds_t*)s_slots, (rns::lds_t*)s_xch + rns::wave_id() * rns::XCH, 0};
+  const int w = rns::wave_id(), lane = threadIdx.x & 63;
+  const int i = blockIdx.x >> 1, b = 2 * (blockIdx.x & 1) + (lane >> 5);  // both halves: digit i
+  const int X = rns::N_CONSTS;
+#pragma unroll
+  for (int j = 0; j < 8; j++)
+    e.slots[(X + 12 * j + w) * rns::SLOT + lane] = L1[(size_t)((b * 4 + i) * 8 + j) * rns::RES_WORDS + w * 32 + (lane & 31)];
+  __syncthreads();
+  int r = rns_product<8>(e, L, X, X + 96);
+  const int o = r == X + 96 ? X + 108 : X + 96;
+  if (i == 1) {
+    rns::stage<rns::OP_FROB1>(e, L, r, 0, o);
+    r = o;
+  } else if (i == 2) {
+    rns::stage<rns::OP_FROB2>(e, L, r, 0, o);
+    r = o;
+  } else if (i == 3) {
+    rns::stage<rns::OP_FROB3>(e, L, r, 0, o);
+    r = o;
+  }
+  const int b0 = 2 * (blockIdx.x & 1);
+  rns::store_res(e, r, G + (size_t)(tp.out[b0] + i) * rns::RES_WORDS, G + (size_t)(tp.out[b0 + 1] + i) * rns::RES_WORDS,
+                 12);
+}
+
+__global__ void __launch_bounds__(64 * RC_WAVES) k_gt_final_rns(const uint32_t* __restrict__ G, Fq12* __restrict__ out2) {
+  __shared__ uint32_t s_slots[(rns::N_CONSTS + 12 * 12) * rns::SLOT];
+  __shared__ uint32_t s_xch[RC_WAVES * rns::XCH];
+  rns::load_consts((rns::lds_t*)s_slots);
+  const rns::Lane L = rns::load_lane();
+  const rns::Eng e{(rns::lds_t*)s_slots, (rns::lds_t*)s_xch + rns::wave_id() * rns::XCH, 0};
+  const int w = rns::wave_id(), lane = threadIdx.x & 63, h = lane >> 5;
+  const int X = rns::N_CONSTS;
+#pragma unroll
+  for (int f = 0; f < 10; f++)
+    e.slots[(X + 12 * f + w) * rns::SLOT + lane] = G[(size_t)(10 * h + f) * rns::RES_WORDS + w * 32 + (lane & 31)];
+  __syncthreads();
+  const int r = rns_product<10>(e, L, X, X + 120);
+  rns::store(e, L, r, reinterpret_cast<Fq*>(out2), reinterpret_cast<Fq*>(out2 + 1), 12);
+}
+
 hipError_t mipp_sq_tables(hipStream_t s, const Fq12* d_la8, Fq12* d_tab, Fq12* d_G) {
   // tables of A1 A2 B1 B2; A0 A3 / B0 B3 into slots 0, 1 of the two product lists
   const SqPlan sp{4, {2, 3, 6, 7}};
   const CopyPlan cp{4, {0, 1, 4, 5}, {0, 1, 10, 11}};
-  k_gt_sq_table<<<5, 64, SQ_LDS, s>>>(d_la8, sp, d_tab, cp, d_G);
+  if (gt_rns())
+    k_gt_sq_table_rns<<<3, 64 * RC_WAVES, 0, s>>>(d_la8, sp, reinterpret_cast<uint32_t*>(d_tab), cp,
+                                                  reinterpret_cast<uint32_t*>(d_G));
+  else
+    k_gt_sq_table<<<5, 64, SQ_LDS, s>>>(d_la8, sp, d_tab, cp, d_G);
   return hipGetLastError();
 }
 
 hipError_t mipp_combine_tab(hipStream_t s, const Fq12* d_tab, const uint64_t* d_digits, Fq12* d_G, Fq12* d_mid,
                             Fq12* d_out2) {
   const TpPlan tp{4, {0, 1, 2, 3}, {2, 6, 12, 16}};
+  if (gt_rns()) {
+    uint32_t* L1 = reinterpret_cast<uint32_t*>(d_mid);  // 128 partials
+    k_gt_tab_prod1_rns<<<64, 64 * RC_WAVES, 0, s>>>(reinterpret_cast<const uint32_t*>(d_tab), d_digits, tp, L1);
+    TPST_TRY(hipGetLastError());
+    k_gt_tab_prod2_rns<<<8, 64 * RC_WAVES, 0, s>>>(L1, tp, reinterpret_cast<uint32_t*>(d_G));
+    TPST_TRY(hipGetLastError());
+    k_gt_final_rns<<<1, 64 * RC_WAVES, 0, s>>>(reinterpret_cast<const uint32_t*>(d_G), d_out2);
+    return hipGetLastError();
+  }
   k_gt_table_prod<<<16, 64 * TP_WAVES, TP_LDS, s>>>(d_tab, d_digits, tp, d_G);
   TPST_TRY(hipGetLastError());
   // 2 groups x 10 factors -> 3 partials (chunk 4) -> 1

@@ -10,7 +10,11 @@ namespace tpst {
 // G2Prepared for n points: coeffs laid out coefficient-major,
 // d_coeffs[idx * n + i] (idx < 69).  Infinity points get no use (the Miller
 // kernel skips pairs whose G1 or G2 point is infinity).
-hipError_t g2_prepare_batch(hipStream_t s, const uint32_t* d_g2, size_t n, LineCoeff* d_coeffs);
+// scratch: g2_prepare_scratch(n) bytes for the RNS engine's residue lines
+// (nullptr: the radix engine)
+size_t g2_prepare_scratch(size_t n);
+hipError_t g2_prepare_batch(hipStream_t s, const uint32_t* d_g2, size_t n, LineCoeff* d_coeffs,
+                            uint32_t* scratch = nullptr);
 
 // groups x n pairs -> groups GT elements (after final exponentiation).
 // d_g1: groups*n affine G1 (Montgomery); d_coeffs: prepared G2 of the same
@@ -65,6 +69,9 @@ hipError_t mipp_combine(hipStream_t s, Fq12* d_la8, const uint64_t* d_digits, Fq
 // Fq12 product lists, A0 A3 / B0 B3 copied in), then once c is known
 // mipp_combine_tab (d_mid: 2 x 3 Fq12 scratch) -> d_out2 = (t_l, t_r)
 hipError_t mipp_sq_tables(hipStream_t s, const Fq12* d_la8, Fq12* d_tab, Fq12* d_G);
+// bytes per table / partial entry of either engine (d_tab: 4 x 64, d_G: 2 x 10,
+// d_mid: 128 entries of this size; the RNS engine keeps them in residue form)
+constexpr size_t MIPP_TAB_F12_BYTES = 12 * 32 * 4;
 hipError_t mipp_combine_tab(hipStream_t s, const Fq12* d_tab, const uint64_t* d_digits, Fq12* d_G, Fq12* d_mid,
                             Fq12* d_out2);
 

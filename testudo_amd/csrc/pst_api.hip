@@ -9,6 +9,9 @@
 #include <cstring>
 #include <memory>
 #include <vector>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 
 #include "../../include/tpst.h"
 #include "ctx.h"
@@ -42,6 +45,15 @@ Fr fr_canon(const uint64_t* c) {
 void fr_out(const Fr& a, uint64_t* c) {
   Fr r = from_mont(a);
   memcpy(c, r.v, 32);
+}
+
+// TPST_OPEN_TRACE=1: per-round host timings of tpst_poly_open on stderr
+static double host_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static bool open_trace() {
+  static const bool on = getenv("TPST_OPEN_TRACE") != nullptr;
+  return on;
 }
 
 // 64-bit-limb host Montgomery product (CIOS, unsigned __int128) on the same
@@ -395,6 +407,7 @@ struct SrsState {
   DevBuf gmask, hmask;
   BatchTables tables;             // K1 tables over powers_of_g[0]
   DevBuf hprep[2];                // G2Prepared of powers_of_h[odd], odd = 0/1
+  DevBuf prep_scratch;            // residue lines of the RNS G2 preparation (g2_prepare_scratch)
   // fixed-base tables (fbt.h), built on first open
   DevBuf t_pg0;                   // powers_of_g[0]            (U = commit(q))
   DevBuf t_h[2];                  // powers_of_h[odd]           (MIPP h folds)
@@ -482,10 +495,11 @@ static int srs_install(tpst_ctx* ctx, int nv, const uint64_t* flat) {
   TPST_HIP(ctx, take(st->hmask, nv, 48));
   const size_t N = (size_t)1 << nv;
   TPST_HIP(ctx, batch_tables_build(s, st->pg[0]->u(), N, batch_window_bits(N), st->tables));
+  TPST_HIP(ctx, st->prep_scratch.alloc(g2_prepare_scratch((size_t)1 << nv)));
   for (int odd = 0; odd < 2 && odd < nv; odd++) {
     const size_t m = (size_t)1 << (nv - odd);
     TPST_HIP(ctx, st->hprep[odd].alloc(m * N_LINE_COEFFS * sizeof(LineCoeff)));
-    TPST_HIP(ctx, g2_prepare_batch(s, st->ph[odd]->u(), m, (LineCoeff*)st->hprep[odd].p));
+    TPST_HIP(ctx, g2_prepare_batch(s, st->ph[odd]->u(), m, (LineCoeff*)st->hprep[odd].p, st->prep_scratch.u()));
   }
   // fixed-base tables of the opening (a function of the key only, like the
   // cached G2Prepared above): built here so that no open pays for them
@@ -1022,7 +1036,7 @@ static int commit_rows_partial(tpst_ctx* ctx, tpst_poly* p, size_t r0, size_t r1
   ctx->arena.reset();
   TPST_HIP(ctx, ctx->arena.reserve(need));
   LineCoeff* lc = ctx->arena.take<LineCoeff>(R * N_LINE_COEFFS);
-  TPST_HIP(ctx, g2_prepare_batch(s, h, R, lc));
+  TPST_HIP(ctx, g2_prepare_batch(s, h, R, lc, st->prep_scratch.u()));
   TPST_HIP(ctx, multi_pairing_prepared(ctx->arena, s, cm.u(), h, lc, 1, R, (Fq12*)tt.p, false));
   TPST_HIP(ctx, affine_from_mont<Fq>(s, cm.u(), out.u(), R));
   TPST_HIP(ctx, fq12_from_mont(s, (Fq12*)tt.p, out.u() + 24 * R, 1));
@@ -1447,10 +1461,11 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     TPST_HIP(ctx, ScD[i].alloc(8 * C * 32));
     TPST_HIP(ctx, xl[i].alloc(C * sizeof(Xyzz<Fq>)));
     TPST_HIP(ctx, LAo[i].alloc(8 * sizeof(Fq12)));
-    TPST_HIP(ctx, SqT[i].alloc(4 * 64 * sizeof(Fq12)));
-    TPST_HIP(ctx, SqG[i].alloc(2 * 10 * sizeof(Fq12)));
+    // sized for either engine (RNS form: rns::RES_WORDS u32 per Fq12)
+    TPST_HIP(ctx, SqT[i].alloc(4 * 64 * MIPP_TAB_F12_BYTES));
+    TPST_HIP(ctx, SqG[i].alloc(2 * 10 * MIPP_TAB_F12_BYTES));
   }
-  TPST_HIP(ctx, SqM.alloc(2 * 3 * sizeof(Fq12)));
+  TPST_HIP(ctx, SqM.alloc(128 * MIPP_TAB_F12_BYTES));
   TPST_HIP(ctx, canA.alloc(2 * 576));
   TPST_HIP(ctx, canB.alloc(2 * 96));
   TPST_HIP(ctx, canC.alloc((size_t)(m + 1) * 192));
@@ -1643,7 +1658,8 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
       g.D = 1;
       TPST_HIP(ctx, fbt_msm<Fq2>(arC, sC, tH, ScC.u(), g, (Xyzz<Fq2>*)xh.p));
       TPST_HIP(ctx, xyzz_to_affine_mont<Fq2>(sC, (Xyzz<Fq2>*)xh.p, Hb[(r >> 1) & 1].u(), len));
-      TPST_HIP(ctx, g2_prepare_batch(sC, Hb[(r >> 1) & 1].u(), len, (LineCoeff*)Lb[(r >> 1) & 1].p));
+      TPST_HIP(ctx, g2_prepare_batch(sC, Hb[(r >> 1) & 1].u(), len, (LineCoeff*)Lb[(r >> 1) & 1].p,
+                                     st->prep_scratch.u()));
       TPST_HIP(ctx, hipEventRecord(ev_c(r), sC));
     }
 
@@ -1659,7 +1675,9 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     // comms_u (stream B) is ready well before comms_t (the final
     // exponentiations): absorb it while stream A finishes (mipp.rs:97-100
     // order: u_l, u_r, t_l, t_r)
+    const double h0 = host_us();
     TPST_HIP(ctx, hipEventSynchronize(ev_b(r)));
+    const double h1 = host_us();
     memcpy(proof->comms_u[r][0], dn_r, 96);
     memcpy(proof->comms_u[r][1], dn_r + 96, 96);
     uint8_t b[96];
@@ -1667,7 +1685,9 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     sp.absorb_bytes(b, 96);
     g1_bytes(proof->comms_u[r][1], b);
     sp.absorb_bytes(b, 96);
+    const double h2 = host_us();
     TPST_HIP(ctx, hipEventSynchronize(ev_a(r)));
+    const double h3 = host_us();
     memcpy(proof->comms_t[r][0], dn_r + 192, 576);
     memcpy(proof->comms_t[r][1], dn_r + 192 + 576, 576);
     sp.absorb_bytes((const uint8_t*)proof->comms_t[r][0], 576);
@@ -1676,6 +1696,9 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     sp.challenge(ci_c);  // mipp.rs:101
     const Fr c_inv = fr_canon(ci_c);
     const Fr c = fr_inv(c_inv);  // mipp.rs:106
+    if (open_trace())
+      fprintf(stderr, "open round %d: wait_u %.0f absorb_u %.0f wait_t %.0f absorb_t+challenge %.0f us\n", r, h1 - h0,
+              h2 - h1, h3 - h2, host_us() - h3);
     xs_inv.push_back(c_inv);
     cprev = c_inv;
     cprev_c = c;

@@ -182,13 +182,17 @@ __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane
 
 // C/D = OP(A, B): wave w < OP_NO evaluates output coefficient w of both chains;
 // the destination registers must not overlap the inputs
-template <int OP>
+// INPLACE: outputs may overwrite inputs (the G2 region ops, a == c): every
+// wave finishes its reads before any wave writes
+template <int OP, bool INPLACE = false>
 __device__ __forceinline__ void stage(const Eng& e, const Lane& L, int a, int b, int c, int d = 0) {
   const int w = wave_id(), lane = threadIdx.x & 63;
+  int dst = 0;
+  uint64_t acc = 0;
+  if (w < OP_NO[OP])
+    acc = terms<OP>(w, L, e.slots + a * SLOT + lane, e.slots + b * SLOT + lane, e.slots + e.kon * SLOT + lane, dst);
+  if (INPLACE) __syncthreads();
   if (w < OP_NO[OP]) {
-    int dst;
-    const uint64_t acc = terms<OP>(w, L, e.slots + a * SLOT + lane, e.slots + b * SLOT + lane,
-                                   e.slots + e.kon * SLOT + lane, dst);
     const uint32_t r = mont(e, L, red64(acc, L));
     e.slots[(((dst >> 8) ? d : c) + (dst & 0xff)) * SLOT + lane] = r;
   }
@@ -261,59 +265,64 @@ __device__ __forceinline__ void reduce16p(uint32_t (&r)[12]) {
   }
 }
 
-// dst_h[0 .. n) <- slots a .. a+n-1: M-domain to field.h Montgomery form,
-// canonical (< p), through CRT over base B
-__device__ __forceinline__ void store(const Eng& e, const Lane& L, int a, Fq* dst0, Fq* dst1, int n) {
-  const int w = wave_id(), lane = threadIdx.x & 63, hb = lane & 32, ch = lane & 31;
-  if (w < n) {
-    const uint32_t x = e.slots[(a + w) * SLOT + lane];
-    const uint32_t kout = e.slots[(e.kon + K_OUT) * SLOT + lane];
-    const uint32_t r = mont(e, L, red64((uint64_t)x * kout, L));  // x R M^-1... = value * R (< 16 p)
-    // r = sum_i xi_i M_i - alpha M, xi_i = r_i M_i^-1 mod m_i
-    e.xch[lane] = red64((uint64_t)r * L.k5, L);
-    wave_sync();
-    uint32_t xs[NB];
-    read15(e.xch + hb, xs);
-    uint64_t acc = 0;
+// this wave's two values (one per half, residue x of lane) from the M-domain
+// to field.h Montgomery form, canonical (< p), through CRT over base B;
+// lane 0 of each half writes its half's dst (no workgroup barrier)
+__device__ __forceinline__ void to_fq_wave(const Eng& e, const Lane& L, uint32_t x, Fq* dst0, Fq* dst1) {
+  const int lane = threadIdx.x & 63, hb = lane & 32, ch = lane & 31;
+  const uint32_t kout = e.slots[(e.kon + K_OUT) * SLOT + lane];
+  const uint32_t r = mont(e, L, red64((uint64_t)x * kout, L));  // value R, < 16 p
+  // r = sum_i xi_i M_i - alpha M, xi_i = r_i M_i^-1 mod m_i
+  e.xch[lane] = red64((uint64_t)r * L.k5, L);
+  wave_sync();
+  uint32_t xs[NB];
+  read15(e.xch + hb, xs);
+  uint64_t acc = 0;
 #pragma unroll
-    for (int i = 0; i < NB; i++) acc += (uint64_t)xs[i] * L.row1[i];
-    if (ch == R_CH) e.xch[128 + (hb >> 5)] = ((uint32_t)acc - r) * L.minv;  // alpha
-    if (ch < 14) {  // column ch of sum_i xi_i M_i
-      uint64_t col = 0;
+  for (int i = 0; i < NB; i++) acc += (uint64_t)xs[i] * L.row1[i];
+  if (ch == R_CH) e.xch[128 + (hb >> 5)] = ((uint32_t)acc - r) * L.minv;  // alpha
+  if (ch < 14) {  // column ch of sum_i xi_i M_i
+    uint64_t col = 0;
 #pragma unroll
-      for (int i = 0; i < NB; i++) col += (uint64_t)xs[i] * MI_LIMBS[i][ch];
-      e.xch[64 + hb + 2 * ch] = (uint32_t)col;
-      e.xch[64 + hb + 2 * ch + 1] = (uint32_t)(col >> 32);
-    }
-    wave_sync();
-    if (ch == 0) {
-      const uint32_t alpha = e.xch[128 + (hb >> 5)];
-      uint32_t s[15];
-      uint64_t cy = 0;
-#pragma unroll
-      for (int k = 0; k < 14; k++) {
-        cy += (uint64_t)e.xch[64 + hb + 2 * k] | ((uint64_t)e.xch[64 + hb + 2 * k + 1] << 32);
-        s[k] = (uint32_t)cy;
-        cy >>= 32;
-      }
-      s[14] = (uint32_t)cy;
-      uint32_t v[12];
-      uint64_t cm = 0;
-      int64_t br = 0;
-#pragma unroll
-      for (int k = 0; k < 14; k++) {
-        const uint64_t am = (uint64_t)alpha * M_LIMBS[k] + cm;
-        cm = am >> 32;
-        const int64_t t = (int64_t)s[k] - (int64_t)(uint32_t)am + br;
-        if (k < 12) v[k] = (uint32_t)t;
-        br = t >> 32;
-      }
-      reduce16p(v);
-      Fq* d = (hb ? dst1 : dst0) + w;
-#pragma unroll
-      for (int k = 0; k < 12; k++) d->v[k] = v[k];
-    }
+    for (int i = 0; i < NB; i++) col += (uint64_t)xs[i] * MI_LIMBS[i][ch];
+    e.xch[64 + hb + 2 * ch] = (uint32_t)col;
+    e.xch[64 + hb + 2 * ch + 1] = (uint32_t)(col >> 32);
   }
+  wave_sync();
+  if (ch == 0) {
+    const uint32_t alpha = e.xch[128 + (hb >> 5)];
+    uint32_t s[15];
+    uint64_t cy = 0;
+#pragma unroll
+    for (int k = 0; k < 14; k++) {
+      cy += (uint64_t)e.xch[64 + hb + 2 * k] | ((uint64_t)e.xch[64 + hb + 2 * k + 1] << 32);
+      s[k] = (uint32_t)cy;
+      cy >>= 32;
+    }
+    s[14] = (uint32_t)cy;
+    uint32_t v[12];
+    uint64_t cm = 0;
+    int64_t br = 0;
+#pragma unroll
+    for (int k = 0; k < 14; k++) {
+      const uint64_t am = (uint64_t)alpha * M_LIMBS[k] + cm;
+      cm = am >> 32;
+      const int64_t t = (int64_t)s[k] - (int64_t)(uint32_t)am + br;
+      if (k < 12) v[k] = (uint32_t)t;
+      br = t >> 32;
+    }
+    reduce16p(v);
+    Fq* d = hb ? dst1 : dst0;
+#pragma unroll
+    for (int k = 0; k < 12; k++) d->v[k] = v[k];
+  }
+  wave_sync();  // the exchange words are reused by the next call
+}
+
+// dst_h[0 .. n) <- slots a .. a+n-1: M-domain to field.h Montgomery form
+__device__ __forceinline__ void store(const Eng& e, const Lane& L, int a, Fq* dst0, Fq* dst1, int n) {
+  const int w = wave_id(), lane = threadIdx.x & 63;
+  if (w < n) to_fq_wave(e, L, e.slots[(a + w) * SLOT + lane], dst0 + w, dst1 + w);
   __syncthreads();
 }
 

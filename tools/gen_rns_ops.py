@@ -303,7 +303,17 @@ def enc(a, b, c, neg):
 
 
 OPS = ["F12_MUL", "F12_SQR", "CYC_SQR", "FROB1", "FROB2", "FROB3", "CONJ", "COPY",
-       "INV1", "INV2", "INV3", "INV4", "INV5", "INV6", "INV7"]
+       "INV1", "INV2", "INV3", "INV4", "INV5", "INV6", "INV7",
+       "G2_DBL1", "G2_DBL2", "G2_DBL3", "G2_DBL4", "G2_ADD1", "G2_ADD2", "G2_ADD3", "G2_ADD4"]
+
+
+def rw_overlap(progs, name):
+    """1 if an output slot of the op is also one of its A inputs (the G2
+    region ops run in place, a == c): the stage must then finish every
+    wave's reads before any wave writes"""
+    reads = {t[k][1] for _, terms in progs[name] for t in terms for k in (0, 1) if t[k][0] == "A"}
+    outs = {dst & 0xff for dst, _ in progs[name] if dst >> 8 == 0}
+    return int(bool(reads & outs))
 
 
 def build_ops():
@@ -370,7 +380,7 @@ def check_all():
             maxw = max(maxw, bound_check(terms))
     for name in OPS:
         pg, outs = built[name]
-        A, B = W.rnd(16), W.rnd(16)
+        A, B = W.rnd(48), W.rnd(48)
         if name == "CYC_SQR":
             f = W.t2p(A[:12])
             r = O.f12_mul(O.f12_conj(f), O.f12_inv(f))
@@ -386,6 +396,33 @@ def check_all():
                 x = crt(r)
                 assert x < N1, (name, k, x // P)
                 assert x % P == v * MB % P, (name, d, k)
+    # the whole G2Prepared chain (pairing.h g2_double_step / g2_add_step) in
+    # place on one 44-slot region, as k_g2_prepare_rns runs it
+    q = O.g2_mul(O.G2_GEN, 0x1234567)
+    ref = O.g2_prepare(q)
+    vals = {i: 0 for i in range(44)}
+    vals[0], vals[1] = q[0]
+    vals[2], vals[3] = q[1]
+    vals[4], vals[5] = 1, 0
+    vals[26], vals[27] = q[0]
+    vals[28], vals[29] = q[1]
+    reg = [residues(to_m(vals[i])) for i in range(44)]
+    idx = 0
+    for bit in bin(O.X)[3:]:
+        steps = ["G2_DBL1", "G2_DBL2", "G2_DBL3", "G2_DBL4"]
+        if bit == "1":
+            steps += ["G2_ADD1", "G2_ADD2", "G2_ADD3", "G2_ADD4"]
+        for st in steps:
+            out = run_op(rp, progs[st], {"A": reg, "B": reg, "K": kres}, None)
+            for dst, r in out.items():
+                reg[dst & 0xff] = r
+            if st in ("G2_DBL4", "G2_ADD4"):
+                got = [crt(reg[6 + j]) % P * pow(MB, -1, P) % P for j in range(6)]
+                c0, c1, c2 = ref[idx]
+                assert tuple(got) == (*c0, *c1, *c2), (st, idx)
+                assert all(crt(reg[i]) < N1 for i in range(44))
+                idx += 1
+    assert idx == len(ref)
     # conversions: std Montgomery (v R mod p, < p) -> M-domain and back
     kin = rp.const(MB * pow(RQ, -1, P) % P)                           # k M = M^2 / R
     kout = rp.const(RQ * pow(MB, -1, P) % P)                          # k M = R
@@ -468,6 +505,8 @@ def render():
     lines.append("static constexpr int OP_OFF[N_OPS] = {%s};" % ", ".join(map(str, offs)))
     lines.append("static constexpr int OP_NO[N_OPS] = {%s};" % ", ".join(str(blob[o] & 0xff) for o in offs))
     lines.append("static constexpr int OP_NT[N_OPS] = {%s};" % ", ".join(str(blob[o] >> 8) for o in offs))
+    lines.append("static constexpr int OP_RW[N_OPS] = {%s};  // outputs overlap A inputs (in place)" % (
+        ", ".join(str(rw_overlap(progs, n)) for n in OPS)))
     lines.append("// term word: idx_a | kind_a << 8 | idx_b << 10 | kind_b << 18 | neg_b << 20 | c << 24 "
                  "(kinds A 0, B 1, K 2); per output [dst (D << 8 | k), terms...]")
     lines.append("static constexpr uint32_t PROG[%d] = {%s};" % (len(blob), ", ".join("0x%08xu" % t for t in blob)))
