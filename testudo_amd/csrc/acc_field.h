@@ -3,7 +3,8 @@
 // 66.7 vs 48.3 G products/s chip-wide, 0.91 vs 1.65 us lone-wave latency,
 // tools/mb_fq29.py).  Points and XYZZ values stay in memory in field.h's
 // layout (arkworks' Montgomery bytes); AccField<F>::in / out convert them as
-// a kernel loads and stores them.  G2 (Fq2) computes in its own field.
+// a kernel loads and stores them.  G2 (Fq2) accumulates in Fq2 over the same
+// radix-2^29 Fq (Fq2x29).
 // TPST_ACC29=0 selects field.h everywhere (A/B builds).
 #pragma once
 #include "curve.h"
@@ -17,11 +18,44 @@ struct Words<Fq29> {
   static constexpr int n = 13;
 };
 
+// Fq2 = Fq[u]/(u^2 + 5) over field29.h's Fq: the G2 accumulation field
+// (the opening's h folds, the G2 MSMs), same formulas as field.h's Fq2
+struct Fq2x29 {
+  Fq29 c0, c1;
+  static TPST_HD Fq2x29 zero() { return {Fq29::zero(), Fq29::zero()}; }
+  static TPST_HD Fq2x29 one() { return {Fq29::one(), Fq29::zero()}; }
+};
+template <>
+struct Words<Fq2x29> {
+  static constexpr int n = 26;
+};
+TPST_HD bool is_zero(const Fq2x29& a) { return is_zero(a.c0) && is_zero(a.c1); }
+TPST_HD bool eq(const Fq2x29& a, const Fq2x29& b) { return eq(a.c0, b.c0) && eq(a.c1, b.c1); }
+TPST_HD Fq2x29 add(const Fq2x29& a, const Fq2x29& b) { return {add(a.c0, b.c0), add(a.c1, b.c1)}; }
+TPST_HD Fq2x29 sub(const Fq2x29& a, const Fq2x29& b) { return {sub(a.c0, b.c0), sub(a.c1, b.c1)}; }
+TPST_HD Fq2x29 dbl(const Fq2x29& a) { return {dbl(a.c0), dbl(a.c1)}; }
+TPST_HD Fq2x29 neg(const Fq2x29& a) { return {neg(a.c0), neg(a.c1)}; }
+TPST_HD Fq2x29 mul3(const Fq2x29& a) { return {mul3(a.c0), mul3(a.c1)}; }
+TPST_HD Fq29 mul5(const Fq29& a) { return add(dbl(dbl(a)), a); }
+TPST_FQ2_ATTR Fq2x29 mul(const Fq2x29& a, const Fq2x29& b) {
+  const Fq29 v0 = mul(a.c0, b.c0);
+  const Fq29 v1 = mul(a.c1, b.c1);
+  const Fq29 s = mul(add(a.c0, a.c1), add(b.c0, b.c1));
+  return {sub(v0, mul5(v1)), sub(sub(s, v0), v1)};
+}
+TPST_FQ2_ATTR Fq2x29 sqr(const Fq2x29& a) {
+  const Fq29 v0 = mul(a.c0, a.c1);
+  const Fq29 t = mul(add(a.c0, a.c1), sub(a.c0, mul5(a.c1)));
+  return {add(t, dbl(dbl(v0))), dbl(v0)};
+}
+TPST_HD Fq2x29 from_std(const Fq2& a) { return {from_std(a.c0), from_std(a.c1)}; }
+TPST_HD Fq2 to_std(const Fq2x29& a) { return {to_std(a.c0), to_std(a.c1)}; }
+
 // Compute field of the G1 bucket accumulation: the radix-2^29 Fq of
 // field29.h (one v_mad_u64_u32 per limb product, no carry chain); points are
 // converted as they are gathered and bucket pieces as they are stored, so
-// everything outside the accumulation kernels keeps field.h's layout.  G2
-// (Fq2) accumulates in its own field.  TPST_ACC29=0 selects field.h for A/B.
+// everything outside the accumulation kernels keeps field.h's layout.
+// TPST_ACC29=0 selects field.h for A/B.
 template <class F>
 struct AccField {
   using T = F;
@@ -41,6 +75,17 @@ struct AccField<Fq> {
     return {from_std(a.X), from_std(a.Y), from_std(a.ZZ), from_std(a.ZZZ)};
   }
   static __device__ __forceinline__ Xyzz<Fq> out(const Xyzz<T>& a) {
+    return {to_std(a.X), to_std(a.Y), to_std(a.ZZ), to_std(a.ZZZ)};
+  }
+};
+template <>
+struct AccField<Fq2> {
+  using T = Fq2x29;
+  static __device__ __forceinline__ Affine<T> in(const Affine<Fq2>& a) { return {from_std(a.x), from_std(a.y)}; }
+  static __device__ __forceinline__ Xyzz<T> in(const Xyzz<Fq2>& a) {
+    return {from_std(a.X), from_std(a.Y), from_std(a.ZZ), from_std(a.ZZZ)};
+  }
+  static __device__ __forceinline__ Xyzz<Fq2> out(const Xyzz<T>& a) {
     return {to_std(a.X), to_std(a.Y), to_std(a.ZZ), to_std(a.ZZZ)};
   }
 };

@@ -332,12 +332,31 @@ __global__ void __launch_bounds__(64) k_mb_wave_prof(int op, int iters, unsigned
 // RNS engine stages (rns_engine.h): each 12-wave workgroup (two chains) runs
 // `iters` dependent stages of OP; grid = threads / 768 workgroups, so one
 // workgroup measures the stage latency and a full grid the throughput
+template <int OP, class LT>
+__device__ __forceinline__ void mb_rns_body(const LT& L, uint32_t* s_slots, uint32_t* s_xch, int iters,
+                                            uint32_t* __restrict__ sink);
+
 template <int OP>
 __global__ void __launch_bounds__(768) k_mb_rns(int iters, uint32_t* __restrict__ sink) {
   __shared__ uint32_t s_slots[(rns::N_CONSTS + 36) * rns::SLOT];
   __shared__ uint32_t s_xch[12 * rns::XCH];
   rns::load_consts((rns::lds_t*)s_slots);
-  const rns::Lane L = rns::load_lane();
+  mb_rns_body<OP>(rns::load_lane(), s_slots, s_xch, iters, sink);
+}
+
+// the same with the extension rows in LDS (rns::LaneL), two workgroups per CU
+template <int OP>
+__global__ void __launch_bounds__(768, 2) k_mb_rns_l(int iters, uint32_t* __restrict__ sink) {
+  __shared__ uint32_t s_slots[(rns::N_CONSTS + 36) * rns::SLOT];
+  __shared__ uint32_t s_xch[12 * rns::XCH];
+  __shared__ uint32_t s_rows[2 * rns::NB * 32];
+  rns::load_consts((rns::lds_t*)s_slots);
+  mb_rns_body<OP>(rns::load_lane_lds((rns::lds_t*)s_rows), s_slots, s_xch, iters, sink);
+}
+
+template <int OP, class LT>
+__device__ __forceinline__ void mb_rns_body(const LT& L, uint32_t* s_slots, uint32_t* s_xch, int iters,
+                                            uint32_t* __restrict__ sink) {
   const rns::Eng e{(rns::lds_t*)s_slots, (rns::lds_t*)s_xch + rns::wave_id() * rns::XCH, 0};
   for (int i = threadIdx.x; i < 24 * rns::SLOT; i += blockDim.x)
     s_slots[rns::N_CONSTS * rns::SLOT + i] = s_slots[((i / rns::SLOT) % rns::N_CONSTS) * rns::SLOT + (i % rns::SLOT)];
@@ -371,7 +390,7 @@ extern "C" int tpst_microbench(tpst_ctx* ctx, int kind, size_t threads, int iter
   if (!ctx || !ms || threads == 0 || iters <= 0) return fail(ctx, TPST_E_ARG, "bad argument");
   std::lock_guard<std::mutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
-  const bool rnsk = kind >= 64 && kind < 64 + rns::N_OPS;
+  const bool rnsk = kind >= 64 && kind < 96;
   const unsigned bs = rnsk ? 768u : (threads < 256 ? (unsigned)threads : 256u);
   const unsigned grid = grid_for(threads, bs);
   ctx->io.reset();
@@ -417,6 +436,10 @@ extern "C" int tpst_microbench(tpst_ctx* ctx, int kind, size_t threads, int iter
     k_mb_rns<rns::OP_F12_SQR><<<grid, bs, 0, ctx->stream>>>(iters, d);
   } else if (kind == 64 + rns::OP_CYC_SQR) {
     k_mb_rns<rns::OP_CYC_SQR><<<grid, bs, 0, ctx->stream>>>(iters, d);
+  } else if (kind == 80 + rns::OP_F12_MUL) {
+    k_mb_rns_l<rns::OP_F12_MUL><<<grid, bs, 0, ctx->stream>>>(iters, d);
+  } else if (kind == 80 + rns::OP_CYC_SQR) {
+    k_mb_rns_l<rns::OP_CYC_SQR><<<grid, bs, 0, ctx->stream>>>(iters, d);
   } else
     return fail(ctx, TPST_E_ARG, "unknown microbench kind");
   TPST_HIP(ctx, hipGetLastError());

@@ -80,12 +80,13 @@ __global__ void __launch_bounds__(64 * PW) k_g2_prepare_wave(const uint32_t* __r
 // each step's line (region slots 6..11) dumped in residue form, then
 // k_rns_to_fq converts every coefficient to field.h form in bulk -- ~280
 // stages of ~1 us against the radix engine's ~6 us stages.
-__global__ void __launch_bounds__(768) k_g2_prepare_rns(const uint32_t* __restrict__ g2, size_t n,
-                                                        uint32_t* __restrict__ lres) {
+__global__ void __launch_bounds__(768, 2) k_g2_prepare_rns(const uint32_t* __restrict__ g2, size_t n,
+                                                           uint32_t* __restrict__ lres) {
   __shared__ uint32_t s_slots[(rns::N_CONSTS + 44) * rns::SLOT];
   __shared__ uint32_t s_xch[12 * rns::XCH];
+  __shared__ uint32_t s_rows[2 * rns::NB * 32];
   rns::load_consts((rns::lds_t*)s_slots);
-  const rns::Lane L = rns::load_lane();
+  const rns::LaneL L = rns::load_lane_lds((rns::lds_t*)s_rows);
   const rns::Eng e{(rns::lds_t*)s_slots, (rns::lds_t*)s_xch + rns::wave_id() * rns::XCH, 0};
   const int w = rns::wave_id(), lane = threadIdx.x & 63;
   const size_t p0 = 2 * (size_t)blockIdx.x, p1 = p0 + 1 < n ? p0 + 1 : p0;
@@ -684,13 +685,14 @@ __device__ int rc_final_exp(const rns::Eng& e, const rns::Lane& L, int F, int re
 // raw (no reduction), so a chunk costs CH - 1 stages; a short tail chunk is
 // padded with ones so both halves run the same stage sequence.
 template <bool RES_IN, int CH>
-__global__ void __launch_bounds__(64 * RC_WAVES) k_chunk_prod_rns(const void* __restrict__ in, size_t groups,
+__global__ void __launch_bounds__(64 * RC_WAVES, 2) k_chunk_prod_rns(const void* __restrict__ in, size_t groups,
                                                                   size_t n, size_t nout, uint32_t* __restrict__ out) {
   __shared__ uint32_t s_slots[(rns::N_CONSTS + 12 * (CH + 1)) * rns::SLOT];
   __shared__ uint32_t s_xch[RC_WAVES * rns::XCH];
+  __shared__ uint32_t s_rows[2 * rns::NB * 32];
   const size_t items = groups * nout, pairs = (items + 1) / 2;
   rns::load_consts((rns::lds_t*)s_slots);
-  const rns::Lane L = rns::load_lane();
+  const rns::LaneL L = rns::load_lane_lds((rns::lds_t*)s_rows);
   const rns::Eng e{(rns::lds_t*)s_slots, (rns::lds_t*)s_xch + rns::wave_id() * rns::XCH, 0};
   const int w = rns::wave_id(), lane = threadIdx.x & 63;
   const int X = rns::N_CONSTS;  // factor i in slots X + 12 i; the product ping-pongs with X + 12 CH

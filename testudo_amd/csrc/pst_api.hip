@@ -1412,14 +1412,20 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   const size_t n_ev = 8 + 5 * (size_t)m;
   if (int rc = open_streams(ctx, n_ev, up_bytes + dn_bytes)) return rc;
   uint8_t* pin = (uint8_t*)ctx->pinned;
-  // four hardware queues: A (critical), B (cross terms, then the h folds of
-  // "C"), and two look-ahead streams for alternating rounds -- consecutive
-  // look-aheads overlap, each taking longer than a round.  h is prepared
-  // (G2 line coefficients, a ~2 ms chain) only at odd rounds: look-ahead r
-  // pairs E = 2^(r - s) fold sets of a^(r) against the prepared h^(s),
-  // s = r - 2 (r odd) or r - 3 (r even), s = 0 for r <= 2, so stream B
-  // carries one preparation per two rounds
-  hipStream_t sA = ctx->stream, sB = ctx->side[0], sC = ctx->side[0];
+  // four hardware queues: A (critical), B (cross terms), and two look-ahead
+  // streams for alternating rounds -- consecutive look-aheads overlap, each
+  // taking longer than a round.  h is prepared (G2 fold + G2Prepared lines,
+  // ~1.3 ms) only at odd rounds: look-ahead r pairs E = 2^(r - s) fold sets of
+  // a^(r) against the prepared h^(s), s = r - 2 (r odd) or r - 3 (r even),
+  // s = 0 for r <= 2.  That round work "C" rides on stream A: A's own round
+  // work is two short table products, so C delays t^(r+1) by less than the
+  // cross MSMs of stream B take, whereas on B it delayed every even round's
+  // comms_u by ~1 ms (TPST_OPEN_C_ON_B=1 restores that placement); the
+  // epilogue's final h fold runs on the first look-ahead stream (idle by
+  // then), beside final_a (A) and pst_proof_h (B)
+  static const bool c_on_b = getenv("TPST_OPEN_C_ON_B") != nullptr;
+  hipStream_t sA = ctx->stream, sB = ctx->side[0], sC = c_on_b ? ctx->side[0] : ctx->stream;
+  const hipStream_t sCe = ctx->side[1];
   hipStream_t sLA[2] = {ctx->side[1], ctx->side[2]};
   Arena &arA = ctx->arena, &arB = ctx->arena_side[0], &arC = ctx->arena2;
   Arena* arLA[2] = {&ctx->arena_side[1], &ctx->arena_side[2]};
@@ -1429,6 +1435,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   auto ev_a = [&](int r) { return ev[8 + 5 * r + 1]; };
   auto ev_b = [&](int r) { return ev[8 + 5 * r + 2]; };
   auto ev_c = [&](int r) { return ev[8 + 5 * r + 3]; };
+  int last_c = -1;  // the last odd round that issued h work "C"
   auto ev_la = [&](int r) { return ev[8 + 5 * r + 4]; };
   // the prepared h the look-ahead of round r pairs against (see above)
   auto la_src = [](int r) { return r <= 2 ? 0 : (r & 1) ? r - 2 : r - 3; };
@@ -1546,7 +1553,10 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   for (int r = 0; r < m; r++) {  // mipp.rs:58-120
     const size_t len = C >> r, s = len / 2, nW = (size_t)1 << r;
     // stage c_{r-1}, c_{r-1}^-1, the look-ahead factors and digits; upload
-    // once (stream A), form this round's weights there; B, C, D wait on it
+    // once (stream B, whose previous work -- the round's comms_u -- is
+    // already done when the challenge exists: on A the upload queued behind
+    // A's wait for the look-ahead), form this round's weights there; A, C, D
+    // wait on it
     uint8_t* stg = pin + up_off[r];
     // look-ahead fold factors of h^(r) over h^(s), s = la_src(r): f_j = product
     // of c'_{r-1-b} over the set bits b of j (offset j len of h^(s)'s row)
@@ -1565,11 +1575,12 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     uint32_t* dcp = dup_r + 8;   // c' = c_{r-1}^-1 (the y fold)
     uint32_t* dfs = dup_r + 16;  // f_0..f_{E-1}
     const uint64_t* ddig = (const uint64_t*)(dup_r + 80);
-    TPST_HIP(ctx, hipMemcpyAsync(dup_r, stg, UP_ROUND, hipMemcpyHostToDevice, sA));
-    TPST_HIP(ctx, mipp_weights(sA, Wall.u(), Wiall.u(), r, dup_r, dcp));
+    TPST_HIP(ctx, hipMemcpyAsync(dup_r, stg, UP_ROUND, hipMemcpyHostToDevice, sB));
+    TPST_HIP(ctx, mipp_weights(sB, Wall.u(), Wiall.u(), r, dup_r, dcp));
     uint32_t* dW = Wall.u() + 8 * (nW - 1);
     uint32_t* dWi = Wiall.u() + 8 * (nW - 1);
-    TPST_HIP(ctx, hipEventRecord(ev_up(r), sA));
+    TPST_HIP(ctx, hipEventRecord(ev_up(r), sB));
+    TPST_HIP(ctx, hipStreamWaitEvent(sA, ev_up(r), 0));
 
     // -- A: t_l / t_r of this round
     if (r == 0) {  // direct: the rotated comm_list (affine) against h^(0)
@@ -1630,7 +1641,15 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     TPST_HIP(ctx, hipStreamWaitEvent(sB, ev_up(r), 0));
     if (r > 0) TPST_HIP(ctx, compress_fr(sB, Y.u(), len, dcp));  // y_l + c' y_r (mipp.rs:124-136)
     TPST_HIP(ctx, mipp_scalars(sB, dW, Y.u(), len, s, C, ScB.u()));
-    {
+    static const bool var0 = getenv("TPST_OPEN_VAR0") != nullptr;
+    if (r == 0 && var0) {
+      // (measured, not kept: round 0's u_l = sum_{k<s} Sc[k] a_k, u_r =
+      // sum_{k>=s} Sc[k] a_k as two variable-base MSMs over comm_list, to take
+      // the GLV fold table build (~1.25 ms at 2^20) off round 0's path -- two
+      // 512-point K2 MSMs took ~3.4 ms, the table path ~1.7 ms)
+      TPST_HIP(ctx, msm_var<Fq>(arB, sB, A.u(), ScB.u(), s, (Xyzz<Fq>*)xb.p));
+      TPST_HIP(ctx, msm_var<Fq>(arB, sB, A.u() + 24 * s, ScB.u() + 8 * s, s, (Xyzz<Fq>*)xb.p + 1));
+    } else {
       TPST_HIP(ctx, hipStreamWaitEvent(sB, ev[EV_TABLE], 0));
       FbGroups g;
       g.groups = 2;
@@ -1661,6 +1680,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
       TPST_HIP(ctx, g2_prepare_batch(sC, Hb[(r >> 1) & 1].u(), len, (LineCoeff*)Lb[(r >> 1) & 1].p,
                                      st->prep_scratch.u()));
       TPST_HIP(ctx, hipEventRecord(ev_c(r), sC));
+      last_c = r;
     }
 
     // -- host: transcript (mipp.rs:56, 97-101) and the challenge
@@ -1751,15 +1771,16 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(sA, (Xyzz<Fq>*)xa.p, canA.u(), 1));
     TPST_HIP(ctx, hipMemcpyAsync(pin + dn_final, canA.p, 96, hipMemcpyDeviceToHost, sA));
   }
-  TPST_HIP(ctx, hipStreamWaitEvent(sC, ev[EV_FINAL_UP], 0));
+  TPST_HIP(ctx, hipStreamWaitEvent(sCe, ev[EV_FINAL_UP], 0));
+  if (last_c >= 0) TPST_HIP(ctx, hipStreamWaitEvent(sCe, ev_c(last_c), 0));  // xh / ScC / arC reuse
   {  // final_h = h^(m)_0
     FbGroups g;
     g.members = C;
-    TPST_HIP(ctx, mipp_scalars(sC, dWim, nullptr, 1, 0, C, ScC.u()));
-    TPST_HIP(ctx, fbt_msm<Fq2>(arC, sC, tH, ScC.u(), g, (Xyzz<Fq2>*)xh.p));
-    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq2>(sC, (Xyzz<Fq2>*)xh.p, canC.u(), 1));
-    TPST_HIP(ctx, hipMemcpyAsync(pin + dn_final + 96, canC.p, 192, hipMemcpyDeviceToHost, sC));
-    TPST_HIP(ctx, hipEventRecord(ev[EV_C_DONE], sC));
+    TPST_HIP(ctx, mipp_scalars(sCe, dWim, nullptr, 1, 0, C, ScC.u()));
+    TPST_HIP(ctx, fbt_msm<Fq2>(arC, sCe, tH, ScC.u(), g, (Xyzz<Fq2>*)xh.p));
+    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq2>(sCe, (Xyzz<Fq2>*)xh.p, canC.u(), 1));
+    TPST_HIP(ctx, hipMemcpyAsync(pin + dn_final + 96, canC.p, 192, hipMemcpyDeviceToHost, sCe));
+    TPST_HIP(ctx, hipEventRecord(ev[EV_C_DONE], sCe));
   }
   if (m > 0) {  // pst_proof_h = open_g1(p_h, rs) (mipp.rs:144)
     TPST_HIP(ctx, hipStreamWaitEvent(sB, ev[EV_FINAL_UP], 0));

@@ -58,6 +58,19 @@ __device__ __forceinline__ void wave_sync() {
 struct Lane {
   uint32_t m, c32, cc, mask, negk, k1, pj, minv, k3, mpinv, mpn, k5;
   uint32_t row1[NB], row2[NB];
+  __device__ __forceinline__ uint32_t r1(int i) const { return row1[i]; }
+  __device__ __forceinline__ uint32_t r2(int j) const { return row2[j]; }
+};
+
+// the same constants with the two 15-entry extension rows in LDS (a
+// [2 NB][32] table, conflict-free reads): ~30 fewer VGPRs, so two 12-wave
+// workgroups fit a CU -- for the throughput kernels (tree levels, tables)
+struct LaneL {
+  uint32_t m, c32, cc, mask, negk, k1, pj, minv, k3, mpinv, mpn, k5;
+  const __attribute__((address_space(3))) uint32_t* rows;
+  int ch;
+  __device__ __forceinline__ uint32_t r1(int i) const { return rows[i * 32 + ch]; }
+  __device__ __forceinline__ uint32_t r2(int j) const { return rows[(NB + j) * 32 + ch]; }
 };
 
 __device__ __forceinline__ Lane load_lane() {
@@ -83,10 +96,37 @@ __device__ __forceinline__ Lane load_lane() {
   return L;
 }
 
+// rows: 2 NB x 32 u32 of LDS, filled here (the caller's __syncthreads
+// publishes them)
+__device__ __forceinline__ LaneL load_lane_lds(__attribute__((address_space(3))) uint32_t* rows) {
+  for (int i = threadIdx.x; i < 2 * NB * 32; i += blockDim.x) {
+    const int r = i >> 5, c = i & 31;
+    rows[i] = LANE[c][(r < NB ? ROW1_OFF : ROW2_OFF - NB) + r];
+  }
+  const uint32_t* w = LANE[threadIdx.x & 31];
+  LaneL L;
+  L.m = w[LF_MOD];
+  L.c32 = w[LF_C32];
+  L.cc = w[LF_CC];
+  L.mask = w[LF_ISR] ? 0xffffffffu : 0x0fffffffu;
+  L.negk = w[LF_NEGK];
+  L.k1 = w[LF_K1];
+  L.pj = w[LF_PJ];
+  L.minv = w[LF_MINV];
+  L.k3 = w[LF_K3];
+  L.mpinv = w[LF_MPINV];
+  L.mpn = w[LF_MPN];
+  L.k5 = w[LF_K5];
+  L.rows = rows;
+  L.ch = threadIdx.x & 31;
+  return L;
+}
+
 // x mod m (m = 2^28 - c) by folding 2^32 = 16 c twice and 2^28 = c once;
 // on the 2^32 channel c32 = cc = m = 0 and mask = ~0, so the same
 // instructions return the low word
-__device__ __forceinline__ uint32_t red64(uint64_t x, const Lane& L) {
+template <class LT>
+__device__ __forceinline__ uint32_t red64(uint64_t x, const LT& L) {
   const uint64_t y = (uint64_t)(uint32_t)(x >> 32) * L.c32 + (uint32_t)x;
   const uint64_t z = (uint64_t)(uint32_t)(y >> 32) * L.c32 + (uint32_t)y;  // < 2^33
   const uint32_t zh = (uint32_t)(z >> 28);
@@ -94,7 +134,8 @@ __device__ __forceinline__ uint32_t red64(uint64_t x, const Lane& L) {
   return w >= L.m ? w - L.m : w;
 }
 
-__device__ __forceinline__ uint32_t red32(uint32_t v, const Lane& L) {
+template <class LT>
+__device__ __forceinline__ uint32_t red32(uint32_t v, const LT& L) {
   const uint32_t w = __umul24(v >> 28, L.cc) + (v & L.mask);
   return w >= L.m ? w - L.m : w;
 }
@@ -116,7 +157,8 @@ __device__ __forceinline__ void read15(const lds_t* p, uint32_t (&x)[NB]) {
 
 // RNS Montgomery reduction of this lane's residue t of T (< 2^16 p^2 * 2):
 // returns its residue of (T + q p) / M (< 16 p, = T M^-1 mod p)
-__device__ __forceinline__ uint32_t mont(const Eng& e, const Lane& L, uint32_t t) {
+template <class LT>
+__device__ __forceinline__ uint32_t mont(const Eng& e, const LT& L, uint32_t t) {
   const int lane = threadIdx.x & 63, hb = lane & 32, ch = lane & 31;
   e.xch[lane] = red64((uint64_t)t * L.k1, L);  // B: xi_i
   wave_sync();
@@ -124,7 +166,7 @@ __device__ __forceinline__ uint32_t mont(const Eng& e, const Lane& L, uint32_t t
   read15(e.xch + hb, xs);
   uint64_t acc = 0;
 #pragma unroll
-  for (int i = 0; i < NB; i++) acc += (uint64_t)xs[i] * L.row1[i];
+  for (int i = 0; i < NB; i++) acc += (uint64_t)xs[i] * L.r1(i);
   const uint32_t q = red64(acc, L);                      // B', 2^32: q^
   const uint32_t u = red64((uint64_t)q * L.pj + t, L);
   const uint32_t r = red64((uint64_t)u * L.minv, L);     // (t + q^ p) / M
@@ -133,7 +175,7 @@ __device__ __forceinline__ uint32_t mont(const Eng& e, const Lane& L, uint32_t t
   read15(e.xch + 64 + hb + BP0, xs);
   acc = 0;
 #pragma unroll
-  for (int j = 0; j < NB; j++) acc += (uint64_t)xs[j] * L.row2[j];
+  for (int j = 0; j < NB; j++) acc += (uint64_t)xs[j] * L.r2(j);
   // 2^32 channel: beta = (sum xi'_j M'_j - r) / M' exactly (< 15)
   if (ch == R_CH) e.xch[128 + (hb >> 5)] = ((uint32_t)acc - r) * L.mpinv;
   const uint32_t s = red64(acc, L);
@@ -145,8 +187,8 @@ __device__ __forceinline__ uint32_t mont(const Eng& e, const Lane& L, uint32_t t
 
 // ---- stages -----------------------------------------------------------------
 // output O of op OP: sum of its monomials (term words folded at compile time)
-template <int OP, int O>
-__device__ __forceinline__ uint64_t out_terms(const Lane& L, const lds_t* pa, const lds_t* pb, const lds_t* pk,
+template <int OP, int O, class LT>
+__device__ __forceinline__ uint64_t out_terms(const LT& L, const lds_t* pa, const lds_t* pb, const lds_t* pk,
                                               int& dst) {
   constexpr int NT = OP_NT[OP];
   constexpr int BLK = OP_OFF[OP] + 1 + O * (1 + NT);
@@ -169,8 +211,8 @@ __device__ __forceinline__ uint64_t out_terms(const Lane& L, const lds_t* pa, co
   return acc;
 }
 
-template <int OP, int O = 0>
-__device__ __forceinline__ uint64_t terms(int w, const Lane& L, const lds_t* pa, const lds_t* pb, const lds_t* pk,
+template <int OP, int O = 0, class LT>
+__device__ __forceinline__ uint64_t terms(int w, const LT& L, const lds_t* pa, const lds_t* pb, const lds_t* pk,
                                           int& dst) {
   if constexpr (O + 1 < OP_NO[OP]) {
     if (w != O) return terms<OP, O + 1>(w, L, pa, pb, pk, dst);
@@ -184,8 +226,8 @@ __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane
 // the destination registers must not overlap the inputs
 // INPLACE: outputs may overwrite inputs (the G2 region ops, a == c): every
 // wave finishes its reads before any wave writes
-template <int OP, bool INPLACE = false>
-__device__ __forceinline__ void stage(const Eng& e, const Lane& L, int a, int b, int c, int d = 0) {
+template <int OP, bool INPLACE = false, class LT>
+__device__ __forceinline__ void stage(const Eng& e, const LT& L, int a, int b, int c, int d = 0) {
   const int w = wave_id(), lane = threadIdx.x & 63;
   int dst = 0;
   uint64_t acc = 0;
@@ -200,7 +242,8 @@ __device__ __forceinline__ void stage(const Eng& e, const Lane& L, int a, int b,
 }
 
 // this lane's residue of a field.h Montgomery Fq (12 limbs) as an integer
-__device__ __forceinline__ uint32_t residue(const Lane& L, const uint32_t* s) {
+template <class LT>
+__device__ __forceinline__ uint32_t residue(const LT& L, const uint32_t* s) {
   const uint32_t* pw = LANE[threadIdx.x & 31] + POW32_OFF;
   uint64_t acc = 0;
 #pragma unroll
@@ -211,7 +254,8 @@ __device__ __forceinline__ uint32_t residue(const Lane& L, const uint32_t* s) {
 // slots c .. c+n-1 <- src_h[0 .. n): field.h Montgomery Fq (v = a R < p) into
 // the M-domain, times (M/R)^(k-1) for the first of k raw factors: the slot
 // gets mont(v * K_LOAD[k]) = a (M/R)^(k-1) M (chain h = lane >> 5 reads src_h)
-__device__ __forceinline__ void load(const Eng& e, const Lane& L, const Fq* src0, const Fq* src1, int c, int n,
+template <class LT>
+__device__ __forceinline__ void load(const Eng& e, const LT& L, const Fq* src0, const Fq* src1, int c, int n,
                                      int k = 1) {
   const int w = wave_id(), lane = threadIdx.x & 63;
   if (w < n) {
@@ -225,7 +269,8 @@ __device__ __forceinline__ void load(const Eng& e, const Lane& L, const Fq* src0
 // raw factor: slots c .. c+n-1 <- the residues of v = a R itself (the
 // M-domain element a R / M), no reduction; src_h == nullptr loads field.h's
 // one (R mod p) for that chain
-__device__ __forceinline__ void load_raw(const Eng& e, const Lane& L, const Fq* src0, const Fq* src1, int c, int n) {
+template <class LT>
+__device__ __forceinline__ void load_raw(const Eng& e, const LT& L, const Fq* src0, const Fq* src1, int c, int n) {
   const int w = wave_id(), lane = threadIdx.x & 63;
   if (w < n) {
     const Fq* src = (lane & 32) ? src1 : src0;
@@ -268,7 +313,8 @@ __device__ __forceinline__ void reduce16p(uint32_t (&r)[12]) {
 // this wave's two values (one per half, residue x of lane) from the M-domain
 // to field.h Montgomery form, canonical (< p), through CRT over base B;
 // lane 0 of each half writes its half's dst (no workgroup barrier)
-__device__ __forceinline__ void to_fq_wave(const Eng& e, const Lane& L, uint32_t x, Fq* dst0, Fq* dst1) {
+template <class LT>
+__device__ __forceinline__ void to_fq_wave(const Eng& e, const LT& L, uint32_t x, Fq* dst0, Fq* dst1) {
   const int lane = threadIdx.x & 63, hb = lane & 32, ch = lane & 31;
   const uint32_t kout = e.slots[(e.kon + K_OUT) * SLOT + lane];
   const uint32_t r = mont(e, L, red64((uint64_t)x * kout, L));  // value R, < 16 p
@@ -279,7 +325,7 @@ __device__ __forceinline__ void to_fq_wave(const Eng& e, const Lane& L, uint32_t
   read15(e.xch + hb, xs);
   uint64_t acc = 0;
 #pragma unroll
-  for (int i = 0; i < NB; i++) acc += (uint64_t)xs[i] * L.row1[i];
+  for (int i = 0; i < NB; i++) acc += (uint64_t)xs[i] * L.r1(i);
   if (ch == R_CH) e.xch[128 + (hb >> 5)] = ((uint32_t)acc - r) * L.minv;  // alpha
   if (ch < 14) {  // column ch of sum_i xi_i M_i
     uint64_t col = 0;
@@ -320,7 +366,8 @@ __device__ __forceinline__ void to_fq_wave(const Eng& e, const Lane& L, uint32_t
 }
 
 // dst_h[0 .. n) <- slots a .. a+n-1: M-domain to field.h Montgomery form
-__device__ __forceinline__ void store(const Eng& e, const Lane& L, int a, Fq* dst0, Fq* dst1, int n) {
+template <class LT>
+__device__ __forceinline__ void store(const Eng& e, const LT& L, int a, Fq* dst0, Fq* dst1, int n) {
   const int w = wave_id(), lane = threadIdx.x & 63;
   if (w < n) to_fq_wave(e, L, e.slots[(a + w) * SLOT + lane], dst0 + w, dst1 + w);
   __syncthreads();

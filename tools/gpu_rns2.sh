@@ -5,7 +5,7 @@ OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 cd $GRAFT_REPO_ROOT
 mkdir -p $OUT
 PT="python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu"
-timeout -k 10 600 $PT -k "pairing or ipp or open or verify or mipp or commit" > $OUT/gpu_tests.log 2>&1 || exit 1
+timeout -k 10 600 $PT -k "pairing or ipp or open or verify or mipp or commit or g2 or fbt or groth" > $OUT/gpu_tests.log 2>&1 || exit 1
 lscpu > $OUT/lscpu.txt 2>&1; TPST_OPEN_TRACE=1 timeout -k 10 120 python -u tools/prof_open.py 20 3 > $OUT/open_trace_stdout.txt 2> $OUT/open_trace.txt || exit 1
 timeout -k 10 400 python -u bench.py --no-cpu --no-r1cs --no-groth16 --steps 5 > $OUT/bench.json 2> $OUT/bench.err || exit 1
 cd /tmp && export TMPDIR=/tmp
