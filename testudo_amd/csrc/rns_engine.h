@@ -288,25 +288,34 @@ __device__ __forceinline__ void load_raw(const Eng& e, const LT& L, const Fq* sr
   __syncthreads();
 }
 
-// r (12 limbs, < 16 p) mod p
+// r (12 limbs, < 16 p) mod p: a quotient estimate from the top two limbs
+// (scaled down so it never exceeds floor(r / p) and is at most one below),
+// one q p subtraction, one conditional subtraction
 __device__ __forceinline__ void reduce16p(uint32_t (&r)[12]) {
+  constexpr double PTOP = (double)params::FQ_P[11] * 4294967296.0 + (double)params::FQ_P[10];
+  const double num = (double)r[11] * 4294967296.0 + (double)r[10];
+  const uint32_t q = (uint32_t)(num / PTOP * (1.0 - 1e-9));
+  uint64_t cp = 0;
+  int64_t br = 0;
 #pragma unroll
-  for (int k = 8; k >= 1; k >>= 1) {
-    uint32_t d[12];
-    uint64_t cp = 0;
-    int64_t br = 0;
+  for (int i = 0; i < 12; i++) {
+    const uint64_t qp = (uint64_t)params::FQ_P[i] * q + cp;
+    cp = qp >> 32;
+    const int64_t t = (int64_t)r[i] - (int64_t)(uint32_t)qp + br;
+    r[i] = (uint32_t)t;
+    br = t >> 32;
+  }
+  uint32_t d[12];
+  br = 0;
 #pragma unroll
-    for (int i = 0; i < 12; i++) {
-      const uint64_t kp = (uint64_t)params::FQ_P[i] * (uint32_t)k + cp;
-      cp = kp >> 32;
-      const int64_t t = (int64_t)r[i] - (int64_t)(uint32_t)kp + br;
-      d[i] = (uint32_t)t;
-      br = t >> 32;
-    }
-    if (br == 0 && cp == 0) {
+  for (int i = 0; i < 12; i++) {
+    const int64_t t = (int64_t)r[i] - (int64_t)params::FQ_P[i] + br;
+    d[i] = (uint32_t)t;
+    br = t >> 32;
+  }
+  if (br == 0) {
 #pragma unroll
-      for (int i = 0; i < 12; i++) r[i] = d[i];
-    }
+    for (int i = 0; i < 12; i++) r[i] = d[i];
   }
 }
 
