@@ -409,13 +409,17 @@ int tpst_g1_mul_generator_dev(tpst_ctx* ctx, const void* d_scalars, size_t n, vo
 
 /* Field microbenchmark (measured peak for the roofline's compute column):
  * kind 0 = Fq Montgomery multiply, 1 = G1 XYZZ mixed add, 2 = Fq inverse, 3 / 4 = Fq multiply
- * variants (two interleaved accumulation chains / independent columns), 5 = G1 XYZZ doubling, 16 + op = one wave
+ * variants (two interleaved accumulation chains / independent columns), 5 = G1 XYZZ doubling, 15 = Fq inverse
+ * by a whole wave (csrc/inv_wave.h; one chain per 64 threads), 16 + op = one wave
  * running `iters` stages of wave-engine op `op` (csrc/wave_ops.inc).  Runs `threads`
  * threads x `iters` dependent ops each; returns kernel milliseconds. */
 int tpst_microbench(tpst_ctx* ctx, int kind, size_t threads, int iters, double* ms);
 /* shader-clock cycles of the parts of `iters` stages of wave op `op` (forms,
  * product, product store, output forms, output reduce/store) */
 int tpst_microbench_wave_phases(tpst_ctx* ctx, int op, int iters, uint64_t* cycles5);
+/* Self-test of the two device Fq inverses: n Montgomery-form values (6 words
+ * each) -> their inverses by the lone-lane routine and by the wave routine. */
+int tpst_selftest_inv(tpst_ctx* ctx, size_t n, const uint64_t* in, uint64_t* out_lane, uint64_t* out_wave);
 
 /* Per-stage HIP-event timing of the MSM pipeline on the context's stream.
  * stage: 0 decompose, 1 sort, 2 bucket bounds, 3 bucket accumulation (the

@@ -24,6 +24,24 @@ def _fr(v):
     return fr_array([v])[0]
 
 
+# ------------------------------------------------------------ Fq inverse --
+def test_fq_inverse_lane_and_wave(ctx):
+    """csrc/inv_wave.h (one inverse per wave, 15-bit limbs across lanes) and
+    field29.h's lone-lane inverse against Python's modular inverse, on
+    Montgomery-form words (w = a R -> a^-1 R = R^2 / w); 0 -> 0"""
+    p = O.P
+    R = 1 << 384
+    rng = np.random.default_rng(11)
+    vals = [0, 1, 2, p - 1, p - 2, R % p, (1 << 376) + 12345, p // 2]
+    vals += [int.from_bytes(rng.bytes(48), "little") % p for _ in range(120)]
+    words = np.array([[(v >> (64 * i)) & ((1 << 64) - 1) for i in range(6)] for v in vals], dtype=np.uint64)
+    ol, ow = ctx.selftest_inv(words)
+    for v, a, b in zip(vals, ol, ow):
+        want = 0 if v == 0 else R * R * pow(v, -1, p) % p
+        assert limbs_to_int(a) == want, v
+        assert limbs_to_int(b) == want, v
+
+
 # ------------------------------------------------------------------- MSM --
 def test_g1_msm_golden(ctx):
     d = G.load("msm.json")["g1"]

@@ -51,6 +51,7 @@ PROTOTYPES = [
     ("tpst_g1_mul_generator_dev", C.c_int, [_vp, _vp, _sz, _vp]),
     ("tpst_microbench", C.c_int, [_vp, C.c_int, _sz, C.c_int, C.POINTER(C.c_double)]),
     ("tpst_microbench_wave_phases", C.c_int, [_vp, C.c_int, C.c_int, _u64p]),
+    ("tpst_selftest_inv", C.c_int, [_vp, _sz, _u64p, _u64p, _u64p]),
     ("tpst_transcript_init", None, [_vp]),
     ("tpst_transcript_append_g1", C.c_int, [_vp, _u64p]),
     ("tpst_transcript_append_gt", C.c_int, [_vp, _u64p]),

@@ -1,0 +1,246 @@
+// One Fq inversion by a whole wave (device only).
+//
+// Why: the lone-lane inverse (field29.h inv: 26 batches of 29 divsteps on
+// 13-limb values) is a ~0.13 ms serial chain.  Where only one or two values
+// are inverted -- the open's per-round cross commitments, an MSM's single
+// output point, the final-exponentiation chain -- that chain sits on the
+// critical path with 63 lanes idle.  Here the wave shares the work: Pornin's
+// binary GCD in batches of K = 15 divsteps on 32-bit approximations (the
+// batch transition runs on wave-uniform values, i.e. the scalar unit), the big
+// values a, b (the GCD pair) and u, v (the cofactors, signed) as NL = 28 limbs
+// of 15 bits, one limb per lane.  A batch's four updates
+//     (x f + y g + k p) / 2^15
+// are one limb product per lane plus a carry normalisation: a bias makes every
+// limb sum nonnegative, two local carry passes (DPP shift by one lane) leave
+// limbs <= 2^15 + 4, and one ballot pass resolves the remaining +1 ripples
+// (carry-lookahead on the 64-bit lane masks); the division by 2^15 is a shift
+// down by one lane.  Exact model, every step as computed here:
+// tools/inv_wave_model.py.
+//
+// Bounds (checked by the model): |f| + |g| <= 2^15 and limbs < 2^15, so a
+// limb sum stays below 2^31 in magnitude; the cofactors stay below 52 p.
+#pragma once
+#include "field29.h"
+#include "curve.h"
+
+namespace tpst {
+namespace invw {
+
+constexpr int NL = 28;
+constexpr int K = 15;
+constexpr uint32_t LM = (1u << 15) - 1;
+constexpr int ITERS = (2 * 377 - 1 + K - 1) / K;  // 51
+constexpr uint64_t NLMASK = (1ull << NL) - 1;
+
+// p in radix 2^15
+__device__ static constexpr uint32_t P15[32] = {
+    0x0001u, 0x0000u, 0x0000u, 0x2846u, 0x0008u, 0x0000u, 0x510cu, 0x05aeu, 0x0017u, 0x1290u, 0x3ee8u,
+    0x1b11u, 0x71efu, 0x2271u, 0x403du, 0x6cf9u, 0x1a22u, 0x1276u, 0x3285u, 0x2e03u, 0x63b0u, 0x1d58u,
+    0x7144u, 0x230bu, 0x2e3au, 0x0003u, 0x0000u, 0x0000u, 0, 0, 0, 0};
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// lane i receives lane i-1's value, lane 0 receives 0
+__device__ __forceinline__ uint32_t shift_up(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, false);
+}
+// lane i receives lane i+1's value, lane 63 receives 0
+__device__ __forceinline__ uint32_t shift_down(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t rl(uint32_t x, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, l); }
+
+// one-bit lane carries of a 64-bit lane mask -> this lane's bit
+__device__ __forceinline__ uint32_t lane_bit(uint64_t m, uint32_t lane) { return (uint32_t)(m >> lane) & 1u; }
+
+// limb sums t (|t| < 2^31) -> (value / 2^15) as sign + magnitude limbs;
+// the value is a multiple of 2^15 by construction
+__device__ __forceinline__ uint32_t div_signed(int32_t t, uint32_t lane, bool& neg) {
+  const bool live = lane < (uint32_t)NL;
+  uint32_t x = (uint32_t)t + 0x80000000u - (lane ? 0x10000u : 0u);
+  x = live ? x : 0u;
+#pragma unroll
+  for (int pass = 0; pass < 2; pass++) x = (x & LM) + shift_up(x >> 15);
+  const uint64_t g = __ballot(live && x > LM);
+  uint32_t base = x & LM;
+  uint64_t pr = __ballot(live && base == LM);
+  uint32_t limb = (base + lane_bit(((g << 1) + pr) ^ pr, lane)) & LM;
+  limb = live ? limb : 0u;
+  neg = (rl(limb, NL - 1) >> 14) & 1u;
+  if (neg) {  // wave-uniform: magnitude = ~limbs + 1
+    const uint32_t iv = live ? LM - limb : 0u;
+    pr = __ballot(live && iv == LM);
+    limb = (iv + lane_bit((1ull + pr) ^ pr, lane)) & LM;
+    limb = live ? limb : 0u;
+  }
+  return shift_down(limb);  // limb 0 is zero: / 2^15
+}
+
+}  // namespace invw
+
+// y^-1 for a Montgomery-form y (x 2^377 -> x^-1 2^377), 0 -> 0.  Every lane of
+// the wave must call it with the same y (wave-uniform); every lane gets the
+// result.
+__device__ inline __attribute__((noinline)) Fq29 inv_wave(const Fq29& y) {
+  using namespace invw;
+  const uint32_t lane = lane_id();
+  // lane i: bits [15 i, 15 i + 15) of y
+  uint32_t a;
+  {
+    const uint32_t bit = 15u * lane, j = bit / 29u, sh = bit % 29u;
+    uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+    for (int jj = 0; jj < r29::N; jj++) {
+      w0 = (uint32_t)jj == j ? y.v[jj] : w0;
+      w1 = (uint32_t)jj == j + 1 ? y.v[jj] : w1;
+    }
+    a = ((w0 >> sh) | (sh ? w1 << (29u - sh) : 0u)) & LM;
+    a = lane < (uint32_t)NL ? a : 0u;
+  }
+  const uint32_t pl = P15[lane & 31];
+  uint32_t b = lane < (uint32_t)NL ? pl : 0u;
+  uint32_t u = lane == 0 ? 1u : 0u, v = 0;
+  bool us = false, vs = false;
+#pragma unroll 1
+  for (int it = 0; it < ITERS; it++) {
+    // 32-bit approximations: low 15 bits | top 17 bits of n = max(bitlen, 32)
+    const uint64_t nz = __ballot((a | b) != 0u);
+    int n = 32;
+    if (nz) {
+      const int top = 63 - __builtin_clzll(nz);
+      const uint32_t tw = rl(a | b, top);
+      const int nb = 15 * top + 32 - __builtin_clz(tw);
+      n = nb > 32 ? nb : 32;
+    }
+    const int s = n - 17, l0 = s / 15, sh = s % 15;
+    const uint32_t ta = ((rl(a, l0) >> sh) | (rl(a, l0 + 1) << (15 - sh)) | (rl(a, l0 + 2) << (30 - sh))) & 0x1ffffu;
+    const uint32_t tb = ((rl(b, l0) >> sh) | (rl(b, l0 + 1) << (15 - sh)) | (rl(b, l0 + 2) << (30 - sh))) & 0x1ffffu;
+    uint32_t ab = (rl(a, 0) & LM) | (ta << 15);
+    uint32_t bb = (rl(b, 0) & LM) | (tb << 15);
+    int32_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      const uint32_t odd = 0u - (ab & 1u);
+      const uint32_t sw = odd & (0u - (uint32_t)(ab < bb));
+      const uint32_t t = (ab ^ bb) & sw;
+      ab ^= t;
+      bb ^= t;
+      const int32_t sw32 = (int32_t)sw, o32 = (int32_t)odd;
+      const int32_t tf = (f0 ^ f1) & sw32, tg = (g0 ^ g1) & sw32;
+      f0 ^= tf;
+      f1 ^= tf;
+      g0 ^= tg;
+      g1 ^= tg;
+      ab -= bb & odd;
+      f0 -= f1 & o32;
+      g0 -= g1 & o32;
+      ab >>= 1;
+      f1 += f1;
+      g1 += g1;
+    }
+    bool sa, sb;
+    const uint32_t na = div_signed((int32_t)a * f0 + (int32_t)b * g0, lane, sa);
+    const uint32_t nbv = div_signed((int32_t)a * f1 + (int32_t)b * g1, lane, sb);
+    if (sa) {
+      f0 = -f0;
+      g0 = -g0;
+    }
+    if (sb) {
+      f1 = -f1;
+      g1 = -g1;
+    }
+    // signed cofactors; k p clears the low 15 bits
+    const int32_t uf0 = us ? -f0 : f0, vg0 = vs ? -g0 : g0;
+    const int32_t uf1 = us ? -f1 : f1, vg1 = vs ? -g1 : g1;
+    const int32_t u0 = (int32_t)rl(u, 0), v0 = (int32_t)rl(v, 0);
+    const int32_t k0 = (int32_t)((uint32_t)(-(u0 * uf0 + v0 * vg0)) & LM);
+    const int32_t k1 = (int32_t)((uint32_t)(-(u0 * uf1 + v0 * vg1)) & LM);
+    bool nus, nvs;
+    const uint32_t nu = div_signed((int32_t)u * uf0 + (int32_t)v * vg0 + k0 * (int32_t)pl, lane, nus);
+    const uint32_t nv = div_signed((int32_t)u * uf1 + (int32_t)v * vg1 + k1 * (int32_t)pl, lane, nvs);
+    a = na;
+    b = nbv;
+    u = nu;
+    v = nv;
+    us = nus;
+    vs = nvs;
+  }
+  // gcd(y, p) = b = 1 for y != 0; then v = +-y^-1 (plain), |v| < 52 p
+  const bool ok = (__ballot(b != (lane == 0 ? 1u : 0u)) & NLMASK) == 0;
+  uint32_t vl[NL];
+#pragma unroll
+  for (int i = 0; i < NL; i++) vl[i] = rl(v, i);
+  // radix 2^15 -> 14 limbs of 2^29
+  uint32_t r[14];
+#pragma unroll
+  for (int j = 0; j < 14; j++) {
+    uint64_t w = 0;
+#pragma unroll
+    for (int i = 0; i < NL; i++) {
+      const int sh = 15 * i - 29 * j;
+      if (sh > -15 && sh < 29) w |= sh >= 0 ? ((uint64_t)vl[i] << sh) : ((uint64_t)vl[i] >> (-sh));
+    }
+    r[j] = (uint32_t)w & r29::M;
+  }
+  // r mod p: a quotient estimate from the top limbs (q <= 51, low by at most
+  // one), then one conditional subtraction
+  {
+    const double dv = (double)r[13] * 536870912.0 + (double)r[12] + (double)r[11] * (1.0 / 536870912.0);
+    const double dp = (double)r29::P[12] + (double)r29::P[11] * (1.0 / 536870912.0);
+    const int64_t q = (int64_t)(dv / dp * (1.0 - 1e-12));
+    int64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 14; j++) {
+      const int64_t w = (int64_t)r[j] - q * (int64_t)(j < r29::N ? r29::P[j] : 0u) + c;
+      r[j] = (uint32_t)w & r29::M;
+      c = w >> 29;
+    }
+    uint32_t s[14];
+    int64_t bw = 0;
+#pragma unroll
+    for (int j = 0; j < 14; j++) {
+      const int64_t w = (int64_t)r[j] - (int64_t)(j < r29::N ? r29::P[j] : 0u) + bw;
+      s[j] = (uint32_t)w & r29::M;
+      bw = w >> 29;
+    }
+#pragma unroll
+    for (int j = 0; j < 14; j++) r[j] = bw == 0 ? s[j] : r[j];
+  }
+  Fq29 x, k;
+  uint32_t nzv = 0;
+#pragma unroll
+  for (int j = 0; j < r29::N; j++) {
+    x.v[j] = r[j];
+    nzv |= r[j];
+    k.v[j] = r29::R3[j];
+  }
+  if (vs && nzv) {  // -r mod p
+    int64_t bw = 0;
+#pragma unroll
+    for (int j = 0; j < r29::N; j++) {
+      const int64_t w = (int64_t)r29::P[j] - (int64_t)x.v[j] + bw;
+      x.v[j] = (uint32_t)w & r29::M;
+      bw = w >> 29;
+    }
+  }
+  x = mul(x, k);  // x^-1 2^-377 -> x^-1 2^377
+  return ok ? x : Fq29::zero();
+}
+
+// field.h layout wrappers
+__device__ __forceinline__ Fq inv_w(const Fq& a) { return to_std(inv_wave(from_std(a))); }
+__device__ __forceinline__ Fq2 inv_w(const Fq2& a) {
+  const Fq n = add(sqr(a.c0), mul5(sqr(a.c1)));
+  const Fq ni = inv_w(n);
+  return {mul(a.c0, ni), neg(mul(a.c1, ni))};
+}
+
+// curve.h to_affine with the wave inverse (wave-uniform point)
+template <class F>
+__device__ Affine<F> to_affine_w(const Xyzz<F>& p) {
+  if (is_zero(p.ZZ)) return Affine<F>::inf();
+  const F t = inv_w(mul(p.ZZ, p.ZZZ));
+  return {mul(p.X, mul(t, p.ZZZ)), mul(p.Y, mul(t, p.ZZ))};
+}
+
+}  // namespace tpst

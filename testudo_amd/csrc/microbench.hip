@@ -7,6 +7,7 @@
 #include "wave_tower.h"
 #include "rns_engine.h"
 #include "field29.h"
+#include "inv_wave.h"
 
 using namespace tpst;
 
@@ -241,6 +242,51 @@ __global__ void k_mb_inv(int iters, uint32_t* out) {
   store_f<Fq>(out + 12 * (size_t)t, a);
 }
 
+// one wave per 64 threads, `iters` dependent wave-cooperative inverses
+__global__ void __launch_bounds__(64) k_mb_inv_wave(int iters, uint32_t* out) {
+  const uint32_t w = blockIdx.x;
+  Fq a = Fq::one();
+  a.v[0] ^= w * 0x9E3779B9u;
+  a.v[3] ^= w;
+  for (int i = 0; i < iters; i++) {
+    a = inv_w(a);
+    a.v[1] ^= 1u;
+  }
+  if (threadIdx.x == 0) store_f<Fq>(out + 12 * (size_t)w, a);
+}
+
+// inverses of n Montgomery-form Fq values by both inverse routines
+__global__ void __launch_bounds__(64) k_selftest_inv(const uint32_t* __restrict__ in, uint32_t* __restrict__ o_lane,
+                                                     uint32_t* __restrict__ o_wave, size_t n) {
+  const size_t i = blockIdx.x;
+  if (i >= n) return;
+  const Fq a = load_f<Fq>(in + 12 * i);
+  const Fq rw = inv_w(a);
+  if (threadIdx.x == 0) {
+    store_f<Fq>(o_wave + 12 * i, rw);
+    store_f<Fq>(o_lane + 12 * i, inv(a));
+  }
+}
+
+extern "C" int tpst_selftest_inv(tpst_ctx* ctx, size_t n, const uint64_t* in, uint64_t* out_lane, uint64_t* out_wave) {
+  if (!ctx || (n && (!in || !out_lane || !out_wave))) return fail(ctx, TPST_E_ARG, "bad argument");
+  if (!n) return TPST_OK;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
+  ctx->io.reset();
+  TPST_HIP(ctx, ctx->io.reserve(3 * Arena::need(n * 12, 4)));
+  uint32_t* d_in = ctx->io.take<uint32_t>(n * 12);
+  uint32_t* d_l = ctx->io.take<uint32_t>(n * 12);
+  uint32_t* d_w = ctx->io.take<uint32_t>(n * 12);
+  TPST_HIP(ctx, hipMemcpyAsync(d_in, in, n * 48, hipMemcpyHostToDevice, ctx->stream));
+  k_selftest_inv<<<(unsigned)n, 64, 0, ctx->stream>>>(d_in, d_l, d_w, n);
+  TPST_HIP(ctx, hipGetLastError());
+  TPST_HIP(ctx, hipMemcpyAsync(out_lane, d_l, n * 48, hipMemcpyDeviceToHost, ctx->stream));
+  TPST_HIP(ctx, hipMemcpyAsync(out_wave, d_w, n * 48, hipMemcpyDeviceToHost, ctx->stream));
+  TPST_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return TPST_OK;
+}
+
 // one wave running `iters` stages of wave-engine op `op` (wave_tower.h)
 __global__ void __launch_bounds__(64) k_mb_wave(int op, int iters, uint32_t* out) {
   extern __shared__ uint4 smem4[];
@@ -424,6 +470,8 @@ extern "C" int tpst_microbench(tpst_ctx* ctx, int kind, size_t threads, int iter
     k_mb_insn<11><<<grid, bs, 0, ctx->stream>>>(iters, d);
   else if (kind == 12 || kind == 14)
     k_mb_fq29<<<grid, bs, 0, ctx->stream>>>(kind == 14, iters, d);
+  else if (kind == 15)
+    k_mb_inv_wave<<<grid_for(threads, 64), 64, 0, ctx->stream>>>(iters, d);
   else if (kind == 13)
     k_mb_madd29<<<grid, bs, 0, ctx->stream>>>(iters, d);
   else if (kind >= 16 && kind < 16 + wave::N_OPS) {

@@ -7,6 +7,7 @@
 #include "pair_fq2.h"
 #include "glv.h"
 #include "acc_field.h"
+#include "inv_wave.h"
 #include <type_traits>
 
 namespace tpst {
@@ -1066,6 +1067,27 @@ __global__ void __launch_bounds__(64, 1) k_xyzz_to_affine_canonical(const Xyzz<F
   store_affine(out, i, a);
 }
 
+// the same with one wave per point and the wave-cooperative inverse
+// (inv_wave.h): for the few-point conversions on a latency path
+template <class F>
+__global__ void __launch_bounds__(64) k_xyzz_to_affine_wave(const Xyzz<F>* __restrict__ in, uint32_t* __restrict__ out, size_t n) {
+  const size_t i = blockIdx.x;
+  if (i >= n) return;
+  Affine<F> a = to_affine_w(load_xyzz(in, i));
+  Fq* c = reinterpret_cast<Fq*>(&a);
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(Affine<F>) / sizeof(Fq)); k++) c[k] = from_mont(c[k]);
+  if (threadIdx.x == 0) store_affine(out, i, a);
+}
+
+static size_t inv_wave_max() {
+  static const size_t v = [] {
+    const char* e = getenv("TPST_INV_WAVE_MAX");
+    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)4096;
+  }();
+  return v;
+}
+
 template <class F>
 hipError_t points_to_mont(hipStream_t s, const uint32_t* d_in, uint32_t* d_out, size_t n) {
   if (!n) return hipSuccess;
@@ -1083,7 +1105,10 @@ hipError_t affine_from_mont(hipStream_t s, const uint32_t* d_in, uint32_t* d_out
 template <class F>
 hipError_t xyzz_to_affine_canonical(hipStream_t s, const Xyzz<F>* d_in, uint32_t* d_out, size_t n) {
   if (!n) return hipSuccess;
-  k_xyzz_to_affine_canonical<F><<<grid_for(n, 64), 64, 0, s>>>(d_in, d_out, n);
+  if (n <= inv_wave_max())
+    k_xyzz_to_affine_wave<F><<<(unsigned)n, 64, 0, s>>>(d_in, d_out, n);
+  else
+    k_xyzz_to_affine_canonical<F><<<grid_for(n, 64), 64, 0, s>>>(d_in, d_out, n);
   return hipGetLastError();
 }
 

@@ -8,6 +8,7 @@
 #include "pairing_kernels.h"
 #include "wave_tower.h"
 #include "rns_engine.h"
+#include "inv_wave.h"
 #include <cstdlib>
 
 namespace tpst {
@@ -645,7 +646,10 @@ __device__ int rc_final_exp(const rns::Eng& e, const rns::Lane& L, int F, int re
   stage<OP_INV4>(e, L, I + 12, 0, I + 14);   // Fq2 norm n
   store(e, L, I + 14, sh_n, sh_n + 1, 1);
   const int lane = threadIdx.x & 63;
-  if (wave_id() == 0 && (lane & 31) == 0) sh_n[lane >> 5] = inv(sh_n[lane >> 5]);
+  if (wave_id() < 2) {  // one chain's norm per wave, wave-cooperative inverse
+    const Fq ni = inv_w(sh_n[wave_id()]);
+    if (lane == 0) sh_n[wave_id()] = ni;
+  }
   __syncthreads();
   load(e, L, sh_n, sh_n + 1, I + 15, 1);
   stage<OP_INV5>(e, L, I + 12, I + 15, I + 16);  // t'^-1

@@ -191,15 +191,130 @@ Fq hmul3(const Fq& a0, const Fq& b0, const Fq& a1, const Fq& b1, const Fq& a2, c
   return out;
 }
 
+// Montgomery square: the 21 distinct limb products (cross products doubled),
+// then a word-by-word REDC -- the S-box's x^2, x^4, x^8, x^16
+Fq hsqr(const Fq& a) {
+  typedef unsigned __int128 u128;
+  const HostP64& P = hp64();
+  uint64_t x[6];
+  memcpy(x, a.v, 48);
+  uint64_t t[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < 5; i++) {
+    u128 c = 0;
+    for (int j = i + 1; j < 6; j++) {
+      c += (u128)x[i] * x[j] + t[i + j];
+      t[i + j] = (uint64_t)c;
+      c >>= 64;
+    }
+    t[i + 6] = (uint64_t)c;
+  }
+  for (int i = 11; i > 0; i--) t[i] = (t[i] << 1) | (t[i - 1] >> 63);
+  t[0] <<= 1;
+  u128 c = 0;
+  for (int i = 0; i < 6; i++) {
+    const u128 sq = (u128)x[i] * x[i];
+    c += (u128)t[2 * i] + (uint64_t)sq;
+    t[2 * i] = (uint64_t)c;
+    c >>= 64;
+    c += (u128)t[2 * i + 1] + (uint64_t)(sq >> 64);
+    t[2 * i + 1] = (uint64_t)c;
+    c >>= 64;
+  }
+  for (int i = 0; i < 6; i++) {  // REDC
+    const uint64_t m = t[i] * P.inv;
+    u128 d = 0;
+    for (int j = 0; j < 6; j++) {
+      d += (u128)m * P.p[j] + t[i + j];
+      t[i + j] = (uint64_t)d;
+      d >>= 64;
+    }
+    for (int j = i + 6; j < 13 && d; j++) {
+      d += t[j];
+      t[j] = (uint64_t)d;
+      d >>= 64;
+    }
+  }
+  uint64_t r[6];
+  u128 br = 0;
+  for (int j = 0; j < 6; j++) {
+    const u128 d = (u128)t[6 + j] - P.p[j] - (uint64_t)br;
+    r[j] = (uint64_t)d;
+    br = (d >> 64) & 1;
+  }
+  const bool ge = t[12] || !br;
+  Fq out;
+  memcpy(out.v, ge ? r : t + 6, 48);
+  return out;
+}
+
+// x^17 (alpha = 17)
+Fq sbox17(const Fq& x) { return hmul(hsqr(hsqr(hsqr(hsqr(x)))), x); }
+
 // ------------------------------------------------------------ Poseidon ----
+// The permutation is evaluated in the equivalent form of the Poseidon paper's
+// appendix B (same outputs, fewer products), derived once from the sponge's
+// parameters:
+//  - partial-round constants: a partial round's S-box touches only element 0,
+//    so M S(x + c) = M S(x + c_0 e_0) + M (0, c_1, c_2): the second term is
+//    carried into the next round's constants; after the last partial round it
+//    lands in the first closing full round's;
+//  - sparse partial-round matrices: the round matrix M_r = M' M'' with
+//    M'' = [[a, b^T], [D^-1 c, I]] and M' = diag(1, D); M' leaves element 0
+//    alone, so it commutes with the next partial S-box and its e_0 constant
+//    and is folded into the next round's matrix (M_{r+1} = M M').  30 partial
+//    rounds apply a 5-product M''; the last applies its dense M_r.
 struct PoseidonParams {
-  Fq ark[39][3];
+  static constexpr int RF0 = 4, RP = 31, RN = 39;  // full rounds 0..3 and 35..38
+  Fq ark[RN][3];
   Fq mds[3][3];
+  Fq sp[RP - 1][5];  // sparse rounds: a, b1, b2, w1, w2
+  Fq last[3][3];     // dense matrix of the last partial round
+  static Fq finv(const Fq& a) {  // a^(p-2), one-time
+    const HostP64& P = hp64();
+    uint64_t e[6];
+    memcpy(e, P.p, 48);
+    e[0] -= 2;
+    Fq r = Fq::one(), b = a;
+    for (int i = 0; i < 377; i++) {
+      if ((e[i >> 6] >> (i & 63)) & 1) r = hmul(r, b);
+      b = hsqr(b);
+    }
+    return r;
+  }
+  static void mat_mul(const Fq (*x)[3], const Fq (*y)[3], Fq (*z)[3]) {
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) z[i][j] = hmul3(x[i][0], y[0][j], x[i][1], y[1][j], x[i][2], y[2][j]);
+  }
   PoseidonParams() {
-    for (int r = 0; r < 39; r++)
+    for (int r = 0; r < RN; r++)
       for (int i = 0; i < 3; i++) ark[r][i] = fq_canon(POSEIDON_ARK[r][i]);
     for (int i = 0; i < 3; i++)
       for (int j = 0; j < 3; j++) mds[i][j] = fq_canon(POSEIDON_MDS[i][j]);
+    const Fq z = Fq::zero();
+    for (int r = RF0; r < RF0 + RP; r++) {  // constants 1, 2 of partial rounds -> next round
+      for (int i = 0; i < 3; i++)
+        ark[r + 1][i] = add(ark[r + 1][i], hmul3(mds[i][0], z, mds[i][1], ark[r][1], mds[i][2], ark[r][2]));
+      ark[r][1] = ark[r][2] = z;
+    }
+    Fq cur[3][3];
+    memcpy(cur, mds, sizeof(cur));
+    for (int k = 0; k < RP - 1; k++) {
+      // cur = [[a, b^T], [c, D]]: w = D^-1 c
+      const Fq det = sub(hmul(cur[1][1], cur[2][2]), hmul(cur[1][2], cur[2][1]));
+      const Fq di = finv(det);
+      const Fq w1 = hmul(di, sub(hmul(cur[2][2], cur[1][0]), hmul(cur[1][2], cur[2][0])));
+      const Fq w2 = hmul(di, sub(hmul(cur[1][1], cur[2][0]), hmul(cur[2][1], cur[1][0])));
+      sp[k][0] = cur[0][0];
+      sp[k][1] = cur[0][1];
+      sp[k][2] = cur[0][2];
+      sp[k][3] = w1;
+      sp[k][4] = w2;
+      Fq mp[3][3] = {{Fq::one(), z, z}, {z, cur[1][1], cur[1][2]}, {z, cur[2][1], cur[2][2]}};
+      Fq nx[3][3];
+      mat_mul(mds, mp, nx);
+      memcpy(cur, nx, sizeof(cur));
+    }
+    memcpy(last, cur, sizeof(last));
   }
 };
 const PoseidonParams& pparams() {
@@ -223,19 +338,29 @@ struct Sponge {
     t->squeezing = squeezing ? 1 : 0;
     t->index = (uint32_t)idx;
   }
+  void full_round(const PoseidonParams& P, int r) {
+    Fq x[3];
+    for (int i = 0; i < 3; i++) x[i] = sbox17(add(st[i], P.ark[r][i]));
+    for (int i = 0; i < 3; i++) st[i] = hmul3(P.mds[i][0], x[0], P.mds[i][1], x[1], P.mds[i][2], x[2]);
+  }
   void permute() {
     const PoseidonParams& P = pparams();
-    for (int r = 0; r < 39; r++) {
-      for (int i = 0; i < 3; i++) st[i] = add(st[i], P.ark[r][i]);
-      const bool full = r < 4 || r >= 35;
-      for (int i = 0; i < (full ? 3 : 1); i++) {
-        const Fq x = st[i], x2 = hmul(x, x), x4 = hmul(x2, x2), x8 = hmul(x4, x4), x16 = hmul(x8, x8);
-        st[i] = hmul(x16, x);
-      }
+    for (int r = 0; r < P.RF0; r++) full_round(P, r);
+    for (int k = 0; k < P.RP - 1; k++) {
+      const Fq* m = P.sp[k];
+      const Fq x0 = sbox17(add(st[0], P.ark[P.RF0 + k][0]));
+      const Fq n0 = hmul3(m[0], x0, m[1], st[1], m[2], st[2]);
+      st[1] = add(st[1], hmul(m[3], x0));
+      st[2] = add(st[2], hmul(m[4], x0));
+      st[0] = n0;
+    }
+    {
+      const Fq x0 = sbox17(add(st[0], P.ark[P.RF0 + P.RP - 1][0]));
       Fq ns[3];
-      for (int i = 0; i < 3; i++) ns[i] = hmul3(P.mds[i][0], st[0], P.mds[i][1], st[1], P.mds[i][2], st[2]);
+      for (int i = 0; i < 3; i++) ns[i] = hmul3(P.last[i][0], x0, P.last[i][1], st[1], P.last[i][2], st[2]);
       for (int i = 0; i < 3; i++) st[i] = ns[i];
     }
+    for (int r = P.RF0 + P.RP; r < P.RN; r++) full_round(P, r);
   }
   void absorb(const std::vector<Fq>& e) {
     if (e.empty()) return;

@@ -169,6 +169,15 @@ class Context:
         self.check(self.lib.tpst_microbench(self.h, kind, threads, iters, C.byref(ms)), "tpst_microbench")
         return ms.value
 
+    def selftest_inv(self, vals: np.ndarray):
+        """device Fq inverses of Montgomery-form values (n x 6 words) by the
+        lone-lane and the wave-cooperative routine"""
+        vals = np.ascontiguousarray(vals, dtype=np.uint64).reshape(-1, 6)
+        ol = np.zeros_like(vals)
+        ow = np.zeros_like(vals)
+        self.check(self.lib.tpst_selftest_inv(self.h, len(vals), ptr(vals), ptr(ol), ptr(ow)), "tpst_selftest_inv")
+        return ol, ow
+
 
 class Gens:
     """MultiCommitGens {n, G, h} (commitments.rs:9-15) resident on the device,
