@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "curve.h"
+#include "field29.h"
 
 namespace tpst {
 namespace host {
@@ -140,19 +141,9 @@ inline HFq mul(const HFq& a, const HFq& b) {
 
 inline HFq sqr(const HFq& a) { return mul(a, a); }
 
-// a^(p-2) (Fermat); 0 -> 0
-inline HFq inv(const HFq& a) {
-  const Mod64& P = mod64();
-  uint64_t e[6];
-  memcpy(e, P.p, 48);
-  e[0] -= 2;  // p = 1 mod 2^64: no borrow
-  HFq r = HFq::one();
-  for (int i = 377; i >= 0; i--) {
-    r = sqr(r);
-    if ((e[i >> 6] >> (i & 63)) & 1) r = mul(r, a);
-  }
-  return r;
-}
+// a^-1 (0 -> 0): field29.h's binary GCD (batches of 29 divsteps on 13-limb
+// values) runs ~6x faster here than the Fermat power by host products
+inline HFq inv(const HFq& a) { return HFq::from(tpst::inv(a.to())); }
 
 // Fq2 = Fq[u] / (u^2 + 5)
 struct HFq2 {

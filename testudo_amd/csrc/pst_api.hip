@@ -20,23 +20,13 @@
 #include "device_util.h"
 #include "pst_kernels.h"
 #include "trace.h"
+#include "poseidon_host.h"
 
 using namespace tpst;
-
-#include "poseidon_constants.inc"
 
 // =================================================================== host ==
 namespace {
 
-Fq fq_canon(const uint64_t* c) {  // canonical u64 limbs -> Montgomery
-  Fq a;
-  memcpy(a.v, c, 48);
-  return to_mont(a);
-}
-void fq_out(const Fq& a, uint64_t* c) {
-  Fq r = from_mont(a);
-  memcpy(c, r.v, 48);
-}
 Fr fr_canon(const uint64_t* c) {
   Fr a;
   memcpy(a.v, c, 32);
@@ -55,384 +45,6 @@ static bool open_trace() {
   static const bool on = getenv("TPST_OPEN_TRACE") != nullptr;
   return on;
 }
-
-// 64-bit-limb host Montgomery product (CIOS, unsigned __int128) on the same
-// bits as Fq (6 x u64 = 12 x u32, R = 2^384 either way): the transcript's
-// Poseidon permutations run ~17 per MIPP round on the host, between device
-// phases, so their multiplications sit on the open's critical path.
-struct HostP64 {
-  uint64_t p[6];
-  uint64_t inv;  // -p^-1 mod 2^64
-  HostP64() {
-    for (int i = 0; i < 6; i++) p[i] = (uint64_t)params::FQ_P[2 * i] | ((uint64_t)params::FQ_P[2 * i + 1] << 32);
-    uint64_t x = 1;
-    for (int i = 0; i < 7; i++) x *= 2 - p[0] * x;  // Newton: x = p^-1 mod 2^64
-    inv = 0 - x;
-  }
-};
-const HostP64& hp64() {
-  static HostP64 h;
-  return h;
-}
-
-// no-carry CIOS (p's top word < 2^62: the running value fits 6 words + the
-// carry word of each row), fully unrolled over the 6 words of b
-Fq hmul(const Fq& a, const Fq& b) {
-  typedef unsigned __int128 u128;
-  const HostP64& P = hp64();
-  uint64_t x[6], y[6];
-  memcpy(x, a.v, 48);
-  memcpy(y, b.v, 48);
-  uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0, t5 = 0;
-#define TPST_HMUL_ROW(i)                                                              \
-  {                                                                                   \
-    const uint64_t yi = y[i];                                                         \
-    u128 c = (u128)x[0] * yi + t0;                                                    \
-    const uint64_t a0 = (uint64_t)c;                                                  \
-    uint64_t A = (uint64_t)(c >> 64);                                                 \
-    const uint64_t m = a0 * P.inv;                                                    \
-    u128 d = (u128)m * P.p[0] + a0;                                                   \
-    uint64_t C = (uint64_t)(d >> 64);                                                 \
-    c = (u128)x[1] * yi + t1 + A;                                                     \
-    A = (uint64_t)(c >> 64);                                                          \
-    d = (u128)m * P.p[1] + (uint64_t)c + C;                                           \
-    C = (uint64_t)(d >> 64);                                                          \
-    t0 = (uint64_t)d;                                                                 \
-    c = (u128)x[2] * yi + t2 + A;                                                     \
-    A = (uint64_t)(c >> 64);                                                          \
-    d = (u128)m * P.p[2] + (uint64_t)c + C;                                           \
-    C = (uint64_t)(d >> 64);                                                          \
-    t1 = (uint64_t)d;                                                                 \
-    c = (u128)x[3] * yi + t3 + A;                                                     \
-    A = (uint64_t)(c >> 64);                                                          \
-    d = (u128)m * P.p[3] + (uint64_t)c + C;                                           \
-    C = (uint64_t)(d >> 64);                                                          \
-    t2 = (uint64_t)d;                                                                 \
-    c = (u128)x[4] * yi + t4 + A;                                                     \
-    A = (uint64_t)(c >> 64);                                                          \
-    d = (u128)m * P.p[4] + (uint64_t)c + C;                                           \
-    C = (uint64_t)(d >> 64);                                                          \
-    t3 = (uint64_t)d;                                                                 \
-    c = (u128)x[5] * yi + t5 + A;                                                     \
-    A = (uint64_t)(c >> 64);                                                          \
-    d = (u128)m * P.p[5] + (uint64_t)c + C;                                           \
-    C = (uint64_t)(d >> 64);                                                          \
-    t4 = (uint64_t)d;                                                                 \
-    t5 = C + A;                                                                       \
-  }
-  TPST_HMUL_ROW(0) TPST_HMUL_ROW(1) TPST_HMUL_ROW(2) TPST_HMUL_ROW(3) TPST_HMUL_ROW(4) TPST_HMUL_ROW(5)
-#undef TPST_HMUL_ROW
-  // t < 2p: one conditional subtraction
-  const uint64_t t[6] = {t0, t1, t2, t3, t4, t5};
-  uint64_t r[6];
-  u128 br = 0;
-  for (int j = 0; j < 6; j++) {
-    const u128 dd = (u128)t[j] - P.p[j] - (uint64_t)br;
-    r[j] = (uint64_t)dd;
-    br = (dd >> 64) & 1;
-  }
-  Fq out;
-  memcpy(out.v, br ? t : r, 48);
-  return out;
-}
-
-// sum of three Montgomery products with one reduction: the 768-bit products
-// are added unreduced (3 p^2 < p R) and reduced once, so an MDS row costs
-// three multiplications and one REDC instead of three of each
-Fq hmul3(const Fq& a0, const Fq& b0, const Fq& a1, const Fq& b1, const Fq& a2, const Fq& b2) {
-  typedef unsigned __int128 u128;
-  const HostP64& P = hp64();
-  uint64_t t[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  const Fq* as[3] = {&a0, &a1, &a2};
-  const Fq* bs[3] = {&b0, &b1, &b2};
-  for (int k = 0; k < 3; k++) {
-    uint64_t x[6], y[6];
-    memcpy(x, as[k]->v, 48);
-    memcpy(y, bs[k]->v, 48);
-    for (int i = 0; i < 6; i++) {
-      u128 c = 0;
-      for (int j = 0; j < 6; j++) {
-        c += (u128)x[j] * y[i] + t[i + j];
-        t[i + j] = (uint64_t)c;
-        c >>= 64;
-      }
-      for (int j = i + 6; j < 13 && c; j++) {
-        c += t[j];
-        t[j] = (uint64_t)c;
-        c >>= 64;
-      }
-    }
-  }
-  for (int i = 0; i < 6; i++) {  // REDC, word by word
-    const uint64_t m = t[i] * P.inv;
-    u128 c = 0;
-    for (int j = 0; j < 6; j++) {
-      c += (u128)m * P.p[j] + t[i + j];
-      t[i + j] = (uint64_t)c;
-      c >>= 64;
-    }
-    for (int j = i + 6; j < 13 && c; j++) {
-      c += t[j];
-      t[j] = (uint64_t)c;
-      c >>= 64;
-    }
-  }
-  // (T + M p) / R < 2p: one conditional subtraction of t[6..12]
-  uint64_t r[6];
-  u128 br = 0;
-  for (int j = 0; j < 6; j++) {
-    const u128 d = (u128)t[6 + j] - P.p[j] - (uint64_t)br;
-    r[j] = (uint64_t)d;
-    br = (d >> 64) & 1;
-  }
-  const bool ge = t[12] || !br;
-  Fq out;
-  memcpy(out.v, ge ? r : t + 6, 48);
-  return out;
-}
-
-// Montgomery square: the 21 distinct limb products (cross products doubled),
-// then a word-by-word REDC -- the S-box's x^2, x^4, x^8, x^16
-Fq hsqr(const Fq& a) {
-  typedef unsigned __int128 u128;
-  const HostP64& P = hp64();
-  uint64_t x[6];
-  memcpy(x, a.v, 48);
-  uint64_t t[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  for (int i = 0; i < 5; i++) {
-    u128 c = 0;
-    for (int j = i + 1; j < 6; j++) {
-      c += (u128)x[i] * x[j] + t[i + j];
-      t[i + j] = (uint64_t)c;
-      c >>= 64;
-    }
-    t[i + 6] = (uint64_t)c;
-  }
-  for (int i = 11; i > 0; i--) t[i] = (t[i] << 1) | (t[i - 1] >> 63);
-  t[0] <<= 1;
-  u128 c = 0;
-  for (int i = 0; i < 6; i++) {
-    const u128 sq = (u128)x[i] * x[i];
-    c += (u128)t[2 * i] + (uint64_t)sq;
-    t[2 * i] = (uint64_t)c;
-    c >>= 64;
-    c += (u128)t[2 * i + 1] + (uint64_t)(sq >> 64);
-    t[2 * i + 1] = (uint64_t)c;
-    c >>= 64;
-  }
-  for (int i = 0; i < 6; i++) {  // REDC
-    const uint64_t m = t[i] * P.inv;
-    u128 d = 0;
-    for (int j = 0; j < 6; j++) {
-      d += (u128)m * P.p[j] + t[i + j];
-      t[i + j] = (uint64_t)d;
-      d >>= 64;
-    }
-    for (int j = i + 6; j < 13 && d; j++) {
-      d += t[j];
-      t[j] = (uint64_t)d;
-      d >>= 64;
-    }
-  }
-  uint64_t r[6];
-  u128 br = 0;
-  for (int j = 0; j < 6; j++) {
-    const u128 d = (u128)t[6 + j] - P.p[j] - (uint64_t)br;
-    r[j] = (uint64_t)d;
-    br = (d >> 64) & 1;
-  }
-  const bool ge = t[12] || !br;
-  Fq out;
-  memcpy(out.v, ge ? r : t + 6, 48);
-  return out;
-}
-
-// x^17 (alpha = 17)
-Fq sbox17(const Fq& x) { return hmul(hsqr(hsqr(hsqr(hsqr(x)))), x); }
-
-// ------------------------------------------------------------ Poseidon ----
-// The permutation is evaluated in the equivalent form of the Poseidon paper's
-// appendix B (same outputs, fewer products), derived once from the sponge's
-// parameters:
-//  - partial-round constants: a partial round's S-box touches only element 0,
-//    so M S(x + c) = M S(x + c_0 e_0) + M (0, c_1, c_2): the second term is
-//    carried into the next round's constants; after the last partial round it
-//    lands in the first closing full round's;
-//  - sparse partial-round matrices: the round matrix M_r = M' M'' with
-//    M'' = [[a, b^T], [D^-1 c, I]] and M' = diag(1, D); M' leaves element 0
-//    alone, so it commutes with the next partial S-box and its e_0 constant
-//    and is folded into the next round's matrix (M_{r+1} = M M').  30 partial
-//    rounds apply a 5-product M''; the last applies its dense M_r.
-struct PoseidonParams {
-  static constexpr int RF0 = 4, RP = 31, RN = 39;  // full rounds 0..3 and 35..38
-  Fq ark[RN][3];
-  Fq mds[3][3];
-  Fq sp[RP - 1][5];  // sparse rounds: a, b1, b2, w1, w2
-  Fq last[3][3];     // dense matrix of the last partial round
-  static Fq finv(const Fq& a) {  // a^(p-2), one-time
-    const HostP64& P = hp64();
-    uint64_t e[6];
-    memcpy(e, P.p, 48);
-    e[0] -= 2;
-    Fq r = Fq::one(), b = a;
-    for (int i = 0; i < 377; i++) {
-      if ((e[i >> 6] >> (i & 63)) & 1) r = hmul(r, b);
-      b = hsqr(b);
-    }
-    return r;
-  }
-  static void mat_mul(const Fq (*x)[3], const Fq (*y)[3], Fq (*z)[3]) {
-    for (int i = 0; i < 3; i++)
-      for (int j = 0; j < 3; j++) z[i][j] = hmul3(x[i][0], y[0][j], x[i][1], y[1][j], x[i][2], y[2][j]);
-  }
-  PoseidonParams() {
-    for (int r = 0; r < RN; r++)
-      for (int i = 0; i < 3; i++) ark[r][i] = fq_canon(POSEIDON_ARK[r][i]);
-    for (int i = 0; i < 3; i++)
-      for (int j = 0; j < 3; j++) mds[i][j] = fq_canon(POSEIDON_MDS[i][j]);
-    const Fq z = Fq::zero();
-    for (int r = RF0; r < RF0 + RP; r++) {  // constants 1, 2 of partial rounds -> next round
-      for (int i = 0; i < 3; i++)
-        ark[r + 1][i] = add(ark[r + 1][i], hmul3(mds[i][0], z, mds[i][1], ark[r][1], mds[i][2], ark[r][2]));
-      ark[r][1] = ark[r][2] = z;
-    }
-    Fq cur[3][3];
-    memcpy(cur, mds, sizeof(cur));
-    for (int k = 0; k < RP - 1; k++) {
-      // cur = [[a, b^T], [c, D]]: w = D^-1 c
-      const Fq det = sub(hmul(cur[1][1], cur[2][2]), hmul(cur[1][2], cur[2][1]));
-      const Fq di = finv(det);
-      const Fq w1 = hmul(di, sub(hmul(cur[2][2], cur[1][0]), hmul(cur[1][2], cur[2][0])));
-      const Fq w2 = hmul(di, sub(hmul(cur[1][1], cur[2][0]), hmul(cur[2][1], cur[1][0])));
-      sp[k][0] = cur[0][0];
-      sp[k][1] = cur[0][1];
-      sp[k][2] = cur[0][2];
-      sp[k][3] = w1;
-      sp[k][4] = w2;
-      Fq mp[3][3] = {{Fq::one(), z, z}, {z, cur[1][1], cur[1][2]}, {z, cur[2][1], cur[2][2]}};
-      Fq nx[3][3];
-      mat_mul(mds, mp, nx);
-      memcpy(cur, nx, sizeof(cur));
-    }
-    memcpy(last, cur, sizeof(last));
-  }
-};
-const PoseidonParams& pparams() {
-  static PoseidonParams p;
-  return p;
-}
-
-// ark-crypto-primitives PoseidonSponge<Fq>: rate 2, capacity 1, alpha 17,
-// 8 full + 31 partial rounds (parameters.rs:309-338)
-struct Sponge {
-  Fq st[3];
-  bool squeezing;
-  int idx;
-  void load(const tpst_transcript* t) {
-    for (int i = 0; i < 3; i++) st[i] = fq_canon(t->state[i]);
-    squeezing = t->squeezing != 0;
-    idx = (int)t->index;
-  }
-  void store(tpst_transcript* t) const {
-    for (int i = 0; i < 3; i++) fq_out(st[i], t->state[i]);
-    t->squeezing = squeezing ? 1 : 0;
-    t->index = (uint32_t)idx;
-  }
-  void full_round(const PoseidonParams& P, int r) {
-    Fq x[3];
-    for (int i = 0; i < 3; i++) x[i] = sbox17(add(st[i], P.ark[r][i]));
-    for (int i = 0; i < 3; i++) st[i] = hmul3(P.mds[i][0], x[0], P.mds[i][1], x[1], P.mds[i][2], x[2]);
-  }
-  void permute() {
-    const PoseidonParams& P = pparams();
-    for (int r = 0; r < P.RF0; r++) full_round(P, r);
-    for (int k = 0; k < P.RP - 1; k++) {
-      const Fq* m = P.sp[k];
-      const Fq x0 = sbox17(add(st[0], P.ark[P.RF0 + k][0]));
-      const Fq n0 = hmul3(m[0], x0, m[1], st[1], m[2], st[2]);
-      st[1] = add(st[1], hmul(m[3], x0));
-      st[2] = add(st[2], hmul(m[4], x0));
-      st[0] = n0;
-    }
-    {
-      const Fq x0 = sbox17(add(st[0], P.ark[P.RF0 + P.RP - 1][0]));
-      Fq ns[3];
-      for (int i = 0; i < 3; i++) ns[i] = hmul3(P.last[i][0], x0, P.last[i][1], st[1], P.last[i][2], st[2]);
-      for (int i = 0; i < 3; i++) st[i] = ns[i];
-    }
-    for (int r = P.RF0 + P.RP; r < P.RN; r++) full_round(P, r);
-  }
-  void absorb(const std::vector<Fq>& e) {
-    if (e.empty()) return;
-    int i0;
-    if (!squeezing) {
-      i0 = idx;
-      if (i0 == 2) {
-        permute();
-        i0 = 0;
-      }
-    } else {
-      permute();
-      i0 = 0;
-    }
-    size_t k = 0;
-    for (;;) {
-      const size_t rem = e.size() - k;
-      if (i0 + rem <= 2) {
-        for (size_t j = 0; j < rem; j++) st[1 + i0 + j] = add(st[1 + i0 + j], e[k + j]);
-        squeezing = false;
-        idx = i0 + (int)rem;
-        return;
-      }
-      const int take = 2 - i0;
-      for (int j = 0; j < take; j++) st[1 + i0 + j] = add(st[1 + i0 + j], e[k + j]);
-      permute();
-      k += take;
-      i0 = 0;
-    }
-  }
-  // Absorb for Vec<u8>: u64 LE length prefix, 47-byte chunks -> Fq
-  void absorb_bytes(const uint8_t* d, size_t n) {
-    std::vector<uint8_t> buf(8 + n);
-    const uint64_t len = n;
-    memcpy(buf.data(), &len, 8);
-    if (n) memcpy(buf.data() + 8, d, n);
-    std::vector<Fq> e;
-    for (size_t o = 0; o < buf.size(); o += 47) {
-      uint64_t l[6] = {0, 0, 0, 0, 0, 0};
-      const size_t m = buf.size() - o < 47 ? buf.size() - o : 47;
-      memcpy(l, buf.data() + o, m);
-      e.push_back(fq_canon(l));
-    }
-    absorb(e);
-  }
-  Fq squeeze1() {
-    int i0;
-    if (!squeezing) {
-      permute();
-      i0 = 0;
-    } else {
-      i0 = idx;
-      if (i0 == 2) {
-        permute();
-        i0 = 0;
-      }
-    }
-    const Fq out = st[1 + i0];
-    squeezing = true;
-    idx = i0 + 1;
-    return out;
-  }
-  // non-native squeeze_field_elements::<Fr>(1): low 252 bits of one Fq
-  void challenge(uint64_t* fr_canon_out) {
-    uint64_t c[6];
-    fq_out(squeeze1(), c);
-    fr_canon_out[0] = c[0];
-    fr_canon_out[1] = c[1];
-    fr_canon_out[2] = c[2];
-    fr_canon_out[3] = c[3] & ((1ull << 60) - 1);
-  }
-};
 
 // y > -y on canonical limbs  <=>  2y > p
 bool y_is_negative(const uint64_t* y) {
@@ -463,6 +75,22 @@ void g1_bytes(const uint64_t* p, uint8_t* b) {  // ark serialize Compress::No
 
 // host Fr helpers
 Fr fr_inv(const Fr& a) { return inv(a); }
+
+// device XYZZ points (field.h Montgomery limbs, the same bits as host::HFq)
+// -> canonical affine on the host: the open's few-point outputs (a round's
+// u_l / u_r, U, final_a, final_h) need one inversion each, ~15 us here
+// against a ~0.1 ms single-point kernel on the round's critical stream
+template <class F>
+void xyzz_to_canonical_host(const uint8_t* raw, size_t n, uint64_t* out) {
+  using H = typename host::HostOf<F>::T;
+  constexpr size_t PT = sizeof(Xyzz<F>), NQ = host::HostOf<F>::NQ;
+  static_assert(sizeof(Xyzz<H>) == PT, "host and device XYZZ layouts differ");
+  for (size_t i = 0; i < n; i++) {
+    Xyzz<H> x;
+    memcpy(&x, raw + i * PT, PT);
+    host::aff_put(to_affine(x), out + i * 12 * NQ);
+  }
+}
 
 // base-x digits of a canonical Fr e (e < r < x^4): e = sum_j out[j] x^j, for
 // the GT exponentiations by Frobenius splitting (pairing.hip k_gt_pow_wave)
@@ -1532,8 +1160,12 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   up_off[m] = off;  // final: c_{m-1}, c_{m-1}^-1, rs (Montgomery Fr), a_rev (canonical Fr)
   off += (2 + m + k) * 32;
   const size_t up_bytes = off;
-  const size_t dn_U = up_bytes, dn_round = dn_U + 96, dn_final = dn_round + (size_t)m * (192 + 1152);
-  const size_t dn_bytes = 96 + (size_t)m * (192 + 1152) + 96 + 192 + (size_t)m * 96 + (size_t)k * 192;
+  // downloads: U, each round's u_l / u_r as raw XYZZ (converted on the host)
+  // and t_l / t_r; final_a, final_h raw; pst_proof_h, pst_proof canonical
+  constexpr size_t X1 = sizeof(Xyzz<Fq>), X2 = sizeof(Xyzz<Fq2>), DN_ROUND = 2 * X1 + 1152;
+  const size_t dn_U = up_bytes, dn_round = dn_U + X1, dn_final = dn_round + (size_t)m * DN_ROUND;
+  const size_t dn_fh = dn_final + X1, dn_ph = dn_fh + X2, dn_pst = dn_ph + (size_t)m * 96;
+  const size_t dn_bytes = X1 + (size_t)m * DN_ROUND + X1 + X2 + (size_t)m * 96 + (size_t)k * 192;
   const size_t n_ev = 8 + 5 * (size_t)m;
   if (int rc = open_streams(ctx, n_ev, up_bytes + dn_bytes)) return rc;
   uint8_t* pin = (uint8_t*)ctx->pinned;
@@ -1567,8 +1199,8 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
 
   // ---- device buffers (allocated before any stream runs: no hipFree mid-open)
   const size_t Ch = C > 1 ? C / 2 : 1;
-  DevBuf up, A, P, Y, chiC, ScA, ScB, ScC, ScD[2], xa, xb, xd, xh, xp, xl[2], LAo[2], Hb[2], Lb[2], gts, canA, canB,
-      canC, canD, pstA, pstB, Wall, Wiall, SqT[2], SqG[2], SqM;
+  DevBuf up, A, P, Y, chiC, ScA, ScB, ScC, ScD[2], xa, xb, xd, xh, xp, xl[2], LAo[2], Hb[2], Lb[2], gts, canA, canC,
+      canD, pstA, pstB, Wall, Wiall, SqT[2], SqG[2], SqM;
   TPST_HIP(ctx, up.alloc(up_bytes));
   TPST_HIP(ctx, Wall.alloc(2 * C * 32));  // round r's 2^r fold weights at offset 2^r - 1
   TPST_HIP(ctx, Wiall.alloc(2 * C * 32));
@@ -1599,7 +1231,6 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   }
   TPST_HIP(ctx, SqM.alloc(128 * MIPP_TAB_F12_BYTES));
   TPST_HIP(ctx, canA.alloc(2 * 576));
-  TPST_HIP(ctx, canB.alloc(2 * 96));
   TPST_HIP(ctx, canC.alloc((size_t)(m + 1) * 192));
   TPST_HIP(ctx, canD.alloc(96 + (size_t)k * 192));
   TPST_HIP(ctx, pstA.alloc(pst_open_scratch_words(st, m) * 4));
@@ -1634,7 +1265,6 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   // ---- stream B: U = MSM(comm_list, chi(b)) on that table, or the c_u the
   // ranks combined for an opening-only handle
   if (p->has_u) {
-    memcpy(pin + dn_U, p->U, 96);
     TPST_HIP(ctx, hipEventRecord(ev[EV_U], sB));
   } else {
     TPST_HIP(ctx, hipStreamWaitEvent(sB, ev[EV_TABLE], 0));
@@ -1645,9 +1275,8 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     gu.L = gu.D = C;
     gu.glv = true;
     TPST_HIP(ctx, fbt_msm<Fq>(arB, sB, tA, chiC.u(), gu, (Xyzz<Fq>*)xd.p));
-    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(sB, (Xyzz<Fq>*)xd.p, canD.u(), 1));
     pf.end(ST_MSM_U, sB);
-    TPST_HIP(ctx, hipMemcpyAsync(pin + dn_U, canD.p, 96, hipMemcpyDeviceToHost, sB));
+    TPST_HIP(ctx, hipMemcpyAsync(pin + dn_U, xd.p, X1, hipMemcpyDeviceToHost, sB));
     TPST_HIP(ctx, hipEventRecord(ev[EV_U], sB));
   }
   // PST proof of q at a_rev (stream B, after round 0's cross terms)
@@ -1660,8 +1289,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     Xyzz<Fq2>* x2 = (Xyzz<Fq2>*)xd.p + 1;
     TPST_HIP(ctx, pst_open_fbt_s<Fq2>(sB, arB, st, st->t_php.u(), st->nv - k, p->q.u(), k, dup(a_off), x2, pstB.u()));
     TPST_HIP(ctx, xyzz_to_affine_canonical<Fq2>(sB, x2, canD.u() + 24, k));
-    TPST_HIP(ctx, hipMemcpyAsync(pin + dn_final + 96 + 192 + (size_t)m * 96, canD.u() + 24, (size_t)k * 192,
-                                 hipMemcpyDeviceToHost, sB));
+    TPST_HIP(ctx, hipMemcpyAsync(pin + dn_pst, canD.u() + 24, (size_t)k * 192, hipMemcpyDeviceToHost, sB));
     pf.end(ST_PST_OPEN, sB);
     return TPST_OK;
   };
@@ -1676,6 +1304,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   uint64_t la_digits[16] = {};
   bool have_U = false;
   for (int r = 0; r < m; r++) {  // mipp.rs:58-120
+    const double hq = open_trace() ? host_us() : 0.0;
     const size_t len = C >> r, s = len / 2, nW = (size_t)1 << r;
     // stage c_{r-1}, c_{r-1}^-1, the look-ahead factors and digits; upload
     // once (stream B, whose previous work -- the round's comms_u -- is
@@ -1707,6 +1336,34 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     TPST_HIP(ctx, hipEventRecord(ev_up(r), sB));
     TPST_HIP(ctx, hipStreamWaitEvent(sA, ev_up(r), 0));
 
+    // -- B: y fold by the previous challenge, cross MSMs u_l / u_r
+    // (u_l = a[:s]^y[s:], u_r = a[s:]^y[:s], on the comm_list table); B is
+    // enqueued first: its comms_u gate the transcript, and the look-ahead
+    // enqueue below costs the host tens of launches
+    uint8_t* dn_r = pin + dn_round + (size_t)r * DN_ROUND;
+    TPST_HIP(ctx, hipStreamWaitEvent(sB, ev_up(r), 0));
+    if (r > 0) TPST_HIP(ctx, compress_fr(sB, Y.u(), len, dcp));  // y_l + c' y_r (mipp.rs:124-136)
+    TPST_HIP(ctx, mipp_scalars(sB, dW, Y.u(), len, s, C, ScB.u()));
+    static const bool var0 = getenv("TPST_OPEN_VAR0") != nullptr;
+    if (r == 0 && var0) {
+      // (measured, not kept: round 0's u_l = sum_{k<s} Sc[k] a_k, u_r =
+      // sum_{k>=s} Sc[k] a_k as two variable-base MSMs over comm_list, to take
+      // the GLV fold table build (~1.25 ms at 2^20) off round 0's path -- two
+      // 512-point K2 MSMs took ~3.4 ms, the table path ~1.7 ms)
+      TPST_HIP(ctx, msm_var<Fq>(arB, sB, A.u(), ScB.u(), s, (Xyzz<Fq>*)xb.p));
+      TPST_HIP(ctx, msm_var<Fq>(arB, sB, A.u() + 24 * s, ScB.u() + 8 * s, s, (Xyzz<Fq>*)xb.p + 1));
+    } else {
+      TPST_HIP(ctx, hipStreamWaitEvent(sB, ev[EV_TABLE], 0));
+      FbGroups g;
+      g.groups = 2;
+      g.members = C / len * s;
+      g.L = len;
+      g.D = s;
+      g.glv = true;
+      TPST_HIP(ctx, fbt_msm<Fq>(arB, sB, tA, ScB.u(), g, (Xyzz<Fq>*)xb.p));
+    }
+    TPST_HIP(ctx, hipMemcpyAsync(dn_r, xb.p, 2 * X1, hipMemcpyDeviceToHost, sB));
+    TPST_HIP(ctx, hipEventRecord(ev_b(r), sB));
     // -- A: t_l / t_r of this round
     if (r == 0) {  // direct: the rotated comm_list (affine) against h^(0)
       TPST_HIP(ctx, affine_rot(sA, A.u(), P.u(), C, 24));
@@ -1719,8 +1376,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
                                      (Fq12*)SqM.p, (Fq12*)gts.p));
     }
     TPST_HIP(ctx, fq12_from_mont(sA, (Fq12*)gts.p, canA.u(), 2));
-    uint8_t* dn_r = pin + dn_round + (size_t)r * (192 + 1152);
-    TPST_HIP(ctx, hipMemcpyAsync(dn_r + 192, canA.p, 1152, hipMemcpyDeviceToHost, sA));
+    TPST_HIP(ctx, hipMemcpyAsync(dn_r + 2 * X1, canA.p, 1152, hipMemcpyDeviceToHost, sA));
     TPST_HIP(ctx, hipEventRecord(ev_a(r), sA));
 
     // -- D: look-ahead products of this round's vectors for round r+1
@@ -1761,32 +1417,6 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
       TPST_HIP(ctx, hipEventRecord(ev_la(r), sD));
     }
 
-    // -- B: y fold by the previous challenge, cross MSMs u_l / u_r
-    // (u_l = a[:s]^y[s:], u_r = a[s:]^y[:s], on the comm_list table)
-    TPST_HIP(ctx, hipStreamWaitEvent(sB, ev_up(r), 0));
-    if (r > 0) TPST_HIP(ctx, compress_fr(sB, Y.u(), len, dcp));  // y_l + c' y_r (mipp.rs:124-136)
-    TPST_HIP(ctx, mipp_scalars(sB, dW, Y.u(), len, s, C, ScB.u()));
-    static const bool var0 = getenv("TPST_OPEN_VAR0") != nullptr;
-    if (r == 0 && var0) {
-      // (measured, not kept: round 0's u_l = sum_{k<s} Sc[k] a_k, u_r =
-      // sum_{k>=s} Sc[k] a_k as two variable-base MSMs over comm_list, to take
-      // the GLV fold table build (~1.25 ms at 2^20) off round 0's path -- two
-      // 512-point K2 MSMs took ~3.4 ms, the table path ~1.7 ms)
-      TPST_HIP(ctx, msm_var<Fq>(arB, sB, A.u(), ScB.u(), s, (Xyzz<Fq>*)xb.p));
-      TPST_HIP(ctx, msm_var<Fq>(arB, sB, A.u() + 24 * s, ScB.u() + 8 * s, s, (Xyzz<Fq>*)xb.p + 1));
-    } else {
-      TPST_HIP(ctx, hipStreamWaitEvent(sB, ev[EV_TABLE], 0));
-      FbGroups g;
-      g.groups = 2;
-      g.members = C / len * s;
-      g.L = len;
-      g.D = s;
-      g.glv = true;
-      TPST_HIP(ctx, fbt_msm<Fq>(arB, sB, tA, ScB.u(), g, (Xyzz<Fq>*)xb.p));
-    }
-    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(sB, (Xyzz<Fq>*)xb.p, canB.u(), 2));
-    TPST_HIP(ctx, hipMemcpyAsync(dn_r, canB.p, 192, hipMemcpyDeviceToHost, sB));
-    TPST_HIP(ctx, hipEventRecord(ev_b(r), sB));
     if (r == 0)
       if (int rc = pst_q()) return rc;
 
@@ -1811,7 +1441,10 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     // -- host: transcript (mipp.rs:56, 97-101) and the challenge
     if (!have_U) {
       TPST_HIP(ctx, hipEventSynchronize(ev[EV_U]));
-      memcpy(proof->U, pin + dn_U, 96);
+      if (p->has_u)
+        memcpy(proof->U, p->U, 96);
+      else
+        xyzz_to_canonical_host<Fq>(pin + dn_U, 1, proof->U);
       uint8_t b[96];
       g1_bytes(proof->U, b);
       sp.absorb_bytes(b, 96);
@@ -1823,8 +1456,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     const double h0 = host_us();
     TPST_HIP(ctx, hipEventSynchronize(ev_b(r)));
     const double h1 = host_us();
-    memcpy(proof->comms_u[r][0], dn_r, 96);
-    memcpy(proof->comms_u[r][1], dn_r + 96, 96);
+    xyzz_to_canonical_host<Fq>(dn_r, 2, proof->comms_u[r][0]);
     uint8_t b[96];
     g1_bytes(proof->comms_u[r][0], b);
     sp.absorb_bytes(b, 96);
@@ -1833,17 +1465,20 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     const double h2 = host_us();
     TPST_HIP(ctx, hipEventSynchronize(ev_a(r)));
     const double h3 = host_us();
-    memcpy(proof->comms_t[r][0], dn_r + 192, 576);
-    memcpy(proof->comms_t[r][1], dn_r + 192 + 576, 576);
+    memcpy(proof->comms_t[r][0], dn_r + 2 * X1, 576);
+    memcpy(proof->comms_t[r][1], dn_r + 2 * X1 + 576, 576);
     sp.absorb_bytes((const uint8_t*)proof->comms_t[r][0], 576);
     sp.absorb_bytes((const uint8_t*)proof->comms_t[r][1], 576);
+    const double h4 = host_us();
     uint64_t ci_c[4];
     sp.challenge(ci_c);  // mipp.rs:101
     const Fr c_inv = fr_canon(ci_c);
+    const double h5 = host_us();
     const Fr c = fr_inv(c_inv);  // mipp.rs:106
     if (open_trace())
-      fprintf(stderr, "open round %d: wait_u %.0f absorb_u %.0f wait_t %.0f absorb_t+challenge %.0f us\n", r, h1 - h0,
-              h2 - h1, h3 - h2, host_us() - h3);
+      fprintf(stderr,
+              "open round %d: enqueue %.0f wait_u %.0f absorb_u %.0f wait_t %.0f absorb_t %.0f challenge %.0f inv %.0f us\n",
+              r, h0 - hq, h1 - h0, h2 - h1, h3 - h2, h4 - h3, h5 - h4, host_us() - h5);
     xs_inv.push_back(c_inv);
     cprev = c_inv;
     cprev_c = c;
@@ -1859,7 +1494,10 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   }
   if (!have_U) {
     TPST_HIP(ctx, hipEventSynchronize(ev[EV_U]));
-    memcpy(proof->U, pin + dn_U, 96);
+    if (p->has_u)
+      memcpy(proof->U, p->U, 96);
+    else
+      xyzz_to_canonical_host<Fq>(pin + dn_U, 1, proof->U);
     uint8_t b[96];
     g1_bytes(proof->U, b);
     sp.absorb_bytes(b, 96);
@@ -1893,8 +1531,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     TPST_HIP(ctx, mipp_scalars(sA, dWm, nullptr, 1, 0, C, ScA.u()));
     g.glv = true;
     TPST_HIP(ctx, fbt_msm<Fq>(arA, sA, tA, ScA.u(), g, (Xyzz<Fq>*)xa.p));
-    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(sA, (Xyzz<Fq>*)xa.p, canA.u(), 1));
-    TPST_HIP(ctx, hipMemcpyAsync(pin + dn_final, canA.p, 96, hipMemcpyDeviceToHost, sA));
+    TPST_HIP(ctx, hipMemcpyAsync(pin + dn_final, xa.p, X1, hipMemcpyDeviceToHost, sA));
   }
   TPST_HIP(ctx, hipStreamWaitEvent(sCe, ev[EV_FINAL_UP], 0));
   if (last_c >= 0) TPST_HIP(ctx, hipStreamWaitEvent(sCe, ev_c(last_c), 0));  // xh / ScC / arC reuse
@@ -1903,8 +1540,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     g.members = C;
     TPST_HIP(ctx, mipp_scalars(sCe, dWim, nullptr, 1, 0, C, ScC.u()));
     TPST_HIP(ctx, fbt_msm<Fq2>(arC, sCe, tH, ScC.u(), g, (Xyzz<Fq2>*)xh.p));
-    TPST_HIP(ctx, xyzz_to_affine_canonical<Fq2>(sCe, (Xyzz<Fq2>*)xh.p, canC.u(), 1));
-    TPST_HIP(ctx, hipMemcpyAsync(pin + dn_final + 96, canC.p, 192, hipMemcpyDeviceToHost, sCe));
+    TPST_HIP(ctx, hipMemcpyAsync(pin + dn_fh, xh.p, X2, hipMemcpyDeviceToHost, sCe));
     TPST_HIP(ctx, hipEventRecord(ev[EV_C_DONE], sCe));
   }
   if (m > 0) {  // pst_proof_h = open_g1(p_h, rs) (mipp.rs:144)
@@ -1912,8 +1548,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     TPST_HIP(ctx, pst_open_fbt_s<Fq>(sB, arB, st, st->t_pgp.u(), st->nv - m, dWim, m, dfin + 16,
                                      (Xyzz<Fq>*)xp.p, pstA.u()));
     TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(sB, (Xyzz<Fq>*)xp.p, canC.u() + 48, m));
-    TPST_HIP(ctx, hipMemcpyAsync(pin + dn_final + 96 + 192, canC.u() + 48, (size_t)m * 96, hipMemcpyDeviceToHost,
-                                 sB));
+    TPST_HIP(ctx, hipMemcpyAsync(pin + dn_ph, canC.u() + 48, (size_t)m * 96, hipMemcpyDeviceToHost, sB));
   }
   TPST_HIP(ctx, hipEventRecord(ev[EV_B_DONE], sB));
   if (pf.on) {  // device spans end when every stream of the opening has drained
@@ -1925,10 +1560,10 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     pf.end(ST_SQRT_OPEN, sA);
   }
   for (hipStream_t s2 : {sA, sB, sLA[0], sLA[1]}) TPST_HIP(ctx, hipStreamSynchronize(s2));
-  memcpy(proof->final_a, pin + dn_final, 96);
-  memcpy(proof->final_h, pin + dn_final + 96, 192);
-  if (m > 0) memcpy(proof->pst_proof_h, pin + dn_final + 96 + 192, (size_t)m * 96);
-  memcpy(proof->pst_proof, pin + dn_final + 96 + 192 + (size_t)m * 96, (size_t)k * 192);
+  xyzz_to_canonical_host<Fq>(pin + dn_final, 1, proof->final_a);
+  xyzz_to_canonical_host<Fq2>(pin + dn_fh, 1, proof->final_h);
+  if (m > 0) memcpy(proof->pst_proof_h, pin + dn_ph, (size_t)m * 96);
+  memcpy(proof->pst_proof, pin + dn_pst, (size_t)k * 192);
   sp.store(tr);
   return TPST_OK;
 }
