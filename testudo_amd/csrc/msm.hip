@@ -1185,6 +1185,28 @@ __global__ void __launch_bounds__(64) k_seg_run_quad(const Xyzz<F>* __restrict__
   }
 }
 
+// k_seg_run_quad with one lane per segment (throughput shape: >= 2^18
+// segments, e.g. the 2^24 commit's 4096 rows x 128 segments)
+template <class F>
+__global__ void __launch_bounds__(64) k_seg_run_lane(const Xyzz<F>* __restrict__ buckets, uint32_t nb, uint32_t L,
+                                                     size_t nseg, Xyzz<F>* __restrict__ S_out,
+                                                     Xyzz<F>* __restrict__ Tn) {
+  using C = typename AccField<F>::T;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nseg) return;
+  const uint32_t S = nb / L;
+  const size_t g = t / S;
+  const uint32_t k = (uint32_t)(t % S);
+  const size_t base = g * nb + (size_t)k * L;
+  Xyzz<C> acc = Xyzz<C>::inf(), sum = Xyzz<C>::inf();
+  for (int b = (int)L - 1; b >= 0; b--) {
+    acc = add(acc, load_acc(buckets, base + b));
+    sum = add(sum, acc);
+  }
+  store_acc(S_out, t, sum);
+  store_acc(Tn, g * S + (k ? k - 1 : S - 1), k ? acc : Xyzz<C>::inf());
+}
+
 // out[g] = a[g] + 2^lg b[g], one quad per group
 template <class F>
 __global__ void __launch_bounds__(64) k_lift_add_quad(const Xyzz<F>* __restrict__ a, const Xyzz<F>* __restrict__ b,
@@ -1236,7 +1258,10 @@ static hipError_t reduce_buckets2(Arena& ar, hipStream_t s, const Xyzz<F>* d_buc
   Xyzz<F>* Tn = ar.take<Xyzz<F>>(nseg);
   Xyzz<F>* R = ar.take<Xyzz<F>>(groups);
   Xyzz<F>* SS = ar.take<Xyzz<F>>(groups);
-  k_seg_run_quad<F><<<grid_for(4 * nseg, 64), 64, 0, s>>>(d_buckets, nb, L1, nseg, Sk, Tn, prio);
+  if (std::is_same<F, Fq>::value && nseg >= ((size_t)1 << 18))
+    k_seg_run_lane<F><<<grid_for(nseg, 64), 64, 0, s>>>(d_buckets, nb, L1, nseg, Sk, Tn);
+  else
+    k_seg_run_quad<F><<<grid_for(4 * nseg, 64), 64, 0, s>>>(d_buckets, nb, L1, nseg, Sk, Tn, prio);
   TPST_TRY(hipGetLastError());
   TPST_TRY(reduce_buckets<F>(ar, s, Tn, groups, S1, R, prio));
   TPST_TRY(sum_groups<F>(ar, s, Sk, groups, S1, SS, prio));
@@ -1935,12 +1960,21 @@ hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint3
   const size_t m = rows * N * (size_t)W;
   if (m >= (1ull << 32)) return hipErrorInvalidValue;  // entry offsets are u32
   const size_t nbk = rows * nb;
-  const int lg = acc_chunk_lg(m);
+  // chunk length: at least 4 waves of chunks per SIMD (TPST_K1_WAVES; the
+  // 2^20 commit's 26.6 M entries take 64-entry chunks, measured 8.7 -> 8.4 ms
+  // against the 32-entry chunks 8 waves per SIMD would give)
+  static const size_t k1_threads = [] {
+    const char* e = getenv("TPST_K1_WAVES");
+    const int w = e ? atoi(e) : 0;
+    return (size_t)(w > 0 ? w : 4) * 64 * device_simds();
+  }();
+  int lg = 5;
+  while (lg < 8 && (m >> (lg + 1)) >= k1_threads) lg++;
   const size_t nchunk = (m + ((size_t)1 << lg) - 1) >> lg;
   const size_t nblk = (nchunk + ACC_BLOCK - 1) / ACC_BLOCK;
   size_t need = 2 * Arena::need(m, 4) + 2 * Arena::need(nbk, 4) + Arena::need(nbk, sizeof(Xyzz<Fq>)) +
                 Arena::need(nchunk, sizeof(Xyzz<Fq>)) + Arena::need(nblk, sizeof(Xyzz<Fq>)) +
-                reduce_scratch<Fq>(rows, nb) + 4096;
+                reduce_scratch<Fq>(rows, nb) + (red2_ok(nb) ? reduce2_scratch<Fq>(rows, nb) : 0) + 4096;
   ar.reset();
   TPST_TRY(ar.reserve(need));
   uint32_t* keys = ar.take<uint32_t>(m);
@@ -1983,7 +2017,16 @@ hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint3
   TPST_TRY(hipGetLastError());
   pf->end(ST_BUCKET_ACC, s);
   pf->begin(ST_REDUCE, s);
-  TPST_TRY(reduce_buckets<Fq>(ar, s, buckets, rows, nb, d_out));
+  // the two-level reduction (no per-segment scalar multiplications; 2^20
+  // commit 8.7 -> 8.2 ms, 2^24 unchanged); TPST_K1_RED=1: weighted segments
+  static const int k1_red = [] {
+    const char* e = getenv("TPST_K1_RED");
+    return e ? atoi(e) : 2;
+  }();
+  if (k1_red == 2 && red2_ok(nb))
+    TPST_TRY(reduce_buckets2<Fq>(ar, s, buckets, rows, nb, d_out, 0));
+  else
+    TPST_TRY(reduce_buckets<Fq>(ar, s, buckets, rows, nb, d_out));
   pf->end(ST_REDUCE, s);
   return hipSuccess;
 }

@@ -1422,6 +1422,13 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
 
     // -- C: h^(r) prepared at odd r for the look-aheads of rounds r+2, r+3
     if ((r & 1) && r + 4 <= m) {
+      // TPST_OPEN_C=la: behind this round's look-ahead on its stream (the
+      // look-ahead of round r+2, its first reader, runs there next)
+      static const bool c_on_la = [] {
+        const char* e = getenv("TPST_OPEN_C");
+        return e && !strcmp(e, "la");
+      }();
+      if (c_on_la) sC = sLA[r & 1];
       TPST_HIP(ctx, hipStreamWaitEvent(sC, ev_up(r), 0));
       if (r >= 5) TPST_HIP(ctx, hipStreamWaitEvent(sC, ev_la(r - 1), 0));  // last reader of h^(r-4)'s slot
       TPST_HIP(ctx, mipp_scalars(sC, dWi, nullptr, len, 0, C, ScC.u()));
