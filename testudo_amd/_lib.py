@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtpst.so")
+LIB_PATH = os.environ.get("TPST_LIB_PATH") or os.path.join(_HERE, "libtpst.so")  # override: A/B builds (experiments)
 
 _u64p = C.POINTER(C.c_uint64)
 _vp = C.c_void_p

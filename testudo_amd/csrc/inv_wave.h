@@ -4,21 +4,24 @@
 // 13-limb values) is a ~0.13 ms serial chain.  Where only one or two values
 // are inverted -- the open's per-round cross commitments, an MSM's single
 // output point, the final-exponentiation chain -- that chain sits on the
-// critical path with 63 lanes idle.  Here the wave shares the work: Pornin's
-// binary GCD in batches of K = 15 divsteps on 32-bit approximations (the
-// batch transition runs on wave-uniform values, i.e. the scalar unit), the big
-// values a, b (the GCD pair) and u, v (the cofactors, signed) as NL = 28 limbs
-// of 15 bits, one limb per lane.  A batch's four updates
-//     (x f + y g + k p) / 2^15
+// critical path with 63 lanes idle.  Here the wave shares the work: the
+// Bernstein-Yang GCD in batches of K = 15 divsteps, variable time (the
+// libsecp256k1 modinv shape: each inner step skips g's trailing zeros and
+// cancels up to eta + 1 low bits with one multiple of f), run on wave-uniform
+// low bits, i.e. on the scalar unit -- 5 inner steps per batch on average
+// against 15 branch-free divsteps of Pornin's form -- and the big values f, g
+// (the GCD pair) and d, e (the cofactors, signed) as NL = 28 limbs of 15 bits,
+// one limb per lane.  A batch's four updates
+//     (x u + y v + k p) / 2^15
 // are one limb product per lane plus a carry normalisation: a bias makes every
 // limb sum nonnegative, two local carry passes (DPP shift by one lane) leave
 // limbs <= 2^15 + 4, and one ballot pass resolves the remaining +1 ripples
 // (carry-lookahead on the 64-bit lane masks); the division by 2^15 is a shift
 // down by one lane.  Exact model, every step as computed here:
-// tools/inv_wave_model.py.
+// tools/inv_wave_model.py (inv_model_by; 52.6 batches on average, at most 55).
 //
-// Bounds (checked by the model): |f| + |g| <= 2^15 and limbs < 2^15, so a
-// limb sum stays below 2^31 in magnitude; the cofactors stay below 52 p.
+// Bounds (checked by the model): |u| + |v| <= 2^15 and limbs < 2^15, so a
+// limb sum stays below 2^31 in magnitude; the cofactors stay below 60 p.
 #pragma once
 #include "field29.h"
 #include "curve.h"
@@ -29,7 +32,6 @@ namespace invw {
 constexpr int NL = 28;
 constexpr int K = 15;
 constexpr uint32_t LM = (1u << 15) - 1;
-constexpr int ITERS = (2 * 377 - 1 + K - 1) / K;  // 51
 constexpr uint64_t NLMASK = (1ull << NL) - 1;
 
 // p in radix 2^15
@@ -76,6 +78,59 @@ __device__ __forceinline__ uint32_t div_signed(int32_t t, uint32_t lane, bool& n
   return shift_down(limb);  // limb 0 is zero: / 2^15
 }
 
+constexpr int BY_MAX_BATCHES = 64;  // the model's maximum is 55
+
+// low 30 bits of a signed sign-magnitude value (limbs 0 and 1), two's complement
+__device__ __forceinline__ uint32_t low30(uint32_t mag, bool neg) {
+  const uint32_t x = rl(mag, 0) | (rl(mag, 1) << 15);
+  return neg ? 0u - x : x;
+}
+
+// K divsteps of Bernstein-Yang on the low bits, variable time (scalar unit):
+// each step skips g's trailing zeros, then cancels min(eta + 1, i) low bits
+// of g with one multiple of f (f^-1 mod 2^32 by Newton).  Returns eta and the
+// transition matrix, |u| + |v| <= 2^K.  tools/inv_wave_model.py divsteps_var.
+__device__ __forceinline__ int divsteps_var(int eta, uint32_t f, uint32_t g, int32_t& mu, int32_t& mv, int32_t& mq,
+                                            int32_t& mr) {
+  uint32_t u = 1, v = 0, q = 0, r = 1;
+  int i = K;
+#pragma unroll 1
+  for (;;) {
+    const int zeros = __builtin_ctz(g | (0xFFFFFFFFu << i));
+    g >>= zeros;
+    u <<= zeros;
+    v <<= zeros;
+    eta -= zeros;
+    i -= zeros;
+    if (i == 0) break;
+    if (eta < 0) {
+      eta = -eta;
+      const uint32_t tf = f, tu = u, tv = v;
+      f = g;
+      g = 0u - tf;
+      u = q;
+      q = 0u - tu;
+      v = r;
+      r = 0u - tv;
+    }
+    const int limit = eta + 1 < i ? eta + 1 : i;
+    const uint32_t m = (1u << limit) - 1u;
+    uint32_t x = f;
+    x *= 2u - f * x;
+    x *= 2u - f * x;
+    x *= 2u - f * x;
+    const uint32_t w = ((0u - g) * x) & m;
+    g += f * w;
+    q += u * w;
+    r += v * w;
+  }
+  mu = (int32_t)u;
+  mv = (int32_t)v;
+  mq = (int32_t)q;
+  mr = (int32_t)r;
+  return eta;
+}
+
 }  // namespace invw
 
 // y^-1 for a Montgomery-form y (x 2^377 -> x^-1 2^377), 0 -> 0.  Every lane of
@@ -98,75 +153,40 @@ __device__ inline __attribute__((noinline)) Fq29 inv_wave(const Fq29& y) {
     a = lane < (uint32_t)NL ? a : 0u;
   }
   const uint32_t pl = P15[lane & 31];
-  uint32_t b = lane < (uint32_t)NL ? pl : 0u;
-  uint32_t u = lane == 0 ? 1u : 0u, v = 0;
-  bool us = false, vs = false;
+  // Bernstein-Yang, variable time: f = p, g = y; d, e the signed cofactors
+  // (f = d y, g = e y mod p; each batch divides both sides by 2^15, the k p
+  // term keeping the cofactor division exact); stops when g = 0, f = +-1
+  uint32_t f = lane < (uint32_t)NL ? pl : 0u, g = a;
+  uint32_t d = 0, e = lane == 0 ? 1u : 0u;
+  bool fs = false, gs = false, ds = false, es = false;
+  int eta = -1;
 #pragma unroll 1
-  for (int it = 0; it < ITERS; it++) {
-    // 32-bit approximations: low 15 bits | top 17 bits of n = max(bitlen, 32)
-    const uint64_t nz = __ballot((a | b) != 0u);
-    int n = 32;
-    if (nz) {
-      const int top = 63 - __builtin_clzll(nz);
-      const uint32_t tw = rl(a | b, top);
-      const int nb = 15 * top + 32 - __builtin_clz(tw);
-      n = nb > 32 ? nb : 32;
-    }
-    const int s = n - 17, l0 = s / 15, sh = s % 15;
-    const uint32_t ta = ((rl(a, l0) >> sh) | (rl(a, l0 + 1) << (15 - sh)) | (rl(a, l0 + 2) << (30 - sh))) & 0x1ffffu;
-    const uint32_t tb = ((rl(b, l0) >> sh) | (rl(b, l0 + 1) << (15 - sh)) | (rl(b, l0 + 2) << (30 - sh))) & 0x1ffffu;
-    uint32_t ab = (rl(a, 0) & LM) | (ta << 15);
-    uint32_t bb = (rl(b, 0) & LM) | (tb << 15);
-    int32_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
-#pragma unroll
-    for (int j = 0; j < K; j++) {
-      const uint32_t odd = 0u - (ab & 1u);
-      const uint32_t sw = odd & (0u - (uint32_t)(ab < bb));
-      const uint32_t t = (ab ^ bb) & sw;
-      ab ^= t;
-      bb ^= t;
-      const int32_t sw32 = (int32_t)sw, o32 = (int32_t)odd;
-      const int32_t tf = (f0 ^ f1) & sw32, tg = (g0 ^ g1) & sw32;
-      f0 ^= tf;
-      f1 ^= tf;
-      g0 ^= tg;
-      g1 ^= tg;
-      ab -= bb & odd;
-      f0 -= f1 & o32;
-      g0 -= g1 & o32;
-      ab >>= 1;
-      f1 += f1;
-      g1 += g1;
-    }
-    bool sa, sb;
-    const uint32_t na = div_signed((int32_t)a * f0 + (int32_t)b * g0, lane, sa);
-    const uint32_t nbv = div_signed((int32_t)a * f1 + (int32_t)b * g1, lane, sb);
-    if (sa) {
-      f0 = -f0;
-      g0 = -g0;
-    }
-    if (sb) {
-      f1 = -f1;
-      g1 = -g1;
-    }
-    // signed cofactors; k p clears the low 15 bits
-    const int32_t uf0 = us ? -f0 : f0, vg0 = vs ? -g0 : g0;
-    const int32_t uf1 = us ? -f1 : f1, vg1 = vs ? -g1 : g1;
-    const int32_t u0 = (int32_t)rl(u, 0), v0 = (int32_t)rl(v, 0);
-    const int32_t k0 = (int32_t)((uint32_t)(-(u0 * uf0 + v0 * vg0)) & LM);
-    const int32_t k1 = (int32_t)((uint32_t)(-(u0 * uf1 + v0 * vg1)) & LM);
-    bool nus, nvs;
-    const uint32_t nu = div_signed((int32_t)u * uf0 + (int32_t)v * vg0 + k0 * (int32_t)pl, lane, nus);
-    const uint32_t nv = div_signed((int32_t)u * uf1 + (int32_t)v * vg1 + k1 * (int32_t)pl, lane, nvs);
-    a = na;
-    b = nbv;
-    u = nu;
-    v = nv;
-    us = nus;
-    vs = nvs;
+  for (int it = 0; it < BY_MAX_BATCHES && (__ballot(g != 0u) != 0); it++) {
+    int32_t u, v, q, r;
+    eta = divsteps_var(eta, low30(f, fs), low30(g, gs), u, v, q, r);
+    bool nfs, ngs;
+    const uint32_t nf = div_signed((int32_t)f * (fs ? -u : u) + (int32_t)g * (gs ? -v : v), lane, nfs);
+    const uint32_t ng = div_signed((int32_t)f * (fs ? -q : q) + (int32_t)g * (gs ? -r : r), lane, ngs);
+    const int32_t ud = ds ? -u : u, ve = es ? -v : v, qd = ds ? -q : q, re = es ? -r : r;
+    const int32_t d0 = (int32_t)rl(d, 0), e0 = (int32_t)rl(e, 0);
+    const int32_t kd = (int32_t)((uint32_t)(-(d0 * ud + e0 * ve)) & LM);
+    const int32_t ke = (int32_t)((uint32_t)(-(d0 * qd + e0 * re)) & LM);
+    bool nds, nes;
+    const uint32_t nd = div_signed((int32_t)d * ud + (int32_t)e * ve + kd * (int32_t)pl, lane, nds);
+    const uint32_t ne = div_signed((int32_t)d * qd + (int32_t)e * re + ke * (int32_t)pl, lane, nes);
+    f = nf;
+    g = ng;
+    d = nd;
+    e = ne;
+    fs = nfs;
+    gs = ngs;
+    ds = nds;
+    es = nes;
   }
-  // gcd(y, p) = b = 1 for y != 0; then v = +-y^-1 (plain), |v| < 52 p
-  const bool ok = (__ballot(b != (lane == 0 ? 1u : 0u)) & NLMASK) == 0;
+  // f = +-1 for y != 0; then y^-1 = +-d (plain), |d| < 60 p
+  const bool ok = (__ballot(f != (lane == 0 ? 1u : 0u)) & NLMASK) == 0;
+  const uint32_t v = d;
+  const bool vs = ds != fs;
   uint32_t vl[NL];
 #pragma unroll
   for (int i = 0; i < NL; i++) vl[i] = rl(v, i);
@@ -182,7 +202,7 @@ __device__ inline __attribute__((noinline)) Fq29 inv_wave(const Fq29& y) {
     }
     r[j] = (uint32_t)w & r29::M;
   }
-  // r mod p: a quotient estimate from the top limbs (q <= 51, low by at most
+  // r mod p: a quotient estimate from the top limbs (q <= 59, low by at most
   // one), then one conditional subtraction
   {
     const double dv = (double)r[13] * 536870912.0 + (double)r[12] + (double)r[11] * (1.0 / 536870912.0);

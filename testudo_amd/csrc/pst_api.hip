@@ -1066,8 +1066,16 @@ static int pst_open_fbt(tpst_ctx* ctx, SrsState* st, const uint32_t* table, int 
 static int open_streams(tpst_ctx* ctx, size_t n_events, size_t pinned_bytes) {
   int least = 0, greatest = 0;
   TPST_HIP(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
+  // TPST_OPEN_PRIO: bit i puts side stream i (0 = B, 1 / 2 = the look-ahead
+  // streams) at the greatest priority instead of the least (experiments)
+  static const int hi_mask = [] {
+    const char* e = getenv("TPST_OPEN_PRIO");
+    return e ? atoi(e) : 0;
+  }();
   for (int i = 0; i < 3; i++)
-    if (!ctx->side[i]) TPST_HIP(ctx, hipStreamCreateWithPriority(&ctx->side[i], hipStreamNonBlocking, least));
+    if (!ctx->side[i])
+      TPST_HIP(ctx, hipStreamCreateWithPriority(&ctx->side[i], hipStreamNonBlocking,
+                                                ((hi_mask >> i) & 1) ? greatest : least));
   while (ctx->events.size() < n_events) {
     hipEvent_t e;
     TPST_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1364,6 +1372,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     }
     TPST_HIP(ctx, hipMemcpyAsync(dn_r, xb.p, 2 * X1, hipMemcpyDeviceToHost, sB));
     TPST_HIP(ctx, hipEventRecord(ev_b(r), sB));
+    const double hb = open_trace() ? host_us() : 0.0;
     // -- A: t_l / t_r of this round
     if (r == 0) {  // direct: the rotated comm_list (affine) against h^(0)
       TPST_HIP(ctx, affine_rot(sA, A.u(), P.u(), C, 24));
@@ -1379,6 +1388,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     TPST_HIP(ctx, hipMemcpyAsync(dn_r + 2 * X1, canA.p, 1152, hipMemcpyDeviceToHost, sA));
     TPST_HIP(ctx, hipEventRecord(ev_a(r), sA));
 
+    const double ha = open_trace() ? host_us() : 0.0;
     // -- D: look-ahead products of this round's vectors for round r+1
     if (len >= 4) {
       hipStream_t sD = sLA[r & 1];
@@ -1417,9 +1427,11 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
       TPST_HIP(ctx, hipEventRecord(ev_la(r), sD));
     }
 
+    const double hd = open_trace() ? host_us() : 0.0;
     if (r == 0)
       if (int rc = pst_q()) return rc;
 
+    const double hp = open_trace() ? host_us() : 0.0;
     // -- C: h^(r) prepared at odd r for the look-aheads of rounds r+2, r+3
     if ((r & 1) && r + 4 <= m) {
       // TPST_OPEN_C=la: behind this round's look-ahead on its stream (the
@@ -1484,8 +1496,10 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     const Fr c = fr_inv(c_inv);  // mipp.rs:106
     if (open_trace())
       fprintf(stderr,
-              "open round %d: enqueue %.0f wait_u %.0f absorb_u %.0f wait_t %.0f absorb_t %.0f challenge %.0f inv %.0f us\n",
-              r, h0 - hq, h1 - h0, h2 - h1, h3 - h2, h4 - h3, h5 - h4, host_us() - h5);
+              "open round %d: enqueue %.0f (B %.0f A %.0f D %.0f pst %.0f C %.0f) wait_u %.0f absorb_u %.0f wait_t %.0f "
+              "absorb_t %.0f challenge %.0f inv %.0f us\n",
+              r, h0 - hq, hb - hq, ha - hb, hd - ha, hp - hd, h0 - hp, h1 - h0, h2 - h1, h3 - h2, h4 - h3, h5 - h4,
+              host_us() - h5);
     xs_inv.push_back(c_inv);
     cprev = c_inv;
     cprev_c = c;

@@ -86,7 +86,7 @@ int main() {
     g.v[1] ^= 1;
   }
   double t10 = now_ns();
-  printf("inverse: host Fermat %.2f us, binary GCD (field29) %.2f us (check %llx)\n", (t9 - t8) / 2000 * 1e-3,
+  printf("inverse: host::inv %.2f us, tpst::inv (field29 binary GCD) %.2f us (check %llx)\n", (t9 - t8) / 2000 * 1e-3,
          (t10 - t9) / 2000 * 1e-3, (unsigned long long)(h.v[0] ^ g.v[0]));
   printf("permute (sponge form) %.2f us, textbook %.2f us; hmul %.1f ns, hsqr %.1f ns, hmul3 %.1f ns, add %.1f ns"
          " (check %llx)\n",

@@ -118,12 +118,103 @@ def inv_model(y):
     return vv % P
 
 
+def divsteps_var(eta, f0, g0):
+    """Bernstein-Yang divsteps, variable time (libsecp256k1 modinv32's
+    divsteps_30_var shape) on the low 30 bits of the signed f, g (uint32
+    wraparound, as the scalar unit computes them): K divsteps -> eta and the
+    transition matrix (u, v, q, r), |u| + |v| <= 2^K, f' = (u f + v g) / 2^K,
+    g' = (q f + r g) / 2^K.  Each inner iteration skips g's trailing zeros and
+    cancels up to min(eta + 1, i) low bits of g with one multiple of f (f^-1
+    mod 2^16 by three Newton steps)."""
+    M32 = (1 << 32) - 1
+    u, v, q, r = 1, 0, 0, 1
+    f, g = f0 & M32, g0 & M32
+    i = K
+    iters = 0
+    while True:
+        iters += 1
+        gg = (g | (M32 << i)) & M32
+        zeros = (gg & -gg).bit_length() - 1
+        g >>= zeros
+        u <<= zeros
+        v <<= zeros
+        eta -= zeros
+        i -= zeros
+        if i == 0:
+            break
+        if eta < 0:
+            eta = -eta
+            f, g = g, (-f) & M32
+            u, q = q, -u
+            v, r = r, -v
+        limit = min(eta + 1, i)
+        m = (1 << limit) - 1
+        x = f
+        for _ in range(3):
+            x = (x * (2 - f * x)) & 0xFFFF
+        w = ((-g) * x) & m
+        g = (g + f * w) & M32
+        q += u * w
+        r += v * w
+    assert abs(u) + abs(v) <= 1 << K and abs(q) + abs(r) <= 1 << K
+    return eta, u, v, q, r, iters
+
+
+def low30(mag, neg):
+    x = mag[0] | (mag[1] << LB)
+    return (-x) & 0xFFFFFFFF if neg else x
+
+
+def inv_model_by(y):
+    """inv_wave's Bernstein-Yang form: f = p, g = y; d, e the signed cofactors
+    (f = d y, g = e y mod p, both sides divided by 2^15 per batch, the k p step
+    keeping the division exact); stop when g = 0, then f = +-1 and
+    y^-1 = +-d."""
+    f, fs = P_L[:], False
+    g, gs = to_limbs(y), False
+    d, ds = to_limbs(0), False
+    e, es = to_limbs(1), False
+    eta = -1
+    batches = iters = 0
+    while any(g):
+        eta, u, v, q, r, it = divsteps_var(eta, low30(f, fs), low30(g, gs))
+        iters += it
+        batches += 1
+        nfs, nf = lincomb(f, fs, u, g, gs, v)
+        ngs, ng = lincomb(f, fs, q, g, gs, r)
+        ud = -u if ds else u
+        ve = -v if es else v
+        qd = -q if ds else q
+        re = -r if es else r
+        kd = (-(d[0] * ud + e[0] * ve)) & LM
+        ke = (-(d[0] * qd + e[0] * re)) & LM
+        nds, nd = lincomb(d, ds, u, e, es, v, kd)
+        nes, ne = lincomb(d, ds, q, e, es, r, ke)
+        f, fs, g, gs, d, ds, e, es = nf, nfs, ng, ngs, nd, nds, ne, nes
+        assert batches <= 60
+    assert from_limbs(f) == 1, from_limbs(f)
+    dv = from_limbs(d)
+    assert dv < 60 * P
+    neg = ds != fs
+    return (-dv if neg else dv) % P, batches, iters
+
+
 def main():
     random.seed(5)
-    for y in [1, 2, 3, P - 1, P - 2, (1 << 376) + 12345, P // 2] + [random.randrange(1, P) for _ in range(300)]:
+    ys = [1, 2, 3, P - 1, P - 2, (1 << 376) + 12345, P // 2] + [random.randrange(1, P) for _ in range(300)]
+    for y in ys:
         r = inv_model(y)
         assert r * y % P == 1, y
     print("inv_wave model ok: %d iterations of %d divsteps" % (ITERS, K))
+    nb = ni = mb = 0
+    for y in ys:
+        r, b, it = inv_model_by(y)
+        assert r * y % P == 1, y
+        nb += b
+        ni += it
+        mb = max(mb, b)
+    print("Bernstein-Yang variable-time form ok: %.1f batches (max %d), %.1f inner iterations per inverse"
+          % (nb / len(ys), mb, ni / len(ys)))
 
 
 if __name__ == "__main__":
