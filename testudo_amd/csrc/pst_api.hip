@@ -170,6 +170,9 @@ struct SrsState {
   bool fbt_ready = false, t_h_ready[2] = {false, false};
   DevBuf t_A;                     // per-opening table over the row commitments
   size_t t_A_n = 0;
+  // t_A prebuilt by tpst_poly_commit (beside its IPP) for exactly these
+  // canonical row commitments; consumed by the next opening of them
+  std::vector<uint64_t> t_A_key;
   std::vector<uint64_t> flat;     // canonical export
   ~SrsState() { batch_tables_free(tables); }
 };
@@ -621,7 +624,12 @@ extern "C" int tpst_poly_eval(tpst_ctx* ctx, tpst_poly* p, const uint64_t* point
 }
 
 // commit (sqrt_pst.rs:117-149): K1 row MSMs + IPP T = prod e(C_i, h_i)
-static int poly_commit_dev(tpst_ctx* ctx, tpst_poly* p, uint32_t* d_comms_mont, Fq12* d_T) {
+static int open_streams(tpst_ctx* ctx, size_t n_events, size_t pinned_bytes);
+
+// prebuild (tpst_poly_commit): also build the opening's fold table over the
+// row commitments on a side stream while the IPP runs (TPST_COMMIT_TABLE=0 /
+// 1 forces it off / on)
+static int poly_commit_dev(tpst_ctx* ctx, tpst_poly* p, uint32_t* d_comms_mont, Fq12* d_T, bool prebuild = false) {
   SrsState* st = srs_of(ctx);
   if (!st) return fail(ctx, TPST_E_STATE, "no SRS loaded");
   if (st->nv != p->m_row) return fail(ctx, TPST_E_ARG, "SRS num_vars != ceil(n/2)");
@@ -639,6 +647,19 @@ static int poly_commit_dev(tpst_ctx* ctx, tpst_poly* p, uint32_t* d_comms_mont, 
     TPST_HIP(ctx, xyzz_to_affine_mont<Fq>(s, rows, d_comms_mont, C));
     pf.end(ST_COMM_LIST, s);
   }
+  if (prebuild) {  // the opening's GLV fold table over comm_list, beside the IPP
+    if (int rc = open_streams(ctx, 8, 0)) return rc;
+    if (st->t_A_n < C) {
+      TPST_HIP(ctx, st->t_A.alloc(fbt_words<Fq>(C) * 4));
+      st->t_A_n = C;
+    }
+    st->t_A_key.clear();
+    hipEvent_t* ev = ctx->events.data();
+    TPST_HIP(ctx, hipEventRecord(ev[0], s));
+    TPST_HIP(ctx, hipStreamWaitEvent(ctx->side[1], ev[0], 0));
+    TPST_HIP(ctx, fbt_build<Fq>(ctx->arena_side[1], ctx->side[1], d_comms_mont, C, st->t_A.u(), true));
+    TPST_HIP(ctx, hipEventRecord(ev[1], ctx->side[1]));
+  }
   {
     TraceRange tr("ipp");  // sqrt_pst.rs:131-144
     pf.begin(ST_IPP, s);
@@ -648,6 +669,7 @@ static int poly_commit_dev(tpst_ctx* ctx, tpst_poly* p, uint32_t* d_comms_mont, 
     TPST_HIP(ctx, multi_pairing_prepared(ctx->arena, s, d_comms_mont, st->ph[p->odd]->u(), hp, 1, C, d_T));
     pf.end(ST_IPP, s);
   }
+  if (prebuild) TPST_HIP(ctx, hipStreamWaitEvent(s, ctx->events[1], 0));
   pf.end(ST_SQRT_COMMIT, s);
   return TPST_OK;
 }
@@ -663,7 +685,15 @@ extern "C" int tpst_poly_commit(tpst_ctx* ctx, tpst_poly* p, uint64_t* comms, ui
   TPST_HIP(ctx, cm.alloc(C * 96));
   TPST_HIP(ctx, tt.alloc(sizeof(Fq12)));
   TPST_HIP(ctx, out.alloc(C * 96 + 576));
-  int rc = poly_commit_dev(ctx, p, cm.u(), (Fq12*)tt.p);
+  // the table build fits beside the IPP up to C = 2048 row commitments (2^20:
+  // commit + open 21.7 -> 21.2 ms); at C = 4096 it outlasts the IPP and only
+  // moves ~2 ms from the open to the commit (2^24: 109.3 vs 109.8 ms)
+  static const int table_env = [] {
+    const char* e = getenv("TPST_COMMIT_TABLE");
+    return e ? atoi(e) : -1;
+  }();
+  const bool prebuild = table_env < 0 ? C <= 2048 : table_env != 0;
+  int rc = poly_commit_dev(ctx, p, cm.u(), (Fq12*)tt.p, prebuild);
   if (rc) return rc;
   hipStream_t s = ctx->stream;
   TPST_HIP(ctx, affine_from_mont<Fq>(s, cm.u(), out.u(), C));
@@ -671,6 +701,7 @@ extern "C" int tpst_poly_commit(tpst_ctx* ctx, tpst_poly* p, uint64_t* comms, ui
   TPST_HIP(ctx, hipMemcpyAsync(comms, out.p, C * 96, hipMemcpyDeviceToHost, s));
   TPST_HIP(ctx, hipMemcpyAsync(T, out.u() + 24 * C, 576, hipMemcpyDeviceToHost, s));
   TPST_HIP(ctx, hipStreamSynchronize(s));
+  if (prebuild) srs_of(ctx)->t_A_key.assign(comms, comms + 12 * C);
   return TPST_OK;
 }
 
@@ -1268,7 +1299,10 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   TraceRange trace_mipp("mipp_prove");
 
   // ---- look-ahead stream 1 (idle until round 1): the fold table over comm_list
-  TPST_HIP(ctx, fbt_build<Fq>(*arLA[1], sLA[1], A.u(), C, st->t_A.u(), true));
+  // (prebuilt by the commit of exactly these row commitments: used once)
+  const bool prebuilt = st->t_A_key.size() == 12 * C && !memcmp(st->t_A_key.data(), comms, C * 96);
+  st->t_A_key.clear();
+  if (!prebuilt) TPST_HIP(ctx, fbt_build<Fq>(*arLA[1], sLA[1], A.u(), C, st->t_A.u(), true));
   TPST_HIP(ctx, hipEventRecord(ev[EV_TABLE], sLA[1]));
   // ---- stream B: U = MSM(comm_list, chi(b)) on that table, or the c_u the
   // ranks combined for an opening-only handle
