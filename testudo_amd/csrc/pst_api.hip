@@ -1098,12 +1098,13 @@ static int open_streams(tpst_ctx* ctx, size_t n_events, size_t pinned_bytes) {
   int least = 0, greatest = 0;
   TPST_HIP(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
   // TPST_OPEN_PRIO: bit i puts side stream i (0 = B, 1 / 2 = the look-ahead
-  // streams) at the greatest priority instead of the least; default 6: the
-  // look-ahead streams, whose chain gates each round's comms_t (2^20 open
-  // 14.2 -> 13.8 ms in A/B sweeps)
+  // streams) at the greatest priority instead of the least.  Default 0: 6
+  // (look-ahead streams high) won an open-only sweep (14.2 -> 13.8 ms) but
+  // lost in the commit + open bench (2^20 open 12.3 -> 13.9 ms, 2^24 31.6 ->
+  // 33.6 ms; profiles/r04/late/prio6_bench*.json)
   static const int hi_mask = [] {
     const char* e = getenv("TPST_OPEN_PRIO");
-    return e ? atoi(e) : 6;
+    return e ? atoi(e) : 0;
   }();
   for (int i = 0; i < 3; i++)
     if (!ctx->side[i])
