@@ -47,6 +47,7 @@ const HostP64& hp64() {
 
 // no-carry CIOS (p's top word < 2^62: the running value fits 6 words + the
 // carry word of each row), fully unrolled over the 6 words of b
+template <bool LAZY = false>
 Fq hmul(const Fq& a, const Fq& b) {
   typedef unsigned __int128 u128;
   const HostP64& P = hp64();
@@ -92,8 +93,13 @@ Fq hmul(const Fq& a, const Fq& b) {
   }
   TPST_HMUL_ROW(0) TPST_HMUL_ROW(1) TPST_HMUL_ROW(2) TPST_HMUL_ROW(3) TPST_HMUL_ROW(4) TPST_HMUL_ROW(5)
 #undef TPST_HMUL_ROW
-  // t < 2p: one conditional subtraction
+  // t < 2p: one conditional subtraction (LAZY: left < 2p for a product)
   const uint64_t t[6] = {t0, t1, t2, t3, t4, t5};
+  if (LAZY) {
+    Fq out;
+    memcpy(out.v, t, 48);
+    return out;
+  }
   uint64_t r[6];
   u128 br = 0;
   for (int j = 0; j < 6; j++) {
@@ -109,6 +115,7 @@ Fq hmul(const Fq& a, const Fq& b) {
 // word-by-word Montgomery reduction of a 12-word t (t < p R): t R^-1 mod p,
 // one conditional subtraction (t R^-1 < 2p).  Carries out of each row go to
 // the next row's top word (c2) -- no data-dependent branches.
+template <bool LAZY = false>
 __attribute__((always_inline)) inline Fq redc12(uint64_t* t) {
   typedef unsigned __int128 u128;
   const HostP64& P = hp64();
@@ -126,6 +133,11 @@ __attribute__((always_inline)) inline Fq redc12(uint64_t* t) {
     const u128 s2 = (u128)t[i + 6] + (uint64_t)c + c2;
     t[i + 6] = (uint64_t)s2;
     c2 = (uint64_t)(s2 >> 64);
+  }
+  if (LAZY) {  // t < 12 p^2 (three products of inputs < 2p): t R^-1 < 1.1 p, c2 = 0
+    Fq out;
+    memcpy(out.v, t + 6, 48);
+    return out;
   }
   uint64_t r[6];
   u128 br = 0;
@@ -163,6 +175,7 @@ __attribute__((always_inline)) inline void mac12(uint64_t* t, const uint64_t* x,
 // sum of three Montgomery products with one reduction: the 768-bit products
 // are added unreduced (3 p^2 < p R) and reduced once, so an MDS row costs
 // three multiplications and one REDC instead of three of each
+template <bool LAZY = false>
 Fq hmul3(const Fq& a0, const Fq& b0, const Fq& a1, const Fq& b1, const Fq& a2, const Fq& b2) {
   uint64_t t[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, x[6], y[6];
   memcpy(x, a0.v, 48);
@@ -174,11 +187,12 @@ Fq hmul3(const Fq& a0, const Fq& b0, const Fq& a1, const Fq& b1, const Fq& a2, c
   memcpy(x, a2.v, 48);
   memcpy(y, b2.v, 48);
   mac12(t, x, y);
-  return redc12(t);
+  return redc12<LAZY>(t);
 }
 
 // Montgomery square: the 15 cross products once, doubled, plus the 6
 // squares, then the REDC -- the S-box's x^2, x^4, x^8, x^16
+template <bool LAZY = false>
 Fq hsqr(const Fq& a) {
   typedef unsigned __int128 u128;
   uint64_t x[6];
@@ -209,7 +223,7 @@ Fq hsqr(const Fq& a) {
     t[2 * i + 1] = (uint64_t)c;
     c >>= 64;
   }
-  return redc12(t);
+  return redc12<LAZY>(t);
 }
 
 // a + b mod p on 64-bit words (a, b < p)
@@ -236,8 +250,51 @@ inline Fq hadd(const Fq& a, const Fq& b) {
   return out;
 }
 
-// x^17 (alpha = 17)
-Fq sbox17(const Fq& x) { return hmul(hsqr(hsqr(hsqr(hsqr(x)))), x); }
+// a + b for a, b < 2p, left < 2p (the permutation's lazy form: every value
+// inside it stays below 2p, products and REDCs skip the final subtraction)
+inline Fq hadd_lazy(const Fq& a, const Fq& b) {
+  typedef unsigned __int128 u128;
+  const HostP64& P = hp64();
+  uint64_t x[6], y[6], t[6], r[6], p2[6];
+  memcpy(x, a.v, 48);
+  memcpy(y, b.v, 48);
+  u128 c = 0;
+  for (int j = 0; j < 6; j++) {
+    c += (u128)x[j] + y[j];
+    t[j] = (uint64_t)c;
+    c >>= 64;
+    p2[j] = (P.p[j] << 1) | (j ? P.p[j - 1] >> 63 : 0);
+  }
+  u128 br = 0;
+  for (int j = 0; j < 6; j++) {
+    const u128 d = (u128)t[j] - p2[j] - (uint64_t)br;
+    r[j] = (uint64_t)d;
+    br = (d >> 64) & 1;
+  }
+  Fq out;
+  memcpy(out.v, br ? t : r, 48);  // a + b < 4p < 2^379
+  return out;
+}
+
+// x < 2p -> canonical
+inline Fq hcanon(const Fq& a) {
+  typedef unsigned __int128 u128;
+  const HostP64& P = hp64();
+  uint64_t t[6], r[6];
+  memcpy(t, a.v, 48);
+  u128 br = 0;
+  for (int j = 0; j < 6; j++) {
+    const u128 d = (u128)t[j] - P.p[j] - (uint64_t)br;
+    r[j] = (uint64_t)d;
+    br = (d >> 64) & 1;
+  }
+  Fq out;
+  memcpy(out.v, br ? t : r, 48);
+  return out;
+}
+
+// x^17 (alpha = 17), lazy: x < 2p in, < 2p out
+Fq sbox17(const Fq& x) { return hmul<true>(hsqr<true>(hsqr<true>(hsqr<true>(hsqr<true>(x)))), x); }
 
 // ------------------------------------------------------------ Poseidon ----
 // The permutation is evaluated in the equivalent form of the Poseidon paper's
@@ -329,27 +386,30 @@ struct Sponge {
   }
   void full_round(const PoseidonParams& P, int r) {
     Fq x[3];
-    for (int i = 0; i < 3; i++) x[i] = sbox17(hadd(st[i], P.ark[r][i]));
-    for (int i = 0; i < 3; i++) st[i] = hmul3(P.mds[i][0], x[0], P.mds[i][1], x[1], P.mds[i][2], x[2]);
+    for (int i = 0; i < 3; i++) x[i] = sbox17(hadd_lazy(st[i], P.ark[r][i]));
+    for (int i = 0; i < 3; i++) st[i] = hmul3<true>(P.mds[i][0], x[0], P.mds[i][1], x[1], P.mds[i][2], x[2]);
   }
+  // lazy throughout (values < 2p), canonical state in and out
   void permute() {
     const PoseidonParams& P = pparams();
     for (int r = 0; r < P.RF0; r++) full_round(P, r);
     for (int k = 0; k < P.RP - 1; k++) {
       const Fq* m = P.sp[k];
-      const Fq x0 = sbox17(hadd(st[0], P.ark[P.RF0 + k][0]));
-      const Fq n0 = hmul3(m[0], x0, m[1], st[1], m[2], st[2]);
-      st[1] = hadd(st[1], hmul(m[3], x0));
-      st[2] = hadd(st[2], hmul(m[4], x0));
+      const Fq x0 = sbox17(hadd_lazy(st[0], P.ark[P.RF0 + k][0]));
+      const Fq n0 = hmul3<true>(m[0], x0, m[1], st[1], m[2], st[2]);
+      st[1] = hadd_lazy(st[1], hmul<true>(m[3], x0));
+      st[2] = hadd_lazy(st[2], hmul<true>(m[4], x0));
       st[0] = n0;
     }
     {
-      const Fq x0 = sbox17(hadd(st[0], P.ark[P.RF0 + P.RP - 1][0]));
+      const Fq x0 = sbox17(hadd_lazy(st[0], P.ark[P.RF0 + P.RP - 1][0]));
       Fq ns[3];
-      for (int i = 0; i < 3; i++) ns[i] = hmul3(P.last[i][0], x0, P.last[i][1], st[1], P.last[i][2], st[2]);
+      for (int i = 0; i < 3; i++)
+        ns[i] = hmul3<true>(P.last[i][0], x0, P.last[i][1], st[1], P.last[i][2], st[2]);
       for (int i = 0; i < 3; i++) st[i] = ns[i];
     }
     for (int r = P.RF0 + P.RP; r < P.RN; r++) full_round(P, r);
+    for (int i = 0; i < 3; i++) st[i] = hcanon(st[i]);
   }
   void absorb(const std::vector<Fq>& e) {
     if (e.empty()) return;
