@@ -15,5 +15,5 @@ def test_inv_wave_model_by_and_pornin():
     for y in ys:
         r, batches, _ = M.inv_model_by(y)
         assert r * y % M.P == 1
-        assert batches <= 60  # inv_wave.h BY_MAX_BATCHES = 64
+        assert batches <= 73  # the 1091-divstep bound; inv_wave.h BY_MAX_BATCHES = 80
         assert M.inv_model(y) * y % M.P == 1

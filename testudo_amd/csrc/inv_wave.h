@@ -21,7 +21,8 @@
 // tools/inv_wave_model.py (inv_model_by; 52.6 batches on average, at most 55).
 //
 // Bounds (checked by the model): |u| + |v| <= 2^15 and limbs < 2^15, so a
-// limb sum stays below 2^31 in magnitude; the cofactors stay below 60 p.
+// limb sum stays below 2^31 in magnitude; the cofactors grow by at most p per
+// batch (below 80 p < 2^384).
 #pragma once
 #include "field29.h"
 #include "curve.h"
@@ -78,7 +79,10 @@ __device__ __forceinline__ uint32_t div_signed(int32_t t, uint32_t lane, bool& n
   return shift_down(limb);  // limb 0 is zero: / 2^15
 }
 
-constexpr int BY_MAX_BATCHES = 64;  // the model's maximum is 55
+// (49 d + 80) / 17 = 1091 divsteps bound the GCD for d = 377 bits
+// (Bernstein-Yang), i.e. 73 batches of 15; the loop stops at g = 0 (52.6
+// batches on average in the model), so the cap costs nothing
+constexpr int BY_MAX_BATCHES = 80;
 
 // low 30 bits of a signed sign-magnitude value (limbs 0 and 1), two's complement
 __device__ __forceinline__ uint32_t low30(uint32_t mag, bool neg) {
@@ -183,7 +187,7 @@ __device__ inline __attribute__((noinline)) Fq29 inv_wave(const Fq29& y) {
     ds = nds;
     es = nes;
   }
-  // f = +-1 for y != 0; then y^-1 = +-d (plain), |d| < 60 p
+  // f = +-1 for y != 0; then y^-1 = +-d (plain), |d| < 80 p
   const bool ok = (__ballot(f != (lane == 0 ? 1u : 0u)) & NLMASK) == 0;
   const uint32_t v = d;
   const bool vs = ds != fs;
@@ -202,7 +206,7 @@ __device__ inline __attribute__((noinline)) Fq29 inv_wave(const Fq29& y) {
     }
     r[j] = (uint32_t)w & r29::M;
   }
-  // r mod p: a quotient estimate from the top limbs (q <= 59, low by at most
+  // r mod p: a quotient estimate from the top limbs (q < 80, low by at most
   // one), then one conditional subtraction
   {
     const double dv = (double)r[13] * 536870912.0 + (double)r[12] + (double)r[11] * (1.0 / 536870912.0);

@@ -191,10 +191,10 @@ def inv_model_by(y):
         nds, nd = lincomb(d, ds, u, e, es, v, kd)
         nes, ne = lincomb(d, ds, q, e, es, r, ke)
         f, fs, g, gs, d, ds, e, es = nf, nfs, ng, ngs, nd, nds, ne, nes
-        assert batches <= 60
+        assert batches <= 80  # inv_wave.h BY_MAX_BATCHES (73 batches cover the 1091-divstep bound)
     assert from_limbs(f) == 1, from_limbs(f)
     dv = from_limbs(d)
-    assert dv < 60 * P
+    assert dv < 80 * P
     neg = ds != fs
     return (-dv if neg else dv) % P, batches, iters
 
