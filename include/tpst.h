@@ -79,7 +79,7 @@ int tpst_g1_msm_dev(tpst_ctx* ctx, const void* d_bases, const void* d_scalars, s
  * each rank's share of the points as the raw XYZZ sum (192 B: X, Y, ZZ, ZZZ,
  * Montgomery u64 limbs; no per-rank affine inversion), gathered as bytes,
  * then summed on one device to one canonical affine G1 (k shares, stride_bytes
- * apart in d_parts). */
+ * apart in d_parts; d_parts and stride_bytes 16-byte aligned, else TPST_E_ARG). */
 int tpst_g1_msm_xyzz_dev(tpst_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, void* d_out_xyzz);
 int tpst_g1_xyzz_sum_dev(tpst_ctx* ctx, const void* d_parts, size_t k, size_t stride_bytes, void* d_out);
 

@@ -161,14 +161,16 @@ def _msm_worker(rank, world, port, n, q):
         dist.destroy_process_group()
 
 
-def test_sharded_msm_gloo_world2():
+@pytest.mark.parametrize("n", [1000, 1 << 18])
+def test_sharded_msm_gloo_world2(n):
     """Strong-scaled MSM orchestration: two ranks take halves of the points,
     one all-gather of the shares, the combine on rank 0 equals the oracle MSM
-    of all points."""
+    of all points.  n = 2^18 gives each share exactly 2^17 points (the
+    window-group boundary configs[1] hits at 8 GPUs)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_msm_worker, args=(r, 2, port, 1000, q)) for r in range(2)]
+    procs = [ctx.Process(target=_msm_worker, args=(r, 2, port, n, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in procs]

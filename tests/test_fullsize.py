@@ -96,6 +96,61 @@ def test_fullsize_commit_open_n24(ctx):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world", [8])
+def test_fullsize_sharded_n24(ctx, world):
+    """BASELINE configs[3] in its sharded form (sqrt_pst.rs:121-143 row MSMs +
+    IPP, :198 c_u, then the opening), the world-`world` split run rank by rank
+    in one process on one GPU: each rank uploads only its column block
+    (from_evaluations_cols, 512 rows at world 8), writes [row commitments |
+    Miller partial] into its row of one (world, R*12+72) device tensor -- the
+    all-gather buffer of distributed.sharded_commit -- and its z_q / c_u
+    shares; rank 0's combines (final exponentiation read from the gathered
+    device buffer, mod-r sum, G1 sum) and the opening from q alone must give
+    the fixture's comm_list, T, v, U, PST proof and every MippProof element."""
+    import torch
+    from testudo_amd import sqrt_pst as S
+    n = 24
+    d = G.load("fullsize_n%d.json" % n)
+    m_col, m_row = n // 2, n - n // 2
+    S.srs_setup(ctx, d["srs_nv"], d["seed_srs"])
+    Z, k = S.fr_stream(d["seed_z"], 1 << n)
+    pt, _ = S.fr_stream(d["seed_z"], n, k)
+    C, N = 1 << m_col, 1 << m_row
+    R = C // world
+    dev = torch.device("cuda", 0)
+    gathered = torch.empty((world, R * 12 + 72), dtype=torch.int64, device=dev)
+    zq_parts = torch.empty((world, N * 4), dtype=torch.int64, device=dev)
+    cu = []
+    for g in range(world):
+        sl = S.Polynomial.from_evaluations_cols(ctx, Z, g * R, (g + 1) * R)
+        sl.commit_rows_partial_into(g * R, (g + 1) * R, gathered[g])
+        sl.get_q_partial_into(pt, g * R, (g + 1) * R, zq_parts[g])
+        own = gathered[g, :12 * R].cpu().numpy().view(np.uint64).reshape(R, 12)
+        cu.append(S.cu_partial(ctx, n, pt, g * R, (g + 1) * R, own))
+        del sl
+    del Z
+    comms = gathered[:, :12 * R].cpu().numpy().view(np.uint64).reshape(C, 12).copy()
+    assert hashlib.sha256(comms.tobytes()).hexdigest() == d["comms_sha256"]
+    T = S.gt_final_exp_product_gathered(ctx, gathered, R)
+    assert np.array_equal(T, _arr(d["T"], (72,)))
+    zq = S.fr_sum(ctx, zq_parts)
+    U = S.g1_sum(ctx, np.stack(cu))
+    assert np.array_equal(U, _arr(d["U"], (12,)))
+    pq = S.Polynomial.from_q(ctx, n, pt, zq, U)
+    v = pq.eval(pt)
+    assert np.array_equal(v, _arr(d["eval"], (4,)))
+    U2, pst_proof, mipp = pq.open(S.PoseidonTranscript(), comms, pt, T)
+    assert np.array_equal(U2, U)
+    assert np.array_equal(pst_proof, _arr(d["pst_proof"], (m_row, 24)))
+    assert np.array_equal(mipp.comms_t, _arr(d["comms_t"], (m_col, 2, 72)))
+    assert np.array_equal(mipp.comms_u, _arr(d["comms_u"], (m_col, 2, 12)))
+    assert np.array_equal(mipp.final_a, _arr(d["final_a"], (12,)))
+    assert np.array_equal(mipp.final_h, _arr(d["final_h"], (24,)))
+    assert np.array_equal(mipp.pst_proof_h, _arr(d["pst_proof_h"], (m_col, 12)))
+    assert S.verify(ctx, S.PoseidonTranscript(), U, pt, v, pst_proof, mipp, T)
+
+
+@pytest.mark.gpu
 def test_fullsize_groth16_2p20(ctx):
     """Groth16 at the R1CS leg's size (2^20 constraints and variables, 10
     inputs, domain 2^21): the device proof satisfies the pairing equation, a

@@ -180,14 +180,17 @@ def test_msm_long_buckets_small_n(ctx, g2):
     assert np.array_equal(got, ref)
 
 
-@pytest.mark.parametrize("world", [1, 2, 4, 8])
-def test_split_msm_shares_combine(ctx, world):
+@pytest.mark.parametrize("world,lg", [(1, 16), (2, 16), (4, 16), (8, 16), (2, 18), (8, 20)])
+def test_split_msm_shares_combine(ctx, world, lg):
     """Strong-scaled MSM pieces: the XYZZ shares of `world`
     equal point ranges (tpst_g1_msm_xyzz_dev), summed on the device
-    (tpst_g1_xyzz_sum_dev), equal the oracle MSM of all points."""
+    (tpst_g1_xyzz_sum_dev), equal the MSM of all points.  (2, 18) and (8, 20)
+    put exactly 2^17 points in each share -- the boundary of the
+    window-grouped pipeline that configs[1] split over 8 GPUs hits; there the
+    reference is (sum s_i k_i) G (bases k_i G)."""
     import torch
     from testudo_amd import sqrt_pst as S
-    n = 1 << 16
+    n = 1 << lg
     k, _ = orc.fr_stream(76, n)
     s, _ = orc.fr_stream(77, n)
     dev = torch.device("cuda", 0)
@@ -206,8 +209,31 @@ def test_split_msm_shares_combine(ctx, world):
     wide[::2] = parts
     out = S.g1_xyzz_combine(ctx, parts).cpu().numpy().view(np.uint64)
     out2 = S.g1_xyzz_combine(ctx, wide[::2]).cpu().numpy().view(np.uint64)
-    ref = orc.g1_msm(orc.g1_mul_gen(k), s, parallel=True)
+    if lg <= 16:
+        ref = orc.g1_msm(orc.g1_mul_gen(k), s, parallel=True)
+    else:
+        si = [limbs_to_int(r) for r in s]
+        ki = [limbs_to_int(r) for r in k]
+        ref = orc.g1_mul_gen(fr_array([sum(a * b for a, b in zip(si, ki)) % O.R]))[0]
     assert np.array_equal(out, ref) and np.array_equal(out2, ref)
+
+
+def test_xyzz_sum_rejects_misaligned_shares(ctx):
+    """k_xyzz_sum reads shares with 16-byte loads: a share pointer or stride
+    that is not 16-byte aligned is an argument error, not a misread."""
+    import torch
+    from testudo_amd import TpstError
+    dev = torch.device("cuda", 0)
+    buf = torch.zeros(3 * 26, dtype=torch.int64, device=dev)
+    out = torch.empty(12, dtype=torch.int64, device=dev)
+    with pytest.raises(TpstError):
+        ctx.g1_xyzz_sum_dev(buf.data_ptr(), 2, 200, out.data_ptr())  # stride % 16 != 0
+    with pytest.raises(TpstError):
+        ctx.g1_xyzz_sum_dev(buf.data_ptr() + 8, 2, 208, out.data_ptr())  # base % 16 != 0
+    ctx.torch_to_lib()
+    ctx.g1_xyzz_sum_dev(buf.data_ptr(), 2, 208, out.data_ptr())  # zero shares: ZZ = 0, infinity
+    ctx.lib_to_torch()
+    assert not out.cpu().numpy().any()
 
 
 def test_fr_sum_non_contiguous_gathered_view(ctx):

@@ -246,7 +246,9 @@ static __global__ void __launch_bounds__(64) k_xyzz_sum(const uint8_t* __restric
 
 extern "C" int tpst_g1_xyzz_sum_dev(tpst_ctx* ctx, const void* d_parts, size_t k, size_t stride_bytes, void* d_out) {
   if (!ctx || !d_out || (k && !d_parts)) return fail(ctx, TPST_E_ARG, "null argument");
-  if (k && (stride_bytes < sizeof(Xyzz<Fq>) || stride_bytes % 4)) return fail(ctx, TPST_E_ARG, "bad stride");
+  // k_xyzz_sum reads each share with 16-byte vector loads
+  if (k && (stride_bytes < sizeof(Xyzz<Fq>) || stride_bytes % 16 || ((uintptr_t)d_parts & 15)))
+    return fail(ctx, TPST_E_ARG, "shares must be 16-byte aligned with a 16-byte-multiple stride");
   std::lock_guard<std::mutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   ctx->io.reset();

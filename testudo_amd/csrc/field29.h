@@ -203,9 +203,16 @@ TPST_HD Fq29 sqr(const Fq29& a) {
 // bits [s, s + 29) of a 13-word little-endian value (s + 29 <= 416)
 TPST_HD uint32_t bits29(const uint32_t* w, int s) {
   const int q = s >> 5, o = s & 31;
-  const uint64_t lo = q < 13 ? w[q] : 0u;
-  const uint64_t hi = q + 1 < 13 ? w[q + 1] : 0u;
-  return (uint32_t)(((hi << 32) | lo) >> o) & r29::M;
+  const uint32_t lo = q < 13 ? w[q] : 0u;
+  const uint32_t hi = q + 1 < 13 ? w[q + 1] : 0u;
+#if defined(__HIP_DEVICE_COMPILE__)
+  // a funnel shift of two words: composing (hi << 32) | lo made the compiler
+  // read w[q], w[q + 1] as one unaligned 64-bit word from a private-memory
+  // copy of w (64 B/lane scratch in every accumulation kernel)
+  return __builtin_amdgcn_alignbit(hi, lo, (uint32_t)o) & r29::M;
+#else
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> o) & r29::M;
+#endif
 }
 
 // field.h Montgomery (x 2^384, 12 x u32) -> x 2^377 in radix 2^29:

@@ -561,16 +561,17 @@ __global__ void __launch_bounds__(ACC_BLOCK, MINW)
   const size_t c0 = t << lg;
   // entries with a bucket key: range[W] for msm_var (its sentinel tail is never sorted)
   const size_t m = mend ? (size_t)*mend : m_all;
+  using A = AccField<F>;
+  using C = typename A::T;
+  // the chunk's last segment, when its bucket continues past the chunk, is
+  // left in acc at the loop's end (no second accumulator live in the loop)
   uint32_t tail_key = sent;
-  Xyzz<F> tail = Xyzz<F>::inf();
+  Xyzz<C> acc = Xyzz<C>::inf();
   if (c0 < m) {
-    using A = AccField<F>;
-    using C = typename A::T;
     const size_t c1 = (c0 + ((size_t)1 << lg) < m) ? c0 + ((size_t)1 << lg) : m;
     uint32_t key = keys[c0];
     Affine<C> pt;
     if (key < sent) pt = A::in(fetch_point<F>(bases, phib, nbase, vals[c0]));
-    Xyzz<C> acc = Xyzz<C>::inf();
     for (size_t e = c0; e < c1; e++) {
       uint32_t key_n = sent;
       Affine<C> pt_n;
@@ -581,21 +582,24 @@ __global__ void __launch_bounds__(ACC_BLOCK, MINW)
       if (key < sent) {
         acc = add_affine(acc, pt);
         if (key_n != key) {
-          const bool starts = bstart[key] >= c0;
-          const bool ends = bend[key] <= c1;
-          if (starts && ends) {
-            store_xyzz(buckets, key, A::out(acc));
-          } else if (starts) {  // only the chunk's last segment can continue
-            tail = A::out(acc);
+          if (bend[key] <= c1) {  // the bucket ends in this chunk
+            // began here: complete; began earlier: the chunk's first segment
+            if (bstart[key] >= c0)
+              store_xyzz(buckets, key, A::out(acc));
+            else
+              store_xyzz(part, t, A::out(acc));
+            acc = Xyzz<C>::inf();
+          } else {  // continues: the chunk's last segment (e + 1 == c1)
             tail_key = key;
-          } else {  // only the chunk's first segment can have begun earlier
-            store_xyzz(part, t, A::out(acc));
           }
-          acc = Xyzz<C>::inf();
         }
       }
       key = key_n;
       pt = pt_n;
+    }
+    if (tail_key < sent && bstart[tail_key] < c0) {  // spans the whole chunk
+      store_xyzz(part, t, A::out(acc));
+      tail_key = sent;
     }
   }
   __threadfence_block();
@@ -604,11 +608,11 @@ __global__ void __launch_bounds__(ACC_BLOCK, MINW)
   const size_t t1 = ((size_t)bend[tail_key] - 1) >> lg;  // chunk of the bucket's last entry
   const size_t tb = (size_t)blockIdx.x * ACC_BLOCK + (ACC_BLOCK - 1);
   const size_t stop = t1 < tb ? t1 : tb;
-  for (size_t u = t + 1; u <= stop; u++) tail = add(tail, load_xyzz(part, u));
+  for (size_t u = t + 1; u <= stop; u++) acc = add(acc, load_acc(part, u));
   if (t1 <= tb)
-    store_xyzz(buckets, tail_key, tail);
+    store_acc(buckets, tail_key, acc);
   else
-    store_xyzz(bpart, blockIdx.x, tail);
+    store_acc(bpart, blockIdx.x, acc);
 }
 
 // buckets crossing a workgroup boundary: thread B finishes the bucket holding
@@ -1429,7 +1433,7 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
                 Arena::need(W, sizeof(Xyzz<F>)) + Arena::need(NG, sizeof(Xyzz<F>)) + Arena::need(W + 1, 4) +
                 Arena::need(glv ? n * PW : 1, 4) + Arena::need((size_t)sp.ntile * sp.nbins, 4) +
                 Arena::need(sp.nbins, 4) + Arena::need(sp.nbins + 1, 4) + Arena::need(NG, 4) +
-                Arena::need((size_t)NG * ((m >> (lg + 6)) + 1), 4) + 8192;
+                Arena::need((size_t)NG * (m / ((size_t)LONG_PARTS << lg) + 1), 4) + 8192;
   ar.reset();
   TPST_TRY(ar.reserve(need));
   uint32_t* keys = ar.take<uint32_t>(m);
@@ -1448,7 +1452,10 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   uint32_t* tab = ar.take<uint32_t>((size_t)sp.ntile * sp.nbins);
   uint32_t* btot = ar.take<uint32_t>(sp.nbins);
   uint32_t* bin0 = ar.take<uint32_t>(sp.nbins + 1);
-  const uint32_t lcap = (uint32_t)(m >> (lg + 6)) + 1;  // LONG_PARTS = 2^6 whole chunks per listed bucket
+  // a listed bucket spans more than LONG_PARTS chunks, so more than
+  // LONG_PARTS << lg entries, and buckets are disjoint: at most m / (LONG_PARTS
+  // << lg) of them in any group (the list can never overflow)
+  const uint32_t lcap = (uint32_t)(m / ((size_t)LONG_PARTS << lg)) + 1;
   uint32_t* lcnt = ar.take<uint32_t>(NG);
   uint32_t* llist = ar.take<uint32_t>((size_t)NG * lcap);
 

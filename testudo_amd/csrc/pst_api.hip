@@ -251,7 +251,7 @@ static int srs_install(tpst_ctx* ctx, int nv, const uint64_t* flat) {
   TPST_HIP(ctx, take(st->hmask, nv, 48));
   const size_t N = (size_t)1 << nv;
   TPST_HIP(ctx, batch_tables_build(s, st->pg[0]->u(), N, batch_window_bits(N), st->tables));
-  TPST_HIP(ctx, st->prep_scratch.alloc(g2_prepare_scratch((size_t)1 << nv)));
+  TPST_HIP(ctx, st->prep_scratch.alloc(g2_prepare_scratch((size_t)1 << nv)));  // released below
   for (int odd = 0; odd < 2 && odd < nv; odd++) {
     const size_t m = (size_t)1 << (nv - odd);
     TPST_HIP(ctx, st->hprep[odd].alloc(m * N_LINE_COEFFS * sizeof(LineCoeff)));
@@ -264,11 +264,23 @@ static int srs_install(tpst_ctx* ctx, int nv, const uint64_t* flat) {
     if (rc) return rc;
   }
   TPST_HIP(ctx, hipStreamSynchronize(s));
+  TPST_HIP(ctx, st->prep_scratch.alloc(0));
   srs_slot(ctx) = std::move(st);
   return TPST_OK;
 }
 
 static SrsState* srs_of(tpst_ctx* ctx) { return srs_slot(ctx).get(); }
+
+// scratch of the RNS G2 preparation (g2_prepare_scratch(n) bytes: residue
+// lines, ~53 KB per point) sized for the largest batch prepared since the
+// SRS was installed -- the install's 2^nv batch is released right after it
+// (217 MB at nv = 12); callers size it before enqueueing any stream work
+static int prep_scratch_for(tpst_ctx* ctx, SrsState* st, size_t n) {
+  const size_t b = g2_prepare_scratch(n);
+  if (st->prep_scratch.p && st->prep_scratch.bytes >= b) return TPST_OK;
+  TPST_HIP(ctx, st->prep_scratch.alloc(b));  // hipFree of a smaller one waits for its users
+  return TPST_OK;
+}
 
 // SplitMix64 Fr stream (same definition as the bench / oracle generators)
 static uint64_t splitmix(uint64_t seed, uint64_t i) {
@@ -806,6 +818,7 @@ static int commit_rows_partial(tpst_ctx* ctx, tpst_poly* p, size_t r0, size_t r1
     }
     return TPST_OK;
   }
+  if (int rc = prep_scratch_for(ctx, st, R)) return rc;
   DevBuf rows, cm, out, hsub, tt;
   TPST_HIP(ctx, rows.alloc(R * sizeof(Xyzz<Fq>)));
   TPST_HIP(ctx, cm.alloc(R * 96));
@@ -1281,6 +1294,8 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     TPST_HIP(ctx, st->t_A.alloc(fbt_words<Fq>(C) * 4));
     st->t_A_n = C;
   }
+  if (m >= 5)  // h^(r) prepared at odd rounds r >= 1 with r + 4 <= m: at most C / 2 points
+    if (int rc = prep_scratch_for(ctx, st, C / 2)) return rc;
   const uint32_t* H0 = st->ph[p->odd]->u();
   const LineCoeff* L0 = (const LineCoeff*)st->hprep[p->odd].p;
   const uint32_t* tA = st->t_A.u();
