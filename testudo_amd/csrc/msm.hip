@@ -48,11 +48,7 @@ static size_t device_simds() {
 }
 
 static int acc_chunk_lg(size_t m) {
-  static const size_t threads = [] {
-    const char* e = getenv("TPST_ACC_WAVES");
-    const int w = e ? atoi(e) : 0;
-    return (size_t)(w > 0 ? w : 8) * 64 * device_simds();
-  }();
+  static const size_t threads = (size_t)8 * 64 * device_simds();  // 8 waves of chunks per SIMD
   int lg = 5;
   while (lg < 8 && (m >> (lg + 1)) >= threads) lg++;
   return lg;
@@ -525,15 +521,10 @@ static __global__ void __launch_bounds__(SORTB_THREADS)
   for (uint32_t p = nz + t; p < len; p += SORTB_THREADS) keys[s + p] = sent;
 }
 
-// TPST_GATHER_MASK=<bits> (timing experiments only, wrong sums): every
-// gathered point index is masked to its low bits, so the same random access
-// pattern hits a cache-resident slice of the bases / table
-static __device__ uint32_t g_gather_mask = 0x7fffffffu;
-
 template <class F>
 __device__ __forceinline__ Affine<F> fetch_point(const uint32_t* bases, const uint32_t* phib, uint32_t nbase,
                                                 uint32_t v) {
-  const uint32_t idx = v & g_gather_mask;
+  const uint32_t idx = v & 0x7fffffffu;
   Affine<F> p = (idx < nbase) ? load_affine<F>(bases, idx) : load_affine<F>(phib, idx - nbase);
   if (v >> 31) p.y = neg(p.y);
   return p;
@@ -717,7 +708,7 @@ __global__ void __launch_bounds__(64, MINW)
   // every lane issues every staging load (the instruction is wave-wide);
   // lanes without a point load bases[0]
   auto stage_load = [&](int buf, uint32_t v, bool want) {
-    const uint32_t idx = v & g_gather_mask;
+    const uint32_t idx = v & 0x7fffffffu;
     const uint32_t* src = want ? ((idx < nbase) ? bases + 24 * (size_t)idx : phib + 24 * (size_t)(idx - nbase)) : bases;
 #pragma unroll
     for (int j = 0; j < 6; j++)
@@ -1084,13 +1075,9 @@ __global__ void __launch_bounds__(64) k_xyzz_to_affine_wave(const Xyzz<F>* __res
   if (threadIdx.x == 0) store_affine(out, i, a);
 }
 
-static size_t inv_wave_max() {
-  static const size_t v = [] {
-    const char* e = getenv("TPST_INV_WAVE_MAX");
-    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)4096;
-  }();
-  return v;
-}
+// up to this many points one wave-cooperative inverse per point
+// (k_xyzz_to_affine_wave); above it one lone-lane inverse per point
+constexpr size_t INV_WAVE_MAX = 4096;
 
 template <class F>
 hipError_t points_to_mont(hipStream_t s, const uint32_t* d_in, uint32_t* d_out, size_t n) {
@@ -1109,7 +1096,7 @@ hipError_t affine_from_mont(hipStream_t s, const uint32_t* d_in, uint32_t* d_out
 template <class F>
 hipError_t xyzz_to_affine_canonical(hipStream_t s, const Xyzz<F>* d_in, uint32_t* d_out, size_t n) {
   if (!n) return hipSuccess;
-  if (n <= inv_wave_max())
+  if (n <= INV_WAVE_MAX)
     k_xyzz_to_affine_wave<F><<<(unsigned)n, 64, 0, s>>>(d_in, d_out, n);
   else
     k_xyzz_to_affine_canonical<F><<<grid_for(n, 64), 64, 0, s>>>(d_in, d_out, n);
@@ -1273,61 +1260,28 @@ static hipError_t reduce_buckets2(Arena& ar, hipStream_t s, const Xyzz<F>* d_buc
   return hipGetLastError();
 }
 
-// TPST_MSM_FIXUP_QUAD=k: the fixups of the window groups g < k run one quad of
-// lanes per bucket (default 1: the last group's, on the MSM's tail; 0 = none)
-static int fixup_quad_groups() {
-  static const int v = [] {
-    const char* e = getenv("TPST_MSM_FIXUP_QUAD");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
+// the last window group's fixup (on the MSM's tail) runs one quad of lanes
+// per bucket; the aux-stream groups one lane per bucket at s_setprio 2
+constexpr int RED_PRIO = 2;
 
-// TPST_MSM_PRIO: s_setprio level of the aux-stream reductions (default 2)
-static int red_prio() {
-  static const int v = [] {
-    const char* e = getenv("TPST_MSM_PRIO");
-    return e ? atoi(e) : 2;
-  }();
-  return v;
-}
-
-// TPST_MSM_RED2: 0 = weighted-segment reduction everywhere, 1 (default) = the
-// two-level reduction for the aux-stream window groups, 2 = everywhere
-static int red2_mode() {
-  static const int v = [] {
-    const char* e = getenv("TPST_MSM_RED2");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
-
-// window groups of the variable-base MSM (TPST_MSM_GROUPS, default 3): with
-// more than one, the groups' bucket accumulations run top group first on the
-// main stream; each finished group's reduction and doubling chain run on an aux
-// stream under the next group's accumulation, so only the last group's
-// reduction and its c-doubling Horner remain after the accumulation
+// window groups of the variable-base MSM (3; sweep of 1-5 in
+// profiles/r02/sw2): with more than one, the groups' bucket accumulations run
+// top group first on the main stream; each finished group's reduction (the
+// two-level one) and doubling chain run on an aux stream under the next
+// group's accumulation, so only the last group's reduction and its
+// c-doubling Horner remain after the accumulation
 static int msm_groups(size_t n, int W) {
-  static const int env = [] {
-    const char* e = getenv("TPST_MSM_GROUPS");
-    return e ? atoi(e) : 0;
-  }();
   if (n < ((size_t)1 << 17) || W < 4) return 1;
-  int g = env > 0 ? env : 3;
+  int g = 3;
   if (g > (Arena::N_AUX_EV - 1) / 2) g = (Arena::N_AUX_EV - 1) / 2;
   return g > W ? W : g;
 }
 
-// window boundaries wb[0..NG] of the groups: TPST_MSM_SPLIT = window counts
-// from the bottom group up ("1,3,4"), else a short bottom group (~W/8
+// window boundaries wb[0..NG] of the groups: a short bottom group (~W/8
 // windows: its reduction and chain are the tail left after the accumulation)
 // and an even split of the rest -- 1,3,4 for the 2^20 G1 MSM, 1.3 % faster
 // than 2,3,3 in an interleaved A/B (profiles/r02/sw2)
 static void msm_group_bounds(int W, int NG, int* wb) {
-  static const std::string env = [] {
-    const char* e = getenv("TPST_MSM_SPLIT");
-    return std::string(e ? e : "");
-  }();
   if (NG == 1) {
     wb[0] = 0;
     wb[1] = W;
@@ -1336,47 +1290,11 @@ static void msm_group_bounds(int W, int NG, int* wb) {
     wb[0] = 0;
     for (int g = 1; g <= NG; g++) wb[g] = lo + (g - 1) * (W - lo) / (NG - 1);
   }
-  if (env.empty()) return;
-  int cnt[16], k = 0, tot = 0;
-  for (size_t i = 0; i < env.size() && k < 16;) {
-    const int v = atoi(env.c_str() + i);
-    if (v <= 0) return;
-    cnt[k++] = v;
-    tot += v;
-    const size_t j = env.find(',', i);
-    if (j == std::string::npos) break;
-    i = j + 1;
-  }
-  if (k != NG || tot != W) return;
-  wb[0] = 0;
-  for (int g = 0; g < NG; g++) wb[g + 1] = wb[g] + cnt[g];
-}
-
-// G2 window (TPST_G2_WINDOW overrides, for sweeps): a G2 bucket costs ~3x a G1
-// one in the fixup / reduction passes, so fewer, fuller buckets can pay for
-// the extra window of entries
-static int g2_window_bits(int c) {
-  static const int env = [] {
-    const char* e = getenv("TPST_G2_WINDOW");
-    return e ? atoi(e) : 0;
-  }();
-  return (env >= 4 && env <= 16) ? env : c;
-}
-
-static hipError_t gather_mask_init() {
-  static const hipError_t e = [] {
-    const char* v = getenv("TPST_GATHER_MASK");
-    if (!v) return hipSuccess;
-    const uint32_t mask = (1u << atoi(v)) - 1u;
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_gather_mask), &mask, 4);
-  }();
-  return e;
 }
 
 template <class F>
 hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint32_t* d_scalars, size_t n,
                    Xyzz<F>* d_out) {
-  TPST_TRY(gather_mask_init());
   if (n == 0) {
     Xyzz<F> inf = Xyzz<F>::inf();
     return hipMemcpyAsync(d_out, &inf, sizeof(inf), hipMemcpyHostToDevice, s);
@@ -1384,16 +1302,7 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   if (n > MSM_MAX_POINTS) return hipErrorInvalidValue;
   const bool glv = n >= 64;  // phi(x, y) = (beta x, y) on G1, (beta^2 x, y) on G2
   constexpr size_t PW = 2 * Words<F>::n;
-  int c = msm_window_bits(glv ? 2 * n : n);
-  if constexpr (std::is_same<F, Fq2>::value) {
-    c = g2_window_bits(c);
-  } else {
-    static const int env_c = [] {  // TPST_MSM_C: G1 window override (sweeps)
-      const char* e = getenv("TPST_MSM_C");
-      return e ? atoi(e) : 0;
-    }();
-    if (env_c >= 4 && env_c <= 22 && n >= 64) c = env_c;
-  }
+  const int c = msm_window_bits(glv ? 2 * n : n);
   const int W = glv ? num_windows_bits(c, 128) : num_windows(c);
   const uint32_t nb = 1u << (c - 1);
   const size_t per_win = (size_t)(glv ? 2 : 1) * n;  // entries of one window (zero digits included)
@@ -1409,14 +1318,9 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   if (NG > 1) TPST_TRY(ar.aux_init());
   int lg;
   if (NG > 1) {  // per-group launches: keep >= 4 waves per SIMD in each
-    static const int env_lg = [] {
-      const char* e = getenv("TPST_MSM_LG");
-      return e ? atoi(e) : 0;
-    }();
     static const size_t simds = device_simds();
     lg = 4;
     while (lg < 8 && ((m / NG) >> (lg + 1)) >= (size_t)4 * 64 * simds) lg++;
-    if (env_lg >= 3 && env_lg <= 8) lg = env_lg;
   } else {
     lg = acc_chunk_lg(m);
   }
@@ -1527,28 +1431,16 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
                                                                           bstart, bend, d_bases, phib, (uint32_t)n,
                                                                           lg, buckets, part);
     } else {
-      // waves per SIMD the register budget must allow (TPST_ACC_MINW, sweeps)
-      static const int minw = [] {
-        const char* e = getenv("TPST_ACC_MINW");
-        return e ? atoi(e) : 2;  // 3 and 4 spill (32 / 111 VGPRs) and measured slower
-      }();
+      // TPST_ACC_LDS=1: the next point staged through LDS (A/B of the
+      // coalesced staging against the register prefetch)
       static const bool lds = [] {
         const char* e = getenv("TPST_ACC_LDS");
         return e && atoi(e) != 0;
       }();
       const unsigned grid = grid_for(gchunks, 64);
-      if (lds && minw >= 3)
-        k_bucket_acc_short_lds<3><<<grid, 64, 0, bulk>>>(keys, vals, range, wlo, whi, sent, bstart, bend, d_bases,
-                                                          phib, (uint32_t)n, lg, buckets, part);
-      else if (lds)
+      if (lds)
         k_bucket_acc_short_lds<2><<<grid, 64, 0, bulk>>>(keys, vals, range, wlo, whi, sent, bstart, bend, d_bases,
                                                           phib, (uint32_t)n, lg, buckets, part);
-      else if (minw >= 4)
-        k_bucket_acc_short<F, 4><<<grid, 64, 0, bulk>>>(keys, vals, range, wlo, whi, sent, bstart, bend, d_bases,
-                                                         phib, (uint32_t)n, lg, buckets, part);
-      else if (minw == 3)
-        k_bucket_acc_short<F, 3><<<grid, 64, 0, bulk>>>(keys, vals, range, wlo, whi, sent, bstart, bend, d_bases,
-                                                         phib, (uint32_t)n, lg, buckets, part);
       else
         k_bucket_acc_short<F><<<grid, 64, 0, bulk>>>(keys, vals, range, wlo, whi, sent, bstart, bend, d_bases, phib,
                                                       (uint32_t)n, lg, buckets, part);
@@ -1564,30 +1456,27 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
     const LongList ll{lcnt + g, llist + (size_t)g * lcap, lcap};
     if constexpr (std::is_same<F, Fq2>::value)
       k_bucket_fixup_short_pair<<<grid_for(2 * (b1 - b0), 64), 64, 0, a>>>(bstart, bend, b0, b1, lg, part, buckets,
-                                                                          g ? red_prio() : 0, ll);
-    else if (g < fixup_quad_groups())
+                                                                          g ? RED_PRIO : 0, ll);
+    else if (g == 0)
       k_bucket_fixup_quad<F><<<grid_for(4 * (b1 - b0), 64), 64, 0, a>>>(bstart, bend, b0, b1, lg, part, buckets, ll);
     else
       k_bucket_fixup_short<F><<<grid_for(b1 - b0, 64), 64, 0, a>>>(bstart, bend, b0, b1, lg, part, buckets,
-                                                                    g ? red_prio() : 0, ll);
+                                                                    RED_PRIO, ll);
     TPST_TRY(hipGetLastError());
     k_bucket_fixup_long<F><<<LONG_GRID, LONG_THREADS, 0, a>>>(bstart, bend, lg, part, buckets, ll);
     TPST_TRY(hipGetLastError());
     if (g == 0) break;
-    if (red2_mode() >= 1 && red2_ok(nb))
-      TPST_TRY(reduce_buckets2<F>(ar, a, buckets + b0, (size_t)(whi - wlo), nb, win + wlo, red_prio()));
+    if (red2_ok(nb))
+      TPST_TRY(reduce_buckets2<F>(ar, a, buckets + b0, (size_t)(whi - wlo), nb, win + wlo, RED_PRIO));
     else
-      TPST_TRY(reduce_buckets<F>(ar, a, buckets + b0, (size_t)(whi - wlo), nb, win + wlo, red_prio()));
+      TPST_TRY(reduce_buckets<F>(ar, a, buckets + b0, (size_t)(whi - wlo), nb, win + wlo, RED_PRIO));
     k_window_chain<F><<<1, 64, 0, a>>>(win, wlo, whi, c, nullptr, 0, contrib + g);
     TPST_TRY(hipGetLastError());
     TPST_TRY(hipEventRecord(ar.aux_ev[2 * g + 1], a));
   }
   const int w1 = wb[1];  // group 0 = windows [0, w1)
   pf->begin(ST_REDUCE, s);
-  if (red2_mode() >= 2 && red2_ok(nb))
-    TPST_TRY(reduce_buckets2<F>(ar, s, buckets, (size_t)w1, nb, win, 0));
-  else
-    TPST_TRY(reduce_buckets<F>(ar, s, buckets, (size_t)w1, nb, win));
+  TPST_TRY(reduce_buckets<F>(ar, s, buckets, (size_t)w1, nb, win));  // the latency-bound short-segment one
   pf->end(ST_REDUCE, s);
   pf->begin(ST_COMBINE, s);
   for (int g = 1; g < NG; g++) TPST_TRY(hipStreamWaitEvent(s, ar.aux_ev[2 * g + 1], 0));
@@ -1960,8 +1849,7 @@ __global__ void __launch_bounds__(SB_THREADS) k_batch_sort_staged(const uint32_t
 hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint32_t* d_scalars, size_t rows,
                      size_t row_stride, size_t col_stride, Xyzz<Fq>* d_out) {
   if (rows == 0) return hipSuccess;
-  TPST_TRY(gather_mask_init());
-  const int c = t.c, W = t.W;
+    const int c = t.c, W = t.W;
   const size_t N = t.N;
   const uint32_t nb = 1u << (c - 1);
   const size_t m = rows * N * (size_t)W;
@@ -1970,11 +1858,7 @@ hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint3
   // chunk length: at least 4 waves of chunks per SIMD (TPST_K1_WAVES; the
   // 2^20 commit's 26.6 M entries take 64-entry chunks, measured 8.7 -> 8.4 ms
   // against the 32-entry chunks 8 waves per SIMD would give)
-  static const size_t k1_threads = [] {
-    const char* e = getenv("TPST_K1_WAVES");
-    const int w = e ? atoi(e) : 0;
-    return (size_t)(w > 0 ? w : 4) * 64 * device_simds();
-  }();
+  static const size_t k1_threads = (size_t)4 * 64 * device_simds();
   int lg = 5;
   while (lg < 8 && (m >> (lg + 1)) >= k1_threads) lg++;
   const size_t nchunk = (m + ((size_t)1 << lg) - 1) >> lg;
@@ -1997,7 +1881,7 @@ hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint3
   if (!pf) pf = &dummy;
   pf->begin(ST_BATCH_SORT, s);
   TPST_TRY(hipMemsetAsync(buckets, 0, nbk * sizeof(Xyzz<Fq>), s));  // ZZ = 0 == infinity
-  if (N <= (size_t)SB_THREADS * SB_SPT && nb <= SB_NB && !getenv("TPST_BATCH_SORT_DIRECT"))
+  if (N <= (size_t)SB_THREADS * SB_SPT && nb <= SB_NB)
     k_batch_sort_staged<<<nrow_blk, SB_THREADS, 0, s>>>(d_scalars, rows, N, row_stride, col_stride, c, W, keys,
                                                          entries, bstart, bend);
   else
@@ -2006,18 +1890,9 @@ hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint3
   TPST_TRY(hipGetLastError());
   pf->end(ST_BATCH_SORT, s);
   pf->begin(ST_BUCKET_ACC, s);
-  static const int minw = [] {  // TPST_K1_MINW: waves per SIMD the register budget allows (sweeps)
-    const char* e = getenv("TPST_K1_MINW");
-    return e ? atoi(e) : 2;
-  }();
-  if (minw >= 3)
-    k_bucket_acc_chunk<Fq, 3><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys, entries, m, nullptr, (uint32_t)nbk, bstart,
-                                                                    bend, t.d_table, nullptr, 0x7fffffffu, lg,
-                                                                    buckets, part, bpart);
-  else
-    k_bucket_acc_chunk<Fq><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys, entries, m, nullptr, (uint32_t)nbk, bstart,
-                                                                 bend, t.d_table, nullptr, 0x7fffffffu, lg, buckets,
-                                                                 part, bpart);
+  k_bucket_acc_chunk<Fq><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys, entries, m, nullptr, (uint32_t)nbk, bstart, bend,
+                                                               t.d_table, nullptr, 0x7fffffffu, lg, buckets, part,
+                                                               bpart);
   TPST_TRY(hipGetLastError());
   k_bucket_fixup<Fq><<<grid_for(nblk, 64), 64, 0, s>>>(keys, m, nullptr, (uint32_t)nbk, bstart, bend, lg, nblk,
                                                        part, bpart, buckets);
@@ -2025,12 +1900,8 @@ hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint3
   pf->end(ST_BUCKET_ACC, s);
   pf->begin(ST_REDUCE, s);
   // the two-level reduction (no per-segment scalar multiplications; 2^20
-  // commit 8.7 -> 8.2 ms, 2^24 unchanged); TPST_K1_RED=1: weighted segments
-  static const int k1_red = [] {
-    const char* e = getenv("TPST_K1_RED");
-    return e ? atoi(e) : 2;
-  }();
-  if (k1_red == 2 && red2_ok(nb))
+  // commit 8.7 -> 8.2 ms, 2^24 unchanged)
+  if (red2_ok(nb))
     TPST_TRY(reduce_buckets2<Fq>(ar, s, buckets, rows, nb, d_out, 0));
   else
     TPST_TRY(reduce_buckets<Fq>(ar, s, buckets, rows, nb, d_out));

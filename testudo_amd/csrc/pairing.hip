@@ -21,63 +21,10 @@ namespace tpst {
 
 static inline unsigned grid_for(size_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
 
-// ---- G2Prepared on the wave engine ----------------------------------------
-// One wave per G2 point; each doubling / addition step of pairing.h is four
-// stages (tools/gen_wave_ops.py G2_DBL1-4 / G2_ADD1-4) over a 44-slot region.
-constexpr int PW = 4;
-constexpr int PW_SLOTS = 64 + 44;
-constexpr int PW_OPS[] = {wave::OP_G2_DBL1, wave::OP_G2_DBL2, wave::OP_G2_DBL3, wave::OP_G2_DBL4,
-                          wave::OP_G2_ADD1, wave::OP_G2_ADD2, wave::OP_G2_ADD3, wave::OP_G2_ADD4};
-constexpr wave::OpSet<8> PW_SET(PW_OPS);
-constexpr int PW_PROG = PW_SET.words;
-constexpr size_t PW_LDS = (size_t)(PW_PROG + (wave::N_CONSTS + PW * PW_SLOTS) * wave::SLOT) * 4;
-static_assert(PW_LDS <= 65536, "prepare kernel LDS");
-
-__global__ void __launch_bounds__(64 * PW) k_g2_prepare_wave(const uint32_t* __restrict__ g2, size_t n,
-                                                             LineCoeff* __restrict__ coeffs) {
-  extern __shared__ uint4 smem4[];
-  wave::lds_t* prog = (wave::lds_t*)(smem4);
-  wave::lds_t* vals = prog + PW_PROG;
-  wave::load_set(prog, PW_SET);
-  wave::load_consts(vals, 0);
-  __syncthreads();
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const size_t pi = (size_t)blockIdx.x * PW + w;
-  if (pi >= n) return;
-  const G2A q = load_affine<Fq2>(g2, pi);
-  if (is_inf(q)) return;
-  const int base = wave::N_CONSTS + w * PW_SLOTS;
-  const wave::Eng e{vals, base, 0};
-  const int R = base + 64;
-  if (lane < 4) {
-    const Fq v = lane == 0 ? q.x.c0 : lane == 1 ? q.x.c1 : lane == 2 ? q.y.c0 : q.y.c1;
-    wave::put_slot(vals, R + lane, v);
-    wave::put_slot(vals, R + 26 + lane, v);
-  } else if (lane < 6) {
-    wave::put_slot(vals, R + lane, lane == 4 ? Fq::one() : Fq::zero());
-  }
-  wave::wave_sync();
-  Fq* cf = reinterpret_cast<Fq*>(coeffs);
-  int idx = 0;
-  for (int b = X_BITS - 2; b >= 0; b--) {
-#pragma unroll
-    for (int k = 0; k < 4; k++) wave::run(e, prog + PW_SET.off[k], R, R, R);
-    if (lane < 6) cf[((size_t)idx * n + pi) * 6 + lane] = wave::get_slot(vals, R + 6 + lane);
-    idx++;
-    if ((params::BLS_X >> b) & 1) {
-      wave::wave_sync();
-#pragma unroll
-      for (int k = 4; k < 8; k++) wave::run(e, prog + PW_SET.off[k], R, R, R);
-      if (lane < 6) cf[((size_t)idx * n + pi) * 6 + lane] = wave::get_slot(vals, R + 6 + lane);
-      idx++;
-    }
-    wave::wave_sync();
-  }
-}
-
 // ---- G2Prepared on the RNS engine ------------------------------------------
-// The same chain (one 44-slot region per point, the two halves of a
-// 12-wave workgroup holding two points): G2_DBL1-4 / G2_ADD1-4 as RNS stages,
+// The doubling / addition chain of pairing.h per G2 point (one 44-slot region
+// per point, the two halves of a 12-wave workgroup holding two points):
+// G2_DBL1-4 / G2_ADD1-4 (tools/gen_rns_ops.py) as RNS stages,
 // each step's line (region slots 6..11) dumped in residue form, then
 // k_rns_to_fq converts every coefficient to field.h form in bulk -- ~280
 // stages of ~1 us against the radix engine's ~6 us stages.
@@ -145,26 +92,16 @@ __global__ void __launch_bounds__(256) k_rns_to_fq(const uint32_t* __restrict__ 
 
 size_t g2_prepare_scratch(size_t n) { return n * N_LINE_COEFFS * 6 * 32 * sizeof(uint32_t); }
 
-static bool g2_rns() {
-  static const bool on = [] {  // TPST_G2_RNS=0: the radix-engine preparation (A/B)
-    const char* v = getenv("TPST_G2_RNS");
-    return v ? atoi(v) != 0 : true;
-  }();
-  return on;
-}
-
+// scratch: g2_prepare_scratch(n) bytes (the residue lines)
 hipError_t g2_prepare_batch(hipStream_t s, const uint32_t* d_g2, size_t n, LineCoeff* d_coeffs, uint32_t* scratch) {
   if (!n) return hipSuccess;
-  if (scratch && g2_rns()) {
-    k_g2_prepare_rns<<<(unsigned)((n + 1) / 2), 768, 0, s>>>(d_g2, n, scratch);
-    TPST_TRY(hipGetLastError());
-    const size_t count = n * N_LINE_COEFFS * 6;
-    const size_t waves = (count + 1) / 2;
-    const unsigned grid = (unsigned)(waves / 4 < 2048 ? (waves + 3) / 4 : 2048);
-    k_rns_to_fq<<<grid, 256, 0, s>>>(scratch, count, reinterpret_cast<Fq*>(d_coeffs));
-    return hipGetLastError();
-  }
-  k_g2_prepare_wave<<<grid_for(n, PW), 64 * PW, PW_LDS, s>>>(d_g2, n, d_coeffs);
+  if (!scratch) return hipErrorInvalidValue;
+  k_g2_prepare_rns<<<(unsigned)((n + 1) / 2), 768, 0, s>>>(d_g2, n, scratch);
+  TPST_TRY(hipGetLastError());
+  const size_t count = n * N_LINE_COEFFS * 6;
+  const size_t waves = (count + 1) / 2;
+  const unsigned grid = (unsigned)(waves / 4 < 2048 ? (waves + 3) / 4 : 2048);
+  k_rns_to_fq<<<grid, 256, 0, s>>>(scratch, count, reinterpret_cast<Fq*>(d_coeffs));
   return hipGetLastError();
 }
 
@@ -499,124 +436,11 @@ constexpr int BW_PROG = BW_SET.words;
 constexpr size_t BW_LDS = (size_t)(BW_PROG + (wave::N_CONSTS + BW * BW_SLOTS) * wave::SLOT) * 4;
 static_assert(BW_LDS <= 65536, "block-multiplier kernel LDS");
 
-// and MBn[o] = N(MB[o]), the Fq-norm of the block multiplier (the tower norms
-// of the final exponentiation's inversion, fe_final_exp), so that the chain
-// kernel can invert N(f) = prod_j N(MB_j)^(2^(LB j)) off its critical path
-__global__ void __launch_bounds__(64 * BW) k_miller_blocks(const Fq12* __restrict__ M, size_t groups,
-                                                           Fq12* __restrict__ MB, Fq* __restrict__ MBn) {
-  extern __shared__ uint4 smem4[];
-  wave::lds_t* prog = (wave::lds_t*)(smem4);
-  wave::lds_t* vals = prog + BW_PROG;
-  wave::load_set(prog, BW_SET);
-  wave::load_consts(vals, 0);
-  __syncthreads();
-  const int w = threadIdx.x >> 6;
-  const size_t o = (size_t)blockIdx.x * BW + w;
-  if (o >= groups * NBLK) return;
-  const size_t g = o / NBLK;
-  const int blk = (int)(o % NBLK);
-  const int lo = blk * LB, hi = (lo + LB < N_BITS ? lo + LB : N_BITS) - 1;
-  const int base = wave::N_CONSTS + w * BW_SLOTS;
-  const wave::Eng e{vals, base, 0};
-  int acc = base + 64, in_r = base + 76, tmp = base + 88;
-  const Fq12* Mg = M + g * N_LINE_COEFFS;
-  for (int b = hi; b >= lo; b--) {
-    const int idx = dbl_idx(b);
-    const bool add = (params::BLS_X >> b) & 1;
-    if (b == hi) {
-      wave::load_f12(vals, acc, Mg + idx);
-    } else {
-      wave::run(e, prog + BW_SET.off[1], acc, 0, tmp);  // acc^2
-      wave::load_f12(vals, in_r, Mg + idx);
-      wave::run(e, prog + BW_SET.off[0], tmp, in_r, acc);
-    }
-    if (add) {
-      wave::load_f12(vals, in_r, Mg + idx + 1);
-      wave::run(e, prog + BW_SET.off[0], acc, in_r, tmp);
-      const int t = acc;
-      acc = tmp;
-      tmp = t;
-    }
-  }
-  wave::store_f12(vals, acc, MB + o);
-  if (MBn) {
-    const int I = base + 76;  // in_r / tmp are free now: 15 slots of norm temporaries
-    wave::run(e, prog + BW_SET.off[2], acc, 0, I + 0);
-    wave::run(e, prog + BW_SET.off[3], I + 0, 0, I + 6);
-    wave::run(e, prog + BW_SET.off[4], I + 6, I + 0, I + 12);
-    wave::run(e, prog + BW_SET.off[5], I + 12, 0, I + 14);
-    if ((threadIdx.x & 63) == 0) MBn[o] = wave::get_slot(vals, I + 14);
-  }
-}
-
-// one wave per group: F = MB_top, F = F^(2^LB) MB_j, then (optionally) the
-// final exponentiation.  A second wave meanwhile runs the same Horner on the
-// blocks' Fq-norms and inverts the result -- N(F)^-1, the one Fq inversion of
-// the final exponentiation (~0.18 ms on a lone lane) -- so the first wave
-// finds it ready instead of waiting for it.
-constexpr size_t CH_LDS = (size_t)(FW_PROG + (wave::N_CONSTS + FW_SLOTS + FE_SLOTS) * wave::SLOT) * 4;
-static_assert(CH_LDS <= 65536, "chain kernel LDS");
-
-__global__ void __launch_bounds__(128) k_chain_final(const Fq12* __restrict__ MB, const Fq* __restrict__ MBn,
-                                                     Fq12* __restrict__ out, int do_final) {
-  extern __shared__ uint4 smem4[];
-  __shared__ Fq ninv_sh;
-  wave::lds_t* prog = (wave::lds_t*)(smem4);
-  wave::lds_t* vals = prog + FW_PROG;
-  wave::load_set(prog, FE_SET);
-  wave::load_consts(vals, 0);
-  __syncthreads();
-  const size_t g = blockIdx.x;
-  if (threadIdx.x >= 64) {  // norm wave
-    if (!do_final) return;
-    if (threadIdx.x == 64) {
-      const Fq* nb = MBn + g * NBLK;
-      Fq n = nb[NBLK - 1];
-      for (int blk = NBLK - 2; blk >= 0; blk--) {
-        for (int i = 0; i < LB; i++) n = sqr(n);
-        n = mul(n, nb[blk]);
-      }
-      ninv_sh = inv(n);
-    }
-    __syncthreads();  // hand-over: pairs with the one inside fe_final_exp
-    return;
-  }
-  const int base = wave::N_CONSTS;
-  const wave::Eng e{vals, base, 0};
-  int acc = base + 64, in_r = base + 76, tmp = base + 88;
-  const Fq12* MBg = MB + g * NBLK;
-  wave::load_f12(vals, acc, MBg + NBLK - 1);
-  for (int blk = NBLK - 2; blk >= 0; blk--) {
-    for (int i = 0; i < LB; i++) {
-      wave::run(e, prog + FE_SET.off[FE_SQR12], acc, 0, tmp);
-      const int t = acc;
-      acc = tmp;
-      tmp = t;
-    }
-    wave::load_f12(vals, in_r, MBg + blk);
-    wave::run(e, prog + FE_SET.off[FE_MUL], acc, in_r, tmp);
-    const int t = acc;
-    acc = tmp;
-    tmp = t;
-  }
-  if (!do_final) {
-    wave::store_f12(vals, acc, out + g);
-    return;
-  }
-  const int fe = wave::N_CONSTS + FW_SLOTS;
-  const int r = fe_final_exp(e, prog, acc, fe, fe + 120, &ninv_sh);
-  wave::store_f12(vals, r, out + g);
-}
-
 // ---- the same chain on the RNS engine (rns_engine.h) ------------------------
 // Two groups per workgroup (the two halves of every wave), twelve waves: one
 // per Fq12 output coefficient, so a stage is a dozen parallel RNS Montgomery
 // reductions instead of a wave's lone-lane product chain.  The Fq inversion of
 // the final exponentiation runs on lanes 0 / 32 of wave 0 between two stages.
-// TPST_CHAIN_RNS=0 keeps k_chain_final (A/B and fallback for the tests).
-#ifndef TPST_CHAIN_RNS
-#define TPST_CHAIN_RNS 1
-#endif
 constexpr int RC_WAVES = 12;
 constexpr int RC_SLOTS = rns::N_CONSTS + 36 + 10 * 12 + 24;
 static_assert((size_t)(RC_SLOTS * rns::SLOT + RC_WAVES * rns::XCH) * 4 <= 65536, "RNS chain LDS");
@@ -750,11 +574,7 @@ __global__ void __launch_bounds__(64 * RC_WAVES, 2) k_chunk_prod_rns(const void*
 
 // workgroups for a persistent RNS kernel over `pairs` work items
 static unsigned rns_grid(size_t pairs) {
-  static const unsigned per_cu = [] {
-    const char* v = getenv("TPST_RNS_WG_PER_CU");
-    return v ? (unsigned)atoi(v) : 2u;
-  }();
-  const size_t cap = (size_t)256 * (per_cu ? per_cu : 1);
+  const size_t cap = (size_t)256 * 2;  // two workgroups per CU
   return (unsigned)(pairs < cap ? pairs : cap);
 }
 
@@ -869,23 +689,7 @@ size_t multi_pairing_scratch(size_t groups, size_t n) {
 static hipError_t pairing_from_lines(Arena& ar, hipStream_t s, Fq12* lines, size_t groups, size_t n, Fq12* d_out,
                                      bool final_exp) {
   const size_t G = groups * N_LINE_COEFFS;
-  static const bool use_rns = [] {
-    const char* v = getenv("TPST_CHAIN_RNS");
-    return v ? atoi(v) != 0 : TPST_CHAIN_RNS != 0;
-  }();
-  static const bool tree_rns = [] {  // TPST_TREE_RNS=0: radix-engine tree levels (A/B)
-    const char* v = getenv("TPST_TREE_RNS");
-    return v ? atoi(v) != 0 : true;
-  }();
-  while (n > 1 && !(use_rns && tree_rns)) {
-    const size_t nout = (n + TREE_CHUNK - 1) / TREE_CHUNK;
-    Fq12* nxt = ar.take<Fq12>(G * nout);
-    k_f12_chunk_prod<<<grid_for(G * nout, RW), 64 * RW, RW_LDS, s>>>(lines, G, n, nout, nxt, TREE_CHUNK);
-    TPST_TRY(hipGetLastError());
-    lines = nxt;
-    n = nout;
-  }
-  if (use_rns) {
+  {
     // tree levels in RNS form (the first from the field.h line products)
     const void* cur = lines;
     bool res = false;
@@ -915,12 +719,6 @@ static hipError_t pairing_from_lines(Arena& ar, hipStream_t s, Fq12* lines, size
     k_chain_final_rns<<<pairs, 64 * RC_WAVES, 0, s>>>(MBr, groups, d_out, final_exp ? 1 : 0);
     return hipGetLastError();
   }
-  Fq12* MB = ar.take<Fq12>(groups * NBLK);
-  Fq* MBn = final_exp ? ar.take<Fq>(groups * NBLK) : nullptr;
-  k_miller_blocks<<<grid_for(groups * NBLK, BW), 64 * BW, BW_LDS, s>>>(lines, groups, MB, MBn);
-  TPST_TRY(hipGetLastError());
-  k_chain_final<<<(unsigned)groups, 128, CH_LDS, s>>>(MB, MBn, d_out, final_exp ? 1 : 0);
-  return hipGetLastError();
 }
 
 hipError_t multi_pairing_prepared(Arena& ar, hipStream_t s, const uint32_t* d_g1, const uint32_t* d_g2,
@@ -1122,20 +920,13 @@ hipError_t mipp_combine(hipStream_t s, Fq12* d_la8, const uint64_t* d_digits, Fq
 // The combination t = A0 A3 A1^(c^-1) A2^c needs the four exponentiated
 // look-ahead values to 253-bit exponents, known only once c is.  Their
 // squarings do not depend on c: right after the look-ahead (off the critical
-// path) k_gt_sq_table stores S_b[k] = X_b^(2^k), k < 64, for the four bases
-// X_b = la8[MIPP_POW_SEL[b]] (63 cyclotomic squarings each, one wave per base).
+// path) the table S_b[k] = X_b^(2^k), k < 64, is stored for the four bases
+// X_b = la8[MIPP_POW_SEL[b]] (63 cyclotomic squarings each).
 // With the base-x digits e = sum_i e_i x^i of the exponent (f^p = f^x in GT),
 //     X^e = prod_i frob^i( prod_{bit k of e_i} S[k] ),
-// a product of <= 256 table entries: k_gt_table_prod runs one workgroup per
-// (base, digit) -- 8 waves each multiply the entries of 8 bit positions, a
-// 3-level tree in LDS, then frob^i -- and two short tree levels finish
-// t_l = A0 A3 X_A1 X_A2 and t_r = B0 B3 X_B1 X_B2: ~17 wave-engine stages on the
-// critical path instead of ~140 (63 squarings + ~60 products + table).
-constexpr int SQ_OPS[] = {wave::OP_CYC_SQR};
-constexpr wave::OpSet<1> SQ_SET(SQ_OPS);
-constexpr size_t SQ_LDS = (size_t)(SQ_SET.words + (wave::N_CONSTS + 100) * wave::SLOT) * 4;
-static_assert(SQ_LDS <= 65536, "squaring-table kernel LDS");
-
+// a product of <= 256 table entries per (base, digit), then frob^i, and two
+// short tree levels finish t_l = A0 A3 X_A1 X_A2 and t_r = B0 B3 X_B1 X_B2
+// (kernels below, on the RNS engine).
 // tables of the bases src[sel[b]], b < n (one wave each); blocks n.. copy
 // src[cp.src[j]] (or 1 when cp.src[j] < 0) to dst[cp.dst[j]]
 struct SqPlan {
@@ -1147,50 +938,6 @@ struct CopyPlan {
   int src[12], dst[12];
 };
 
-__global__ void __launch_bounds__(64) k_gt_sq_table(const Fq12* __restrict__ src, SqPlan sp, Fq12* __restrict__ tab,
-                                                    CopyPlan cp, Fq12* __restrict__ dst) {
-  extern __shared__ uint4 smem4[];
-  wave::lds_t* prog = (wave::lds_t*)(smem4);
-  wave::lds_t* vals = prog + SQ_SET.words;
-  const int b = blockIdx.x;
-  const int lane = threadIdx.x & 63;
-  if (b >= sp.n) {  // the copies
-    for (int j = 0; j < cp.n; j++)
-      if (lane < 12) {
-        Fq v = Fq::zero();
-        if (cp.src[j] < 0) {
-          if (lane == 0) v = Fq::one();
-        } else {
-          v = reinterpret_cast<const Fq*>(src + cp.src[j])[lane];
-        }
-        reinterpret_cast<Fq*>(dst + cp.dst[j])[lane] = v;
-      }
-    return;
-  }
-  wave::load_set(prog, SQ_SET);
-  wave::load_consts(vals, 0);
-  __syncthreads();
-  const int base = wave::N_CONSTS;
-  const wave::Eng e{vals, base, 0};
-  int cur = base + 64, nxt = base + 76;
-  wave::load_f12(vals, cur, src + sp.sel[b]);
-  Fq12* T = tab + 64 * b;
-  for (int k = 0; k < 64; k++) {
-    wave::store_f12(vals, cur, T + k);
-    if (k == 63) break;
-    wave::run(e, prog, cur, 0, nxt);
-    const int t = cur;
-    cur = nxt;
-    nxt = t;
-  }
-}
-
-constexpr int TP_WAVES = 4;
-constexpr int TP_OPS[] = {wave::OP_F12_MUL, wave::OP_FROB1, wave::OP_FROB2};
-constexpr wave::OpSet<3> TP_SET(TP_OPS);
-constexpr size_t TP_LDS = (size_t)(TP_SET.words + (wave::N_CONSTS + TP_WAVES * 100) * wave::SLOT) * 4;
-static_assert(TP_LDS <= 65536, "table-product kernel LDS");
-
 // block (b, i): G[tp.out[b] + i] = frob^i( prod_{bit k of e_{b,i}} S_b[k] ),
 // e_{b,i} = digits[4 tp.dig[b] + i] (base-x digits, 4 x u64 per exponent).
 // Wave w multiplies the entries of bit positions [16 w, 16 w + 16) in its
@@ -1200,67 +947,6 @@ struct TpPlan {
   int n;
   int dig[12], out[12];
 };
-
-__global__ void __launch_bounds__(64 * TP_WAVES) k_gt_table_prod(const Fq12* __restrict__ tab,
-                                                                 const uint64_t* __restrict__ digits, TpPlan tp,
-                                                                 Fq12* __restrict__ G) {
-  extern __shared__ uint4 smem4[];
-  __shared__ int acc_of[TP_WAVES];
-  wave::lds_t* prog = (wave::lds_t*)(smem4);
-  wave::lds_t* vals = prog + TP_SET.words;
-  wave::load_set(prog, TP_SET);
-  wave::load_consts(vals, 0);
-  __syncthreads();
-  const int b = blockIdx.x >> 2, i = blockIdx.x & 3, w = threadIdx.x >> 6;
-  const uint64_t e_i = digits[4 * tp.dig[b] + i];
-  const int base = wave::N_CONSTS + w * 100;
-  const wave::Eng e{vals, base, 0};
-  auto reg = [&](int j) { return base + 64 + 12 * (j % 3); };
-  int acc = -1;  // register index 0..2 of the running product
-  const Fq12* T = tab + 64 * b;
-  constexpr int BITS = 64 / TP_WAVES;
-  for (int k = BITS * w; k < BITS * w + BITS; k++) {
-    if (!((e_i >> k) & 1)) continue;
-    if (acc < 0) {
-      acc = 0;
-      wave::load_f12(vals, reg(0), T + k);
-    } else {
-      wave::load_f12(vals, reg(acc + 1), T + k);
-      wave::run(e, prog + TP_SET.off[0], reg(acc), reg(acc + 1), reg(acc + 2));
-      acc = (acc + 2) % 3;
-    }
-  }
-  if (acc < 0) {
-    acc = 0;
-    wave::set_one(vals, reg(0));
-  }
-  if ((threadIdx.x & 63) == 0) acc_of[w] = acc;
-  __syncthreads();
-  for (int h = TP_WAVES / 2; h >= 1; h >>= 1) {
-    if (w < h) {
-      const int other = wave::N_CONSTS + (w + h) * 100 + 64 + 12 * acc_of[w + h];
-      wave::run(e, prog + TP_SET.off[0], reg(acc), other, reg(acc + 1));
-      acc = (acc + 1) % 3;
-    }
-    __syncthreads();
-    if (w < h && (threadIdx.x & 63) == 0) acc_of[w] = acc;
-    __syncthreads();
-  }
-  if (w != 0) return;
-  int r = acc;
-  if (i == 1) {
-    wave::run(e, prog + TP_SET.off[1], reg(r), 0, reg(r + 1));
-    r = (r + 1) % 3;
-  } else if (i == 2) {
-    wave::run(e, prog + TP_SET.off[2], reg(r), 0, reg(r + 1));
-    r = (r + 1) % 3;
-  } else if (i == 3) {
-    wave::run(e, prog + TP_SET.off[2], reg(r), 0, reg(r + 1));
-    wave::run(e, prog + TP_SET.off[1], reg(r + 1), 0, reg(r + 2));
-    r = (r + 2) % 3;
-  }
-  wave::store_f12(vals, reg(r), G + tp.out[b] + i);
-}
 
 // ---- the same combination on the RNS engine ---------------------------------
 // Tables and partial products stay in RNS form (rns::RES_WORDS u32 per Fq12):
@@ -1276,17 +962,6 @@ __global__ void __launch_bounds__(64 * TP_WAVES) k_gt_table_prod(const Fq12* __r
 //                       back to field.h Montgomery form
 // about 25 stages on the critical path after the challenge, against the
 // radix engine's ~17 slower stages and its table conversions.
-#ifndef TPST_GT_RNS
-#define TPST_GT_RNS 1
-#endif
-static bool gt_rns() {
-  static const bool on = [] {
-    const char* v = getenv("TPST_GT_RNS");
-    return v ? atoi(v) != 0 : TPST_GT_RNS != 0;
-  }();
-  return on;
-}
-
 __global__ void __launch_bounds__(64 * RC_WAVES) k_gt_sq_table_rns(const Fq12* __restrict__ src, SqPlan sp,
                                                                    uint32_t* __restrict__ tab, CopyPlan cp,
                                                                    uint32_t* __restrict__ G) {
@@ -1413,32 +1088,20 @@ hipError_t mipp_sq_tables(hipStream_t s, const Fq12* d_la8, Fq12* d_tab, Fq12* d
   // tables of A1 A2 B1 B2; A0 A3 / B0 B3 into slots 0, 1 of the two product lists
   const SqPlan sp{4, {2, 3, 6, 7}};
   const CopyPlan cp{4, {0, 1, 4, 5}, {0, 1, 10, 11}};
-  if (gt_rns())
-    k_gt_sq_table_rns<<<3, 64 * RC_WAVES, 0, s>>>(d_la8, sp, reinterpret_cast<uint32_t*>(d_tab), cp,
-                                                  reinterpret_cast<uint32_t*>(d_G));
-  else
-    k_gt_sq_table<<<5, 64, SQ_LDS, s>>>(d_la8, sp, d_tab, cp, d_G);
+  k_gt_sq_table_rns<<<3, 64 * RC_WAVES, 0, s>>>(d_la8, sp, reinterpret_cast<uint32_t*>(d_tab), cp,
+                                                reinterpret_cast<uint32_t*>(d_G));
   return hipGetLastError();
 }
 
 hipError_t mipp_combine_tab(hipStream_t s, const Fq12* d_tab, const uint64_t* d_digits, Fq12* d_G, Fq12* d_mid,
                             Fq12* d_out2) {
   const TpPlan tp{4, {0, 1, 2, 3}, {2, 6, 12, 16}};
-  if (gt_rns()) {
-    uint32_t* L1 = reinterpret_cast<uint32_t*>(d_mid);  // 128 partials
-    k_gt_tab_prod1_rns<<<64, 64 * RC_WAVES, 0, s>>>(reinterpret_cast<const uint32_t*>(d_tab), d_digits, tp, L1);
-    TPST_TRY(hipGetLastError());
-    k_gt_tab_prod2_rns<<<8, 64 * RC_WAVES, 0, s>>>(L1, tp, reinterpret_cast<uint32_t*>(d_G));
-    TPST_TRY(hipGetLastError());
-    k_gt_final_rns<<<1, 64 * RC_WAVES, 0, s>>>(reinterpret_cast<const uint32_t*>(d_G), d_out2);
-    return hipGetLastError();
-  }
-  k_gt_table_prod<<<16, 64 * TP_WAVES, TP_LDS, s>>>(d_tab, d_digits, tp, d_G);
+  uint32_t* L1 = reinterpret_cast<uint32_t*>(d_mid);  // 128 partials
+  k_gt_tab_prod1_rns<<<64, 64 * RC_WAVES, 0, s>>>(reinterpret_cast<const uint32_t*>(d_tab), d_digits, tp, L1);
   TPST_TRY(hipGetLastError());
-  // 2 groups x 10 factors -> 3 partials (chunk 4) -> 1
-  k_f12_chunk_prod<<<grid_for(2 * 3, RW), 64 * RW, RW_LDS, s>>>(d_G, 2, 10, 3, d_mid, 4);
+  k_gt_tab_prod2_rns<<<8, 64 * RC_WAVES, 0, s>>>(L1, tp, reinterpret_cast<uint32_t*>(d_G));
   TPST_TRY(hipGetLastError());
-  k_f12_chunk_prod<<<1, 64 * RW, RW_LDS, s>>>(d_mid, 2, 3, 1, d_out2, 3);
+  k_gt_final_rns<<<1, 64 * RC_WAVES, 0, s>>>(reinterpret_cast<const uint32_t*>(d_G), d_out2);
   return hipGetLastError();
 }
 

@@ -1,7 +1,6 @@
 // sqrt-PST protocol kernels for gfx950 (see pst_kernels.h).
 #include "device_util.h"
 #include "pst_kernels.h"
-#include "inv_wave.h"
 #include <cstdlib>
 
 namespace tpst {
@@ -207,73 +206,13 @@ __global__ void __launch_bounds__(64, 1) k_xyzz_to_affine_mont(const Xyzz<F>* __
   store_affine(out, i, to_affine(load_xyzz(in, i)));
 }
 
-// The same with one inverse per wave (Montgomery's batch trick across the
-// 64 lanes): each lane's Fq norm of ZZ ZZZ, a lane prefix and suffix product
-// (six shuffle + product steps each), one wave-cooperative inverse of the
-// wave's product (inv_wave.h), then each lane's own inverse from its
-// neighbours' products -- ~20 lone-lane products + one shared inverse instead
-// of one lone-lane inverse per point.
-__device__ __forceinline__ Fq shfl_fq(const Fq& a, int src_delta, bool up) {
-  Fq r;
-#pragma unroll
-  for (int k = 0; k < 12; k++)
-    r.v[k] = up ? __shfl_up(a.v[k], src_delta, 64) : __shfl_down(a.v[k], src_delta, 64);
-  return r;
-}
-__device__ __forceinline__ Fq lane_norm(const Fq& z) { return z; }
-__device__ __forceinline__ Fq lane_norm(const Fq2& z) { return add(sqr(z.c0), mul5(sqr(z.c1))); }
-__device__ __forceinline__ Fq from_norm_inv(const Fq& z, const Fq& ni) { (void)z; return ni; }
-__device__ __forceinline__ Fq2 from_norm_inv(const Fq2& z, const Fq& ni) { return {mul(z.c0, ni), neg(mul(z.c1, ni))}; }
-
-template <class F>
-__global__ void __launch_bounds__(64) k_xyzz_to_affine_batch(const Xyzz<F>* __restrict__ in, uint32_t* __restrict__ out,
-                                                           size_t n) {
-  const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
-  const int lane = threadIdx.x;
-  Xyzz<F> p = i < n ? load_xyzz(in, i) : Xyzz<F>::inf();
-  const bool inf = is_zero(p.ZZ);
-  const F z = inf ? F::one() : mul(p.ZZ, p.ZZZ);
-  const Fq nz = lane_norm(z);
-  // inclusive prefix and suffix products of the lane norms
-  Fq pre = nz, suf = nz;
-#pragma unroll 1
-  for (int d = 1; d < 64; d <<= 1) {
-    const Fq a = shfl_fq(pre, d, true), b = shfl_fq(suf, d, false);
-    if (lane >= d) pre = mul(pre, a);
-    if (lane + d < 64) suf = mul(suf, b);
-  }
-  Fq total;
-#pragma unroll
-  for (int k = 0; k < 12; k++) total.v[k] = (uint32_t)__builtin_amdgcn_readlane((int)pre.v[k], 63);
-  const Fq tinv = inv_w(total);
-  // this lane's norm inverse = tinv * prefix(lane - 1) * suffix(lane + 1)
-  Fq before = shfl_fq(pre, 1, true), after = shfl_fq(suf, 1, false);
-  if (lane == 0) before = Fq::one();
-  if (lane == 63) after = Fq::one();
-  const Fq ni = mul(tinv, mul(before, after));
-  if (i >= n) return;
-  const F t = from_norm_inv(z, ni);  // 1 / (ZZ ZZZ)
-  Affine<F> a = inf ? Affine<F>::inf() : Affine<F>{mul(p.X, mul(t, p.ZZZ)), mul(p.Y, mul(t, p.ZZ))};
-  store_affine(out, i, a);
-}
-
-// TPST_AFFINE_BATCH=1: one inverse per wave (default: one lone-lane inverse
-// per point, k_xyzz_to_affine_mont)
-static bool affine_batch() {
-  static const bool v = [] {
-    const char* e = getenv("TPST_AFFINE_BATCH");
-    return e && atoi(e) != 0;
-  }();
-  return v;
-}
+// (one inverse per wave by Montgomery's batch trick across the lanes was
+// measured within noise for the h vector of the opening: not kept)
 
 template <class F>
 hipError_t xyzz_to_affine_mont(hipStream_t s, const Xyzz<F>* d_in, uint32_t* d_out, size_t n) {
   if (!n) return hipSuccess;
-  if (affine_batch() && n >= 16)
-    k_xyzz_to_affine_batch<F><<<grid_for(n, 64), 64, 0, s>>>(d_in, d_out, n);
-  else
-    k_xyzz_to_affine_mont<F><<<grid_for(n, 64), 64, 0, s>>>(d_in, d_out, n);
+  k_xyzz_to_affine_mont<F><<<grid_for(n, 64), 64, 0, s>>>(d_in, d_out, n);
   return hipGetLastError();
 }
 

@@ -1110,19 +1110,11 @@ static int pst_open_fbt(tpst_ctx* ctx, SrsState* st, const uint32_t* table, int 
 static int open_streams(tpst_ctx* ctx, size_t n_events, size_t pinned_bytes) {
   int least = 0, greatest = 0;
   TPST_HIP(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
-  // TPST_OPEN_PRIO: bit i puts side stream i (0 = B, 1 / 2 = the look-ahead
-  // streams) at the greatest priority instead of the least.  Default 0: 6
-  // (look-ahead streams high) won an open-only sweep (14.2 -> 13.8 ms) but
-  // lost in the commit + open bench (2^20 open 12.3 -> 13.9 ms, 2^24 31.6 ->
-  // 33.6 ms; profiles/r04/late/prio6_bench*.json)
-  static const int hi_mask = [] {
-    const char* e = getenv("TPST_OPEN_PRIO");
-    return e ? atoi(e) : 0;
-  }();
+  // side streams at the least priority (the look-ahead streams at the
+  // greatest won an open-only sweep, 14.2 -> 13.8 ms, but lost in the commit +
+  // open bench: 2^20 open 12.3 -> 13.9 ms; profiles/r04/late/prio6_bench*.json)
   for (int i = 0; i < 3; i++)
-    if (!ctx->side[i])
-      TPST_HIP(ctx, hipStreamCreateWithPriority(&ctx->side[i], hipStreamNonBlocking,
-                                                ((hi_mask >> i) & 1) ? greatest : least));
+    if (!ctx->side[i]) TPST_HIP(ctx, hipStreamCreateWithPriority(&ctx->side[i], hipStreamNonBlocking, least));
   while (ctx->events.size() < n_events) {
     hipEvent_t e;
     TPST_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1232,11 +1224,9 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   // s = 0 for r <= 2.  That round work "C" rides on stream A: A's own round
   // work is two short table products, so C delays t^(r+1) by less than the
   // cross MSMs of stream B take, whereas on B it delayed every even round's
-  // comms_u by ~1 ms (TPST_OPEN_C_ON_B=1 restores that placement); the
-  // epilogue's final h fold runs on the first look-ahead stream (idle by
-  // then), beside final_a (A) and pst_proof_h (B)
-  static const bool c_on_b = getenv("TPST_OPEN_C_ON_B") != nullptr;
-  hipStream_t sA = ctx->stream, sB = ctx->side[0], sC = c_on_b ? ctx->side[0] : ctx->stream;
+  // comms_u by ~1 ms; the epilogue's final h fold runs on the first
+  // look-ahead stream (idle by then), beside final_a (A) and pst_proof_h (B)
+  const hipStream_t sA = ctx->stream, sB = ctx->side[0], sC = ctx->stream;
   const hipStream_t sCe = ctx->side[1];
   hipStream_t sLA[2] = {ctx->side[1], ctx->side[2]};
   Arena &arA = ctx->arena, &arB = ctx->arena_side[0], &arC = ctx->arena2;
@@ -1404,15 +1394,8 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     TPST_HIP(ctx, hipStreamWaitEvent(sB, ev_up(r), 0));
     if (r > 0) TPST_HIP(ctx, compress_fr(sB, Y.u(), len, dcp));  // y_l + c' y_r (mipp.rs:124-136)
     TPST_HIP(ctx, mipp_scalars(sB, dW, Y.u(), len, s, C, ScB.u()));
-    static const bool var0 = getenv("TPST_OPEN_VAR0") != nullptr;
-    if (r == 0 && var0) {
-      // (measured, not kept: round 0's u_l = sum_{k<s} Sc[k] a_k, u_r =
-      // sum_{k>=s} Sc[k] a_k as two variable-base MSMs over comm_list, to take
-      // the GLV fold table build (~1.25 ms at 2^20) off round 0's path -- two
-      // 512-point K2 MSMs took ~3.4 ms, the table path ~1.7 ms)
-      TPST_HIP(ctx, msm_var<Fq>(arB, sB, A.u(), ScB.u(), s, (Xyzz<Fq>*)xb.p));
-      TPST_HIP(ctx, msm_var<Fq>(arB, sB, A.u() + 24 * s, ScB.u() + 8 * s, s, (Xyzz<Fq>*)xb.p + 1));
-    } else {
+    {  // (round 0 as two variable-base K2 MSMs over comm_list, skipping the
+       // table build, measured slower: 3.4 vs 1.7 ms at 2^20)
       TPST_HIP(ctx, hipStreamWaitEvent(sB, ev[EV_TABLE], 0));
       FbGroups g;
       g.groups = 2;
@@ -1486,13 +1469,6 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     const double hp = open_trace() ? host_us() : 0.0;
     // -- C: h^(r) prepared at odd r for the look-aheads of rounds r+2, r+3
     if ((r & 1) && r + 4 <= m) {
-      // TPST_OPEN_C=la: behind this round's look-ahead on its stream (the
-      // look-ahead of round r+2, its first reader, runs there next)
-      static const bool c_on_la = [] {
-        const char* e = getenv("TPST_OPEN_C");
-        return e && !strcmp(e, "la");
-      }();
-      if (c_on_la) sC = sLA[r & 1];
       TPST_HIP(ctx, hipStreamWaitEvent(sC, ev_up(r), 0));
       if (r >= 5) TPST_HIP(ctx, hipStreamWaitEvent(sC, ev_la(r - 1), 0));  // last reader of h^(r-4)'s slot
       TPST_HIP(ctx, mipp_scalars(sC, dWi, nullptr, len, 0, C, ScC.u()));
