@@ -247,6 +247,42 @@ int tpst_poly_from_q_dev(tpst_ctx* ctx, int n, const uint64_t* point, const void
  * U = MSM(comms, chi(b)) over the caller's comm_list (sqrt_pst.rs:198). */
 int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, const uint64_t* comms,
                    const uint64_t* point, const uint64_t* T, tpst_open_proof* proof);
+/* Row-sharded Polynomial::open (the MIPP rounds of
+ * mipp.rs:58-120 split across `world` ranks, one process per GPU).  Rank g
+ * owns the rows i = g mod world of comm_list (and of h, y): while a round's
+ * length is >= 4 world its cross MSMs, folds, h preparations and look-ahead
+ * pairings run on the rank's own rows, and one all-gather per product
+ * combines them (cross partials summed, Miller partials multiplied before
+ * the final exponentiation); every rank replays the transcript.  At the first
+ * shorter round the folded a-vector (2 world points) is gathered to rank 0,
+ * which finishes the rounds and the epilogue alone.  Same proof bytes as
+ * tpst_poly_open on the same inputs.
+ *
+ * The library does no communication: `allgather` is the caller's transport
+ * (RCCL, gloo, MPI, ...).  It must gather `bytes` from d_arena + send_off of
+ * every rank into d_arena + recv_off (world x bytes, rank-major) ordered
+ * after the work queued on `stream` (a hipStream_t of the library) and before
+ * work queued on it afterwards -- e.g. an RCCL all-gather enqueued on that
+ * stream; return 0 on success.  Every rank issues the same gathers in the
+ * same order.  d_arena: device memory of arena_bytes >=
+ * tpst_open_sharded_arena_bytes(n, world), reachable by the transport.
+ *
+ * rank 0: p = the opening handle (tpst_poly_from_q_dev, or a whole
+ * polynomial) and `proof`; other ranks: p and proof may be NULL.  Every
+ * rank: the whole comm_list, the point, U = c_u (canonical affine, e.g. the
+ * combined tpst_poly_cu_partial shares) and its own transcript copy.  With
+ * fewer than 4 world rows rank 0 opens alone (the others return at once). */
+typedef int (*tpst_allgather_fn)(void* user, size_t send_off, size_t recv_off, size_t bytes, void* stream);
+typedef struct {
+  int world, rank;
+  tpst_allgather_fn allgather;
+  void* user;
+  void* d_arena;
+  size_t arena_bytes;
+} tpst_exchange;
+size_t tpst_open_sharded_arena_bytes(int n, int world);
+int tpst_poly_open_sharded(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, const uint64_t* comms,
+                           const uint64_t* point, const uint64_t* U, const tpst_exchange* x, tpst_open_proof* proof);
 /* Polynomial::verify (sqrt_pst.rs:232-264): TPST_OK if valid, TPST_E_VERIFY if
  * not, including any proof element that is non-canonical, off its curve or
  * outside the prime-order subgroup (checked before the transcript absorbs it). */

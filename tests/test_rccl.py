@@ -9,7 +9,8 @@ Checked bit for bit against the single-process library on the same inputs:
 the row-sharded commit (C1/C2: [row commitments | Miller partial] all-gather,
 final exponentiation read from the gathered device buffer), the opening
 inputs (C3: z_q / c_u shares, device mod-r sum of a non-contiguous gathered
-view), the opening from q alone, and the split (strong-scaled) MSM with its
+view), the opening from q alone, the sharded opening (C4, all-gathers on the
+library's comm stream through TorchExchange), and the split (strong-scaled) MSM with its
 device combine of the gathered XYZZ shares.
 """
 import os
@@ -78,6 +79,15 @@ def _child(port, n, n_msm, q):
             np.array_equal(getattr(mippq, f), getattr(mipp2, f))
             for f in ("comms_t", "comms_u", "final_a", "final_h", "pst_proof_h")))
         res["verified"] = bool(S.verify(ctx, S.PoseidonTranscript(), Uq, pt, vq, pstq, mippq, T))
+        # the sharded opening (C4) with its all-gathers through RCCL on the
+        # library's comm stream: a one-rank group runs every sharded round
+        # (len >= 4) and the hand-over to rank 0 at len = 2
+        from testudo_amd.distributed import sharded_open
+        pq2 = S.Polynomial.from_q(ctx, n, pt, zq, U)
+        Us, psts, mipps = sharded_open(ctx, n, pq2, comms, pt, U, S.PoseidonTranscript(), dist, dev)
+        res["sharded_open"] = bool(np.array_equal(Us, U2) and np.array_equal(psts, pst2) and all(
+            np.array_equal(getattr(mipps, f), getattr(mipp2, f))
+            for f in ("comms_t", "comms_u", "final_a", "final_h", "pst_proof_h")))
         # split MSM over the group, combined on the device
         sc, _ = S.fr_stream(0x7E57D5, n_msm)
         bk, _ = S.fr_stream(0x7E57D6, n_msm)

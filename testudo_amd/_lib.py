@@ -80,6 +80,8 @@ PROTOTYPES = [
     ("tpst_poly_cu_partial", C.c_int, [_vp, C.c_int, _u64p, _sz, _sz, _u64p, _u64p]),
     ("tpst_poly_from_q_dev", C.c_int, [_vp, C.c_int, _u64p, _vp, _u64p, C.POINTER(_vp)]),
     ("tpst_poly_open", C.c_int, [_vp, _vp, _vp, _u64p, _u64p, _u64p, _vp]),
+    ("tpst_open_sharded_arena_bytes", _sz, [C.c_int, C.c_int]),
+    ("tpst_poly_open_sharded", C.c_int, [_vp, _vp, _vp, C.c_int, _u64p, _u64p, _u64p, _vp, _vp]),
     ("tpst_pst_verify", C.c_int, [_vp, _vp, C.c_int, _u64p, _u64p, _u64p, _vp]),
     ("tpst_mlpc_commit", C.c_int, [_vp, _u64p, C.c_int, _u64p]),
     ("tpst_mlpc_commit_g2", C.c_int, [_vp, _u64p, C.c_int, _u64p]),
@@ -140,6 +142,16 @@ class OpenProof(C.Structure):
         ("final_h", C.c_uint64 * 24),
         ("pst_proof_h", (C.c_uint64 * 12) * MAX_VARS),
     ]
+
+# tpst_allgather_fn(user, send_off, recv_off, bytes, stream) -> 0 on success
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, _vp, _sz, _sz, _sz, _vp)
+
+
+class Exchange(C.Structure):
+    """tpst_exchange: the caller's all-gather for tpst_poly_open_sharded."""
+    _fields_ = [("world", C.c_int), ("rank", C.c_int), ("allgather", ALLGATHER_FN), ("user", _vp),
+                ("d_arena", _vp), ("arena_bytes", _sz)]
+
 
 R1CS_MAX_ROUNDS = 48
 

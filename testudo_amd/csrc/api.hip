@@ -67,6 +67,10 @@ extern "C" void tpst_destroy(tpst_ctx* ctx) {
     }
     ctx->arena_side[i].release();
   }
+  if (ctx->comm) {
+    (void)hipStreamSynchronize(ctx->comm);
+    (void)hipStreamDestroy(ctx->comm);
+  }
   for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
   if (ctx->ev_wait) (void)hipEventDestroy(ctx->ev_wait);
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);

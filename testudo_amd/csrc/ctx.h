@@ -20,6 +20,7 @@ struct tpst_ctx {
   // `stream` + side[0..2], each with its own scratch arena; created on first use
   hipStream_t side[3] = {nullptr, nullptr, nullptr};
   tpst::Arena arena_side[3];
+  hipStream_t comm = nullptr;      // the row-sharded opening's all-gathers (tpst_poly_open_sharded)
   std::vector<hipEvent_t> events;  // timing-free event pool of the opening
   hipEvent_t ev_wait = nullptr;    // tpst_wait_stream / tpst_join_stream
   hipEvent_t ev_join = nullptr;

@@ -445,7 +445,7 @@ constexpr int RC_WAVES = 12;
 constexpr int RC_SLOTS = rns::N_CONSTS + 36 + 10 * 12 + 24;
 static_assert((size_t)(RC_SLOTS * rns::SLOT + RC_WAVES * rns::XCH) * 4 <= 65536, "RNS chain LDS");
 
-__device__ int rc_exp_by_x(const rns::Eng& e, const rns::Lane& L, int src, int r1, int r2) {
+__device__ __forceinline__ int rc_exp_by_x(const rns::Eng& e, const rns::Lane& L, int src, int r1, int r2) {
   int cur = src;
   for (int b = X_BITS - 2; b >= 0; b--) {
     int nxt = cur == r1 ? r2 : r1;
@@ -461,7 +461,7 @@ __device__ int rc_exp_by_x(const rns::Eng& e, const rns::Lane& L, int src, int r
 }
 
 // fe_final_exp on the RNS engine (same chain, eprint 2020/875)
-__device__ int rc_final_exp(const rns::Eng& e, const rns::Lane& L, int F, int regs, int I, Fq* sh_n) {
+__device__ __forceinline__ int rc_final_exp(const rns::Eng& e, const rns::Lane& L, int F, int regs, int I, Fq* sh_n) {
   using namespace rns;
 #define R(i) (regs + 12 * (i))
   stage<OP_INV1>(e, L, F, 0, I + 0);         // t = c0^2 - v c1^2
@@ -768,7 +768,7 @@ size_t mipp_lookahead_scratch(size_t sp, int E) {
 }
 
 hipError_t mipp_lookahead(Arena& ar, hipStream_t s, const LineCoeff* d_coeffs, size_t ncol, const uint32_t* d_g2,
-                          const uint32_t* d_g1, bool xyzz, size_t len, int E, Fq12* d_out8) {
+                          const uint32_t* d_g1, bool xyzz, size_t len, int E, Fq12* d_out8, bool final_exp) {
   const size_t sp = len / 4;
   if (!sp || E < 1 || E > 8 || (E & (E - 1)) || ncol < (size_t)E * len) return hipErrorInvalidValue;
   const size_t n = sp * (size_t)E;
@@ -777,7 +777,43 @@ hipError_t mipp_lookahead(Arena& ar, hipStream_t s, const LineCoeff* d_coeffs, s
   k_line_pair<PairMapLA><<<grid_for(G * nout, 64), 64, 0, s>>>(d_coeffs, ncol, d_g1, xyzz ? 1 : 0, d_g2, 8, n,
                                                               PairMapLA{sp, len}, nout, lines);
   TPST_TRY(hipGetLastError());
-  return pairing_from_lines(ar, s, lines, 8, nout, d_out8, true);
+  return pairing_from_lines(ar, s, lines, 8, nout, d_out8, final_exp);
+}
+
+// ---- gathered Miller partials -> final exponentiation (row-sharded opening)
+// out[g] = FE(prod_{w < W} parts[w G + g]): the ranks' unreduced Miller
+// products of group g (look-ahead products, round 0's t_l / t_r) multiplied
+// and final-exponentiated on the RNS engine, two groups per workgroup (the
+// halves of every wave) -- W - 1 products + the chain of k_chain_final_rns
+__global__ void __launch_bounds__(64 * RC_WAVES) k_prod_final_rns(const Fq12* __restrict__ parts, size_t W,
+                                                                  size_t G, Fq12* __restrict__ out) {
+  __shared__ uint32_t s_slots[RC_SLOTS * rns::SLOT];
+  __shared__ uint32_t s_xch[RC_WAVES * rns::XCH];
+  __shared__ Fq sh_n[2];
+  const size_t g0 = 2 * (size_t)blockIdx.x, g1 = g0 + 1 < G ? g0 + 1 : g0;
+  rns::load_consts((rns::lds_t*)s_slots);
+  const rns::Lane L = rns::load_lane();
+  const rns::Eng e{(rns::lds_t*)s_slots, (rns::lds_t*)s_xch + rns::wave_id() * rns::XCH, 0};
+  __syncthreads();
+  int acc = rns::N_CONSTS, in_r = acc + 12, tmp = acc + 24;
+  rns::load(e, L, reinterpret_cast<const Fq*>(parts + g0), reinterpret_cast<const Fq*>(parts + g1), acc, 12);
+  for (size_t w = 1; w < W; w++) {
+    rns::load(e, L, reinterpret_cast<const Fq*>(parts + w * G + g0), reinterpret_cast<const Fq*>(parts + w * G + g1),
+              in_r, 12);
+    rns::stage<rns::OP_F12_MUL>(e, L, acc, in_r, tmp);
+    const int t = acc;
+    acc = tmp;
+    tmp = t;
+  }
+  const int r = rc_final_exp(e, L, acc, rns::N_CONSTS + 36, rns::N_CONSTS + 36 + 120, sh_n);
+  rns::store(e, L, r, reinterpret_cast<Fq*>(out + g0), reinterpret_cast<Fq*>(out + g1), 12);
+}
+
+hipError_t gt_prod_final(hipStream_t s, const Fq12* d_parts, size_t W, size_t G, Fq12* d_out) {
+  if (!G) return hipSuccess;
+  if (!W) return hipErrorInvalidValue;
+  k_prod_final_rns<<<(unsigned)((G + 1) / 2), 64 * RC_WAVES, 0, s>>>(d_parts, W, G, d_out);
+  return hipGetLastError();
 }
 
 hipError_t gt_product_final(Arena& ar, hipStream_t s, const Fq12* d_partials, size_t groups, size_t n, Fq12* d_out) {

@@ -58,8 +58,13 @@ hipError_t gt_pow_wave(hipStream_t s, const Fq12* d_base, const uint64_t* d_digi
 // true), paired against an earlier round's prepared h of row length
 // ncol = E len (E = 1, 2, 4, 8).  Scratch: mipp_lookahead_scratch(len / 4, E).
 size_t mipp_lookahead_scratch(size_t sp, int E);
+// final_exp = false: the 8 unreduced Miller products (a rank's partials of
+// the row-sharded opening, combined by gt_prod_final)
 hipError_t mipp_lookahead(Arena& ar, hipStream_t s, const LineCoeff* d_coeffs, size_t ncol, const uint32_t* d_g2,
-                          const uint32_t* d_g1, bool xyzz, size_t len, int E, Fq12* d_out8);
+                          const uint32_t* d_g1, bool xyzz, size_t len, int E, Fq12* d_out8, bool final_exp = true);
+// out[g] = FE(prod_{w < W} parts[w G + g]) for gathered Montgomery Miller
+// partials (W ranks x G groups), RNS engine
+hipError_t gt_prod_final(hipStream_t s, const Fq12* d_parts, size_t W, size_t G, Fq12* d_out);
 // round r+1's cross terms from the look-ahead products and c = c_r:
 // t_l = A0 A3 A1^(c^-1) A2^c, t_r = B0 B3 B1^(c^-1) B2^c.  d_digits: base-x
 // digits of (c^-1, c, c^-1, c) (4 x 4 u64); d_la8 is overwritten.

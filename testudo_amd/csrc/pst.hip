@@ -232,35 +232,55 @@ hipError_t affine_rot(hipStream_t s, const uint32_t* d_in, uint32_t* d_out, size
 // MIPP fold scalars over the original bases (fbt.h strided groups):
 // fold:  out[k] = W[k / len]                      (a^(r)_i = sum_t W_t a_{i + t len})
 // cross: out[k] = W[k / len] * y[(k % len + s) % len]   (u_l / u_r, mipp.rs:66-75)
+// out[kl] for the base k = sub kl + off (sub = 1, off = 0: every base; a
+// rank of a row-sharded opening takes its rows k = off mod sub)
 __global__ void k_mipp_scalars(const uint32_t* __restrict__ W, const uint32_t* __restrict__ y, size_t len, size_t s,
-                               size_t n, uint32_t* __restrict__ out) {
-  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
+                               size_t n, size_t sub, size_t off, uint32_t* __restrict__ out) {
+  const size_t kl = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (kl >= n) return;
+  const size_t k = sub * kl + off;
   Fr v = load_f<Fr>(W + 8 * (k / len));
   if (y) v = mul(v, load_f<Fr>(y + 8 * ((k % len + s) % len)));
-  store_f<Fr>(out + 8 * k, from_mont(v));
+  store_f<Fr>(out + 8 * kl, from_mont(v));
 }
 
 hipError_t mipp_scalars(hipStream_t s, const uint32_t* d_W, const uint32_t* d_y, size_t len, size_t split, size_t n,
-                        uint32_t* d_out) {
+                        uint32_t* d_out, size_t sub, size_t off) {
   if (!n) return hipSuccess;
-  k_mipp_scalars<<<grid_for(n, 256), 256, 0, s>>>(d_W, d_y, len, split, n, d_out);
+  k_mipp_scalars<<<grid_for(n, 256), 256, 0, s>>>(d_W, d_y, len, split, n, sub, off, d_out);
   return hipGetLastError();
 }
 
-// E fold sets at once: out[j n + k] = canonical(W[k / len] * f[j])
+// E fold sets at once: out[j n + kl] = canonical(W[k / len] * f[j]), k = sub kl + off
 __global__ void k_mipp_scalar_sets(const uint32_t* __restrict__ W, const uint32_t* __restrict__ f, int E, size_t len,
-                                   size_t n, uint32_t* __restrict__ out) {
+                                   size_t n, size_t sub, size_t off, uint32_t* __restrict__ out) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (size_t)E * n) return;
-  const size_t j = t / n, k = t % n;
+  const size_t j = t / n, k = sub * (t % n) + off;
   store_f<Fr>(out + 8 * t, from_mont(mul(load_f<Fr>(W + 8 * (k / len)), load_f<Fr>(f + 8 * j))));
 }
 
 hipError_t mipp_scalar_sets(hipStream_t s, const uint32_t* d_W, const uint32_t* d_f, int E, size_t len, size_t n,
-                            uint32_t* d_out) {
+                            uint32_t* d_out, size_t sub, size_t off) {
   if (!n || E <= 0) return hipSuccess;
-  k_mipp_scalar_sets<<<grid_for((size_t)E * n, 256), 256, 0, s>>>(d_W, d_f, E, len, n, d_out);
+  k_mipp_scalar_sets<<<grid_for((size_t)E * n, 256), 256, 0, s>>>(d_W, d_f, E, len, n, sub, off, d_out);
+  return hipGetLastError();
+}
+
+// out[g] = sum_{w < W} parts[w G + g] (XYZZ): the combine of gathered per-rank
+// partial sums, one lane per group
+__global__ void __launch_bounds__(64, 1) k_xyzz_sum_groups(const Xyzz<Fq>* __restrict__ parts, size_t W, size_t G,
+                                                          Xyzz<Fq>* __restrict__ out) {
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  Xyzz<Fq> acc = load_xyzz(parts, g);
+  for (size_t w = 1; w < W; w++) acc = add(acc, load_xyzz(parts, w * G + g));
+  store_xyzz(out, g, acc);
+}
+
+hipError_t xyzz_sum_groups(hipStream_t s, const Xyzz<Fq>* d_parts, size_t W, size_t G, Xyzz<Fq>* d_out) {
+  if (!G || !W) return hipSuccess;
+  k_xyzz_sum_groups<<<grid_for(G, 64), 64, 0, s>>>(d_parts, W, G, d_out);
   return hipGetLastError();
 }
 

@@ -170,6 +170,12 @@ struct SrsState {
   bool fbt_ready = false, t_h_ready[2] = {false, false};
   DevBuf t_A;                     // per-opening table over the row commitments
   size_t t_A_n = 0;
+  // a rank's share of the SRS side for the row-sharded opening (every W-th
+  // point of powers_of_h[odd] from `rank`, its prepared lines and table)
+  struct Local {
+    int W = 0, rank = -1;
+    DevBuf H0, L0, tH;
+  } local[2];
   // t_A prebuilt by tpst_poly_commit (beside its IPP) for exactly these
   // canonical row commitments; consumed by the next opening of them
   std::vector<uint64_t> t_A_key;
@@ -636,7 +642,7 @@ extern "C" int tpst_poly_eval(tpst_ctx* ctx, tpst_poly* p, const uint64_t* point
 }
 
 // commit (sqrt_pst.rs:117-149): K1 row MSMs + IPP T = prod e(C_i, h_i)
-static int open_streams(tpst_ctx* ctx, size_t n_events, size_t pinned_bytes);
+static int open_streams(tpst_ctx* ctx, size_t n_events, size_t pinned_bytes, bool comm = false);
 
 // prebuild (tpst_poly_commit): also build the opening's fold table over the
 // row commitments on a side stream while the IPP runs (TPST_COMMIT_TABLE=0 /
@@ -1107,7 +1113,7 @@ static int pst_open_fbt(tpst_ctx* ctx, SrsState* st, const uint32_t* table, int 
 
 // ---------------------------------------------------------------- open ----
 // Streams of the opening (created once per context) and a pool of events.
-static int open_streams(tpst_ctx* ctx, size_t n_events, size_t pinned_bytes) {
+static int open_streams(tpst_ctx* ctx, size_t n_events, size_t pinned_bytes, bool comm) {
   int least = 0, greatest = 0;
   TPST_HIP(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
   // side streams at the least priority (the look-ahead streams at the
@@ -1115,6 +1121,8 @@ static int open_streams(tpst_ctx* ctx, size_t n_events, size_t pinned_bytes) {
   // open bench: 2^20 open 12.3 -> 13.9 ms; profiles/r04/late/prio6_bench*.json)
   for (int i = 0; i < 3; i++)
     if (!ctx->side[i]) TPST_HIP(ctx, hipStreamCreateWithPriority(&ctx->side[i], hipStreamNonBlocking, least));
+  // the row-sharded opening's collectives, in one issue order on every rank
+  if (comm && !ctx->comm) TPST_HIP(ctx, hipStreamCreateWithPriority(&ctx->comm, hipStreamNonBlocking, greatest));
   while (ctx->events.size() < n_events) {
     hipEvent_t e;
     TPST_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1162,19 +1170,68 @@ static int open_streams(tpst_ctx* ctx, size_t n_events, size_t pinned_bytes) {
 //     G2Prepared, consumed by the look-ahead of round r+1.
 // The host waits only for the round's comms (pinned staging), absorbs them
 // (mipp.rs:97-101) and squeezes the challenge; no stream is drained mid-open.
-extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, const uint64_t* comms,
-                              const uint64_t* point, const uint64_t* T, tpst_open_proof* proof) {
-  (void)T;  // the reference passes T but the prover does not use it (mipp.rs:38)
-  if (!ctx || !p || !tr || !comms || !point || !proof) return fail(ctx, TPST_E_ARG, "null argument");
+//
+// Row-sharded form (sh != nullptr, tpst_poly_open_sharded):
+// rank g of W owns the rows i = g mod W of comm_list, h and y.  While
+// len >= 4W every fold group (a^(r)_i = sum_t W_t a_{i + t len}) lies on one
+// rank (i + t len = i mod W), and so does every look-ahead pair (positions
+// i + j s' share i's residue), so each rank runs the round on its own rows
+// with every size divided by W: its own table over its C / W commitments,
+// the look-ahead's folds and pairings over len / W positions, the h folds and
+// preparations of its positions, and the cross MSMs as partial sums over its
+// rows.  ONE all-gather per product combines them on every rank: the cross
+// partials summed (XYZZ), the Miller partials multiplied before the single
+// final exponentiation (gt_prod_final); every rank then combines t^(r) and
+// replays the transcript itself (no broadcast).  At the first round with
+// len < 4W the ranks gather the folded a^(r1) (len = 2W points) to rank 0,
+// which tabulates it and finishes the remaining rounds with the a-side
+// rebased on it (a^(r)_i = sum_{t < 2^(r - r1)} W_r[t] a^(r1)_{i + t len}:
+// the first weights of the same W_r) and the epilogue alone.  The exchange is
+// the caller's (tpst_exchange: RCCL, gloo, ...), ordered on a dedicated comm
+// stream so that every rank issues the same collectives in the same order.
+namespace {
+struct Shard {
+  int W = 1, rank = 0;
+  const tpst_exchange* x = nullptr;
+  const uint64_t* U = nullptr;  // c_u (canonical affine), every rank
+};
+
+size_t xch_align(size_t v) { return (v + 255) & ~(size_t)255; }
+size_t xch_slot(size_t bytes, int W) { return xch_align(bytes) + xch_align((size_t)W * bytes); }
+// first round whose look-ahead cannot be split over W ranks (len < 4W)
+int shard_rounds(int m, int W) {
+  int r1 = 0;
+  while (r1 < m && (((size_t)1 << m) >> r1) >= (size_t)4 * W) r1++;
+  return r1;
+}
+}  // namespace
+
+extern "C" size_t tpst_open_sharded_arena_bytes(int n, int world) {
+  if (n < 1 || n > 2 * TPST_MAX_VARS || world < 1 || (world & (world - 1))) return 0;
+  const int m = n / 2, r1 = shard_rounds(m, world);
+  if (r1 == 0) return 0;
+  constexpr size_t X1 = sizeof(Xyzz<Fq>), T12 = sizeof(Fq12);
+  return (size_t)r1 * (xch_slot(2 * X1, world) + xch_slot(8 * T12, world)) + xch_slot(2 * T12, world) +
+         xch_slot(2 * X1, world);
+}
+
+static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, const uint64_t* comms,
+                     const uint64_t* point, tpst_open_proof* proof, const Shard* sh) {
+  const bool shd = sh != nullptr;
+  const int W = shd ? sh->W : 1, rho = shd ? sh->rank : 0;
+  const bool lead = rho == 0;  // produces the proof (and the PST proof of q)
   std::lock_guard<std::mutex> lk(ctx->mu);
-  if (int rc = poly_need_q_source(ctx, p)) return rc;
+  if (lead)
+    if (int rc = poly_need_q_source(ctx, p)) return rc;
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   SrsState* st = srs_of(ctx);
   if (!st) return fail(ctx, TPST_E_STATE, "no SRS loaded");
-  if (st->nv != p->m_row) return fail(ctx, TPST_E_ARG, "SRS num_vars != ceil(n/2)");
-  for (size_t i = 0; i < ((size_t)2 << p->m_col); i++)
+  int m, k, odd;
+  if (poly_dims(n, m, k, odd)) return fail(ctx, TPST_E_ARG, "bad num_vars");
+  if (st->nv != k) return fail(ctx, TPST_E_ARG, "SRS num_vars != ceil(n/2)");
+  for (size_t i = 0; i < ((size_t)2 << m); i++)
     if (!fq_ok(comms + 6 * i)) return fail(ctx, TPST_E_ARG, "comm_list coordinate >= p");
-  if (!p->has_q) {  // before the reference's open timer (sqrt_pst.rs:177-183)
+  if (lead && !p->has_q) {  // before the reference's open timer (sqrt_pst.rs:177-183)
     int rc = poly_get_q(ctx, p, point);
     if (rc) return rc;
   }
@@ -1182,12 +1239,18 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   Profiler& pf = ctx->prof;
   pf.begin(ST_SQRT_OPEN, ctx->stream);
   {
-    int rc = srs_fbt(ctx, st, p->odd);
+    int rc = srs_fbt(ctx, st, odd);
     if (rc) return rc;
   }
-  const int m = p->m_col;
-  const int k = p->m_row;
   const size_t C = (size_t)1 << m;
+  // the rounds split across the ranks: [0, r1); rank 0 alone from r1 on
+  const int r1 = shd ? shard_rounds(m, W) : 0;
+  const size_t Cl = C / W;  // a rank's rows (i = rho mod W)
+  std::unique_ptr<tpst_open_proof> own_proof;
+  if (!proof) {  // a rank other than 0 fills nothing the caller reads
+    own_proof.reset(new tpst_open_proof);
+    proof = own_proof.get();
+  }
   memset(proof, 0, sizeof *proof);
   proof->m_col = m;
   proof->m_row = k;
@@ -1213,8 +1276,8 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   const size_t dn_U = up_bytes, dn_round = dn_U + X1, dn_final = dn_round + (size_t)m * DN_ROUND;
   const size_t dn_fh = dn_final + X1, dn_ph = dn_fh + X2, dn_pst = dn_ph + (size_t)m * 96;
   const size_t dn_bytes = X1 + (size_t)m * DN_ROUND + X1 + X2 + (size_t)m * 96 + (size_t)k * 192;
-  const size_t n_ev = 8 + 5 * (size_t)m;
-  if (int rc = open_streams(ctx, n_ev, up_bytes + dn_bytes)) return rc;
+  const size_t n_ev = 8 + 6 * (size_t)m + (shd ? 8 * (size_t)m + 8 : 0);
+  if (int rc = open_streams(ctx, n_ev, up_bytes + dn_bytes, shd)) return rc;
   uint8_t* pin = (uint8_t*)ctx->pinned;
   // four hardware queues: A (critical), B (cross terms), and two look-ahead
   // streams for alternating rounds -- consecutive look-aheads overlap, each
@@ -1233,24 +1296,70 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   Arena* arLA[2] = {&ctx->arena_side[1], &ctx->arena_side[2]};
   hipEvent_t* ev = ctx->events.data();
   enum { EV_PRE, EV_TABLE, EV_U, EV_FINAL_UP, EV_B_DONE, EV_C_DONE, EV_D_DONE, EV_A_DONE };
-  auto ev_up = [&](int r) { return ev[8 + 5 * r]; };
-  auto ev_a = [&](int r) { return ev[8 + 5 * r + 1]; };
-  auto ev_b = [&](int r) { return ev[8 + 5 * r + 2]; };
-  auto ev_c = [&](int r) { return ev[8 + 5 * r + 3]; };
+  auto ev_up = [&](int r) { return ev[8 + 6 * r]; };
+  auto ev_a = [&](int r) { return ev[8 + 6 * r + 1]; };
+  auto ev_b = [&](int r) { return ev[8 + 6 * r + 2]; };
+  auto ev_c = [&](int r) { return ev[8 + 6 * r + 3]; };
+  auto ev_la = [&](int r) { return ev[8 + 6 * r + 4]; };
+  auto ev_cl = [&](int r) { return ev[8 + 6 * r + 5]; };  // the rank's own h positions prepared
+  hipEvent_t* xev = ev + 8 + 6 * m;                         // exchange events (sharded form)
   int last_c = -1;  // the last odd round that issued h work "C"
-  auto ev_la = [&](int r) { return ev[8 + 5 * r + 4]; };
   // the prepared h the look-ahead of round r pairs against (see above)
   auto la_src = [](int r) { return r <= 2 ? 0 : (r & 1) ? r - 2 : r - 3; };
+  // which odd rounds prepare h: for a look-ahead on the rank's own positions
+  // (local, sharded rounds) or on every position (global)
+  std::vector<char> need_loc(m + 1, 0), need_glob(m + 1, 0);
+  for (int r = 1; r < m; r++) {
+    if ((C >> r) < 4 || la_src(r) == 0) continue;
+    if (shd && r < r1)
+      need_loc[la_src(r)] = 1;
+    else if (lead)
+      need_glob[la_src(r)] = 1;
+  }
+
+  // ---- exchange (sharded form): slots in the caller's arena, one comm stream
+  size_t x_off = 0;
+  int x_n = 0;
+  struct Slot {
+    uint8_t* send;
+    uint8_t* recv;
+    size_t send_off, recv_off;
+  };
+  auto slot = [&](size_t bytes) {
+    Slot sl;
+    sl.send_off = x_off;
+    sl.recv_off = x_off + xch_align(bytes);
+    x_off += xch_slot(bytes, W);
+    sl.send = (uint8_t*)sh->x->d_arena + sl.send_off;
+    sl.recv = (uint8_t*)sh->x->d_arena + sl.recv_off;
+    return sl;
+  };
+  // every rank's `bytes` at its slot's send -> recv (rank-major), ordered
+  // after the work queued on `s` so far; `s` then waits for the result
+  auto gather = [&](hipStream_t s, const Slot& sl, size_t bytes) -> int {
+    hipEvent_t e0 = xev[2 * x_n], e1 = xev[2 * x_n + 1];
+    x_n++;
+    TPST_HIP(ctx, hipEventRecord(e0, s));
+    TPST_HIP(ctx, hipStreamWaitEvent(ctx->comm, e0, 0));
+    if (sh->x->allgather(sh->x->user, sl.send_off, sl.recv_off, bytes, (void*)ctx->comm))
+      return fail(ctx, TPST_E_STATE, "exchange all-gather failed");
+    TPST_HIP(ctx, hipEventRecord(e1, ctx->comm));
+    TPST_HIP(ctx, hipStreamWaitEvent(s, e1, 0));
+    return TPST_OK;
+  };
+  if (shd && (sh->x->arena_bytes < tpst_open_sharded_arena_bytes(n, W) || !sh->x->d_arena || !sh->x->allgather))
+    return fail(ctx, TPST_E_ARG, "exchange arena smaller than tpst_open_sharded_arena_bytes");
 
   // ---- device buffers (allocated before any stream runs: no hipFree mid-open)
   const size_t Ch = C > 1 ? C / 2 : 1;
+  const size_t Ca0 = shd ? Cl : C;  // a-side bases resident: own rows or all
   DevBuf up, A, P, Y, chiC, ScA, ScB, ScC, ScD[2], xa, xb, xd, xh, xp, xl[2], LAo[2], Hb[2], Lb[2], gts, canA, canC,
-      canD, pstA, pstB, Wall, Wiall, SqT[2], SqG[2], SqM;
+      canD, pstA, pstB, Wall, Wiall, SqT[2], SqG[2], SqM, chis_own, tLoc, A1x, A1, tA1, Hbl[2], Lbl[2];
   TPST_HIP(ctx, up.alloc(up_bytes));
   TPST_HIP(ctx, Wall.alloc(2 * C * 32));  // round r's 2^r fold weights at offset 2^r - 1
   TPST_HIP(ctx, Wiall.alloc(2 * C * 32));
-  TPST_HIP(ctx, A.alloc(C * 96));
-  TPST_HIP(ctx, P.alloc(C * 96));
+  TPST_HIP(ctx, A.alloc(Ca0 * 96));
+  TPST_HIP(ctx, P.alloc(Ca0 * 96));
   TPST_HIP(ctx, Y.alloc(C * 32));
   TPST_HIP(ctx, chiC.alloc(C * 32));
   TPST_HIP(ctx, ScA.alloc(2 * C * 32));
@@ -1264,6 +1373,10 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   for (int i = 0; i < 2; i++) {
     TPST_HIP(ctx, Hb[i].alloc(Ch * 192));
     TPST_HIP(ctx, Lb[i].alloc(Ch * N_LINE_COEFFS * sizeof(LineCoeff)));
+    if (shd) {
+      TPST_HIP(ctx, Hbl[i].alloc((Ch / W ? Ch / W : 1) * 192));
+      TPST_HIP(ctx, Lbl[i].alloc((Ch / W ? Ch / W : 1) * N_LINE_COEFFS * sizeof(LineCoeff)));
+    }
   }
   TPST_HIP(ctx, gts.alloc(2 * sizeof(Fq12)));
   for (int i = 0; i < 2; i++) {
@@ -1280,41 +1393,103 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   TPST_HIP(ctx, canD.alloc(96 + (size_t)k * 192));
   TPST_HIP(ctx, pstA.alloc(pst_open_scratch_words(st, m) * 4));
   TPST_HIP(ctx, pstB.alloc(pst_open_scratch_words(st, k) * 4));
-  if (st->t_A_n < C) {
+  if (!shd && st->t_A_n < C) {
     TPST_HIP(ctx, st->t_A.alloc(fbt_words<Fq>(C) * 4));
     st->t_A_n = C;
   }
-  if (m >= 5)  // h^(r) prepared at odd rounds r >= 1 with r + 4 <= m: at most C / 2 points
-    if (int rc = prep_scratch_for(ctx, st, C / 2)) return rc;
-  const uint32_t* H0 = st->ph[p->odd]->u();
-  const LineCoeff* L0 = (const LineCoeff*)st->hprep[p->odd].p;
-  const uint32_t* tA = st->t_A.u();
-  const uint32_t* tH = st->t_h[p->odd].u();
+  if (shd) {
+    TPST_HIP(ctx, tLoc.alloc(fbt_words<Fq>(Cl) * 4));
+    const size_t len1 = C >> r1;
+    TPST_HIP(ctx, A1x.alloc(len1 * X1));
+    TPST_HIP(ctx, A1.alloc(len1 * 96));
+    TPST_HIP(ctx, tA1.alloc(fbt_words<Fq>(len1) * 4));
+  }
+  {  // G2 preparation scratch: h^(r) at odd rounds (global: <= C / 2 points, a rank's: <= C / 2W)
+    size_t mx = 0;
+    for (int r = 1; r <= m; r++) {
+      if (need_glob[r]) mx = std::max(mx, C >> r);
+      if (need_loc[r]) mx = std::max(mx, (C >> r) / W);
+    }
+    if (mx)
+      if (int rc = prep_scratch_for(ctx, st, mx)) return rc;
+  }
+  const uint32_t* H0 = st->ph[odd]->u();
+  const LineCoeff* L0 = (const LineCoeff*)st->hprep[odd].p;
+  const uint32_t* tH = st->t_h[odd].u();
+  // a rank's own positions of the SRS side (every W-th of h, its prepared
+  // lines and its table), cached per (W, rank, parity)
+  const uint32_t *H0l = H0, *tHl = tH;
+  const LineCoeff* L0l = L0;
+  if (shd) {
+    SrsState::Local& lc = st->local[odd];
+    if (lc.W != W || lc.rank != rho) {
+      const size_t tb = fbt_words<Fq2>(1) * 4;  // one point's table block
+      const size_t lb = sizeof(LineCoeff);
+      TPST_HIP(ctx, lc.H0.alloc(Cl * 192));
+      TPST_HIP(ctx, lc.L0.alloc(Cl * N_LINE_COEFFS * lb));
+      TPST_HIP(ctx, lc.tH.alloc(Cl * tb));
+      TPST_HIP(ctx, hipMemcpy2DAsync(lc.H0.p, 192, (const uint8_t*)H0 + 192 * rho, 192 * W, 192, Cl,
+                                     hipMemcpyDeviceToDevice, sA));
+      // coefficient-major [idx][pair]: row idx * Cl + j of the copy is column
+      // W (idx * Cl + j) + rho of the cache (C = W Cl)
+      TPST_HIP(ctx, hipMemcpy2DAsync(lc.L0.p, lb, (const uint8_t*)L0 + lb * rho, lb * W, lb, Cl * N_LINE_COEFFS,
+                                     hipMemcpyDeviceToDevice, sA));
+      TPST_HIP(ctx, hipMemcpy2DAsync(lc.tH.p, tb, (const uint8_t*)tH + tb * rho, tb * W, tb, Cl,
+                                     hipMemcpyDeviceToDevice, sA));
+      lc.W = W;
+      lc.rank = rho;
+    }
+    H0l = lc.H0.u();
+    L0l = (const LineCoeff*)lc.L0.p;
+    tHl = lc.tH.u();
+  }
+  const uint32_t* tA = shd ? tLoc.u() : st->t_A.u();  // the a-side table (rebased at the hand-over)
+  size_t Ca = Ca0;                                    // its base count
   auto dup = [&](size_t byte_off) { return (uint32_t*)((uint8_t*)up.p + byte_off); };
 
-  // ---- prologue (stream A): comm_list -> Montgomery, y = chi(b), canonical chi
+  // ---- prologue (stream A): this rank's comm_list rows -> Montgomery, y = chi(b), canonical chi
   {
     uint8_t* a_stage = pin + up_off[m] + (2 + m) * 32;  // a_rev (canonical) -> D
     for (int i = 0; i < k; i++) memcpy(a_stage + 32 * i, point + 4 * (k - 1 - i), 32);
   }
-  TPST_HIP(ctx, hipMemcpyAsync(A.p, comms, C * 96, hipMemcpyHostToDevice, sA));  // pageable: staged by HIP
-  TPST_HIP(ctx, points_to_mont<Fq>(sA, A.u(), A.u(), C));
-  TPST_HIP(ctx, hipMemcpyAsync(Y.p, p->chis.p, C * 32, hipMemcpyDeviceToDevice, sA));
-  TPST_HIP(ctx, fr_from_mont(sA, p->chis.u(), chiC.u(), C));
+  if (shd) {
+    std::vector<uint64_t> own(Cl * 12);
+    for (size_t j = 0; j < Cl; j++) memcpy(&own[12 * j], comms + 12 * (W * j + rho), 96);
+    TPST_HIP(ctx, hipMemcpyAsync(A.p, own.data(), Cl * 96, hipMemcpyHostToDevice, sA));
+    TPST_HIP(ctx, hipStreamSynchronize(sA));  // `own` is pageable and local
+  } else {
+    TPST_HIP(ctx, hipMemcpyAsync(A.p, comms, C * 96, hipMemcpyHostToDevice, sA));  // pageable: staged by HIP
+  }
+  TPST_HIP(ctx, points_to_mont<Fq>(sA, A.u(), A.u(), Ca0));
+  const uint32_t* chis = nullptr;
+  if (lead) {
+    chis = p->chis.u();
+  } else {
+    if (int rc = chi_b_table(ctx, m, k, point, chis_own)) return rc;
+    chis = chis_own.u();
+  }
+  TPST_HIP(ctx, hipMemcpyAsync(Y.p, chis, C * 32, hipMemcpyDeviceToDevice, sA));
+  TPST_HIP(ctx, fr_from_mont(sA, chis, chiC.u(), C));
   TPST_HIP(ctx, hipEventRecord(ev[EV_PRE], sA));
   for (hipStream_t s2 : {sB, sLA[0], sLA[1]}) TPST_HIP(ctx, hipStreamWaitEvent(s2, ev[EV_PRE], 0));
   pf.begin(ST_MIPP_PROVE, sA);  // mipp.rs:38-149 (sqrt_pst.rs:211-214)
   TraceRange trace_mipp("mipp_prove");
 
   // ---- look-ahead stream 1 (idle until round 1): the fold table over comm_list
-  // (prebuilt by the commit of exactly these row commitments: used once)
-  const bool prebuilt = st->t_A_key.size() == 12 * C && !memcmp(st->t_A_key.data(), comms, C * 96);
-  st->t_A_key.clear();
-  if (!prebuilt) TPST_HIP(ctx, fbt_build<Fq>(*arLA[1], sLA[1], A.u(), C, st->t_A.u(), true));
+  // (prebuilt by the commit of exactly these row commitments: used once), or
+  // over this rank's rows
+  if (shd) {
+    TPST_HIP(ctx, fbt_build<Fq>(*arLA[1], sLA[1], A.u(), Cl, tLoc.u(), true));
+  } else {
+    const bool prebuilt = st->t_A_key.size() == 12 * C && !memcmp(st->t_A_key.data(), comms, C * 96);
+    st->t_A_key.clear();
+    if (!prebuilt) TPST_HIP(ctx, fbt_build<Fq>(*arLA[1], sLA[1], A.u(), C, st->t_A.u(), true));
+  }
   TPST_HIP(ctx, hipEventRecord(ev[EV_TABLE], sLA[1]));
   // ---- stream B: U = MSM(comm_list, chi(b)) on that table, or the c_u the
-  // ranks combined for an opening-only handle
-  if (p->has_u) {
+  // ranks combined
+  const uint64_t* U_given = shd ? sh->U : (p->has_u ? p->U : nullptr);
+  if (U_given) {
     TPST_HIP(ctx, hipEventRecord(ev[EV_U], sB));
   } else {
     TPST_HIP(ctx, hipStreamWaitEvent(sB, ev[EV_TABLE], 0));
@@ -1343,7 +1518,7 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     pf.end(ST_PST_OPEN, sB);
     return TPST_OK;
   };
-  if (m == 0)
+  if (m == 0 && lead)
     if (int rc = pst_q()) return rc;
 
   // W_r[t] / Wi_r[t] (device, mipp_weights): products of the challenges
@@ -1353,9 +1528,11 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   Fr cprev = Fr::one(), cprev_c = Fr::one();
   uint64_t la_digits[16] = {};
   bool have_U = false;
+  hipEvent_t ev_t1 = nullptr;  // the table over the gathered a^(r1) (rank 0, sharded form)
   for (int r = 0; r < m; r++) {  // mipp.rs:58-120
     const double hq = open_trace() ? host_us() : 0.0;
     const size_t len = C >> r, s = len / 2, nW = (size_t)1 << r;
+    const bool loc = shd && r < r1;  // this round on the rank's own rows
     // stage c_{r-1}, c_{r-1}^-1, the look-ahead factors and digits; upload
     // once (stream B, whose previous work -- the round's comms_u -- is
     // already done when the challenge exists: on A the upload queued behind
@@ -1386,6 +1563,38 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     TPST_HIP(ctx, hipEventRecord(ev_up(r), sB));
     TPST_HIP(ctx, hipStreamWaitEvent(sA, ev_up(r), 0));
 
+    if (shd && r == r1) {
+      // -- hand-over: a^(r1) (len = 2W positions) folded by the owners of its
+      // positions, gathered; rank 0 tabulates it and continues alone
+      const size_t per = len / W;
+      TPST_HIP(ctx, hipStreamWaitEvent(sB, ev[EV_TABLE], 0));
+      TPST_HIP(ctx, mipp_scalars(sB, dW, nullptr, len, 0, Cl, ScB.u(), W, rho));
+      FbGroups g;
+      g.groups = per;
+      g.members = C / len;
+      g.L = per;
+      g.D = 1;
+      g.glv = true;
+      const Slot sl = slot(per * X1);
+      TPST_HIP(ctx, fbt_msm<Fq>(arB, sB, tA, ScB.u(), g, (Xyzz<Fq>*)sl.send));
+      if (int rc = gather(sB, sl, per * X1)) return rc;
+      if (!lead) {  // this rank's part is done
+        for (hipStream_t s2 : {sA, sB, sLA[0], sLA[1], ctx->comm}) TPST_HIP(ctx, hipStreamSynchronize(s2));
+        sp.store(tr);
+        return TPST_OK;
+      }
+      // recv[w][j] = a^(r1) at position W j + w
+      for (int w = 0; w < W; w++)
+        TPST_HIP(ctx, hipMemcpy2DAsync((uint8_t*)A1x.p + w * X1, W * X1, sl.recv + (size_t)w * per * X1, X1, X1, per,
+                                       hipMemcpyDeviceToDevice, sB));
+      TPST_HIP(ctx, xyzz_to_affine_mont<Fq>(sB, (const Xyzz<Fq>*)A1x.p, A1.u(), len));
+      TPST_HIP(ctx, fbt_build<Fq>(arB, sB, A1.u(), len, tA1.u(), true));
+      ev_t1 = xev[2 * x_n];  // past the gathers' events
+      TPST_HIP(ctx, hipEventRecord(ev_t1, sB));
+      tA = tA1.u();
+      Ca = len;
+    }
+
     // -- B: y fold by the previous challenge, cross MSMs u_l / u_r
     // (u_l = a[:s]^y[s:], u_r = a[s:]^y[:s], on the comm_list table); B is
     // enqueued first: its comms_u gate the transcript, and the look-ahead
@@ -1393,27 +1602,48 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     uint8_t* dn_r = pin + dn_round + (size_t)r * DN_ROUND;
     TPST_HIP(ctx, hipStreamWaitEvent(sB, ev_up(r), 0));
     if (r > 0) TPST_HIP(ctx, compress_fr(sB, Y.u(), len, dcp));  // y_l + c' y_r (mipp.rs:124-136)
-    TPST_HIP(ctx, mipp_scalars(sB, dW, Y.u(), len, s, C, ScB.u()));
     {  // (round 0 as two variable-base K2 MSMs over comm_list, skipping the
        // table build, measured slower: 3.4 vs 1.7 ms at 2^20)
       TPST_HIP(ctx, hipStreamWaitEvent(sB, ev[EV_TABLE], 0));
       FbGroups g;
       g.groups = 2;
-      g.members = C / len * s;
-      g.L = len;
-      g.D = s;
       g.glv = true;
-      TPST_HIP(ctx, fbt_msm<Fq>(arB, sB, tA, ScB.u(), g, (Xyzz<Fq>*)xb.p));
+      if (loc) {  // partial sums over this rank's rows, gathered and summed
+        TPST_HIP(ctx, mipp_scalars(sB, dW, Y.u(), len, s, Cl, ScB.u(), W, rho));
+        g.members = C / len * s / W;
+        g.L = len / W;
+        g.D = s / W;
+        const Slot sl = slot(2 * X1);
+        TPST_HIP(ctx, fbt_msm<Fq>(arB, sB, tA, ScB.u(), g, (Xyzz<Fq>*)sl.send));
+        if (int rc = gather(sB, sl, 2 * X1)) return rc;
+        TPST_HIP(ctx, xyzz_sum_groups(sB, (const Xyzz<Fq>*)sl.recv, W, 2, (Xyzz<Fq>*)xb.p));
+      } else {
+        TPST_HIP(ctx, mipp_scalars(sB, dW, Y.u(), len, s, Ca, ScB.u()));
+        g.members = Ca / len * s;
+        g.L = len;
+        g.D = s;
+        TPST_HIP(ctx, fbt_msm<Fq>(arB, sB, tA, ScB.u(), g, (Xyzz<Fq>*)xb.p));
+      }
     }
     TPST_HIP(ctx, hipMemcpyAsync(dn_r, xb.p, 2 * X1, hipMemcpyDeviceToHost, sB));
     TPST_HIP(ctx, hipEventRecord(ev_b(r), sB));
     const double hb = open_trace() ? host_us() : 0.0;
     // -- A: t_l / t_r of this round
     if (r == 0) {  // direct: the rotated comm_list (affine) against h^(0)
-      TPST_HIP(ctx, affine_rot(sA, A.u(), P.u(), C, 24));
-      arA.reset();
-      TPST_HIP(ctx, arA.reserve(multi_pairing_scratch(2, s)));
-      TPST_HIP(ctx, multi_pairing_prepared(arA, sA, P.u(), H0, L0, 2, s, (Fq12*)gts.p, true, s, 0));
+      if (loc) {  // this rank's pairs (a_i, h_{s+i}), (a_{s+i}, h_i), i = rho mod W
+        TPST_HIP(ctx, affine_rot(sA, A.u(), P.u(), Cl, 24));
+        arA.reset();
+        TPST_HIP(ctx, arA.reserve(multi_pairing_scratch(2, s / W)));
+        const Slot sl = slot(2 * sizeof(Fq12));
+        TPST_HIP(ctx, multi_pairing_prepared(arA, sA, P.u(), H0l, L0l, 2, s / W, (Fq12*)sl.send, false, s / W, 0));
+        if (int rc = gather(sA, sl, 2 * sizeof(Fq12))) return rc;
+        TPST_HIP(ctx, gt_prod_final(sA, (const Fq12*)sl.recv, W, 2, (Fq12*)gts.p));
+      } else {
+        TPST_HIP(ctx, affine_rot(sA, A.u(), P.u(), C, 24));
+        arA.reset();
+        TPST_HIP(ctx, arA.reserve(multi_pairing_scratch(2, s)));
+        TPST_HIP(ctx, multi_pairing_prepared(arA, sA, P.u(), H0, L0, 2, s, (Fq12*)gts.p, true, s, 0));
+      }
     } else {  // round r-1's look-ahead products, combined with c_{r-1}
       TPST_HIP(ctx, hipStreamWaitEvent(sA, ev_la(r - 1), 0));
       TPST_HIP(ctx, mipp_combine_tab(sA, (Fq12*)SqT[(r - 1) & 1].p, ddig, (Fq12*)SqG[(r - 1) & 1].p,
@@ -1429,48 +1659,87 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
       hipStream_t sD = sLA[r & 1];
       Arena& arD = *arLA[r & 1];
       TPST_HIP(ctx, hipStreamWaitEvent(sD, ev_up(r), 0));
+      if (ev_t1) TPST_HIP(ctx, hipStreamWaitEvent(sD, ev_t1, 0));
+      const size_t ln = loc ? len / W : len;  // positions this rank pairs
       arD.reset();
-      TPST_HIP(ctx, arD.reserve(mipp_lookahead_scratch(len / 4, E) + 4096));
+      TPST_HIP(ctx, arD.reserve(mipp_lookahead_scratch(ln / 4, E) + 4096));
+      Slot sl{};
+      Fq12* la_out = (Fq12*)LAo[r & 1].p;
+      if (loc) {
+        sl = slot(8 * sizeof(Fq12));
+        la_out = (Fq12*)sl.send;
+      }
       if (r == 0) {  // a^(0) = comm_list (affine), h^(0) prepared
-        TPST_HIP(ctx, mipp_lookahead(arD, sD, L0, C, H0, A.u(), false, len, 1, (Fq12*)LAo[0].p));
+        if (loc)
+          TPST_HIP(ctx, mipp_lookahead(arD, sD, L0l, Cl, H0l, A.u(), false, ln, 1, la_out, false));
+        else
+          TPST_HIP(ctx, mipp_lookahead(arD, sD, L0, C, H0, A.u(), false, len, 1, la_out));
       } else {
         // E fold sets f_j a^(r): h^(r)_q = sum_j f_j h^(s)[q + j len]
         TPST_HIP(ctx, hipStreamWaitEvent(sD, ev[EV_TABLE], 0));
         uint32_t* sc = ScD[r & 1].u();
-        TPST_HIP(ctx, mipp_scalar_sets(sD, dW, dfs, E, len, C, sc));
         FbGroups g;
-        g.groups = len;
-        g.members = C / len;
-        g.L = len;
+        g.groups = ln;
+        g.L = ln;
         g.D = 1;
         g.sets = (size_t)E;
-        g.set_stride = C;
         g.glv = true;
+        if (loc) {
+          TPST_HIP(ctx, mipp_scalar_sets(sD, dW, dfs, E, len, Cl, sc, W, rho));
+          g.members = C / len;
+          g.set_stride = Cl;
+        } else {
+          TPST_HIP(ctx, mipp_scalar_sets(sD, dW, dfs, E, len, Ca, sc));
+          g.members = Ca / len;
+          g.set_stride = Ca;
+        }
         TPST_HIP(ctx, fbt_msm<Fq>(arD, sD, tA, sc, g, (Xyzz<Fq>*)xl[r & 1].p));
         const int src = la_src(r);  // h^(0), or h^(src) prepared by stream C in round src
-        const uint32_t* hp = H0;
-        const LineCoeff* lp = L0;
+        const uint32_t* hp = loc ? H0l : H0;
+        const LineCoeff* lp = loc ? L0l : L0;
         if (src > 0) {
-          TPST_HIP(ctx, hipStreamWaitEvent(sD, ev_c(src), 0));
-          hp = Hb[(src >> 1) & 1].u();
-          lp = (const LineCoeff*)Lb[(src >> 1) & 1].p;
+          TPST_HIP(ctx, hipStreamWaitEvent(sD, loc ? ev_cl(src) : ev_c(src), 0));
+          hp = (loc ? Hbl : Hb)[(src >> 1) & 1].u();
+          lp = (const LineCoeff*)(loc ? Lbl : Lb)[(src >> 1) & 1].p;
         }
-        TPST_HIP(ctx, mipp_lookahead(arD, sD, lp, (size_t)E * len, hp, xl[r & 1].u(), true, len, E,
-                                     (Fq12*)LAo[r & 1].p));
+        TPST_HIP(ctx, mipp_lookahead(arD, sD, lp, (size_t)E * ln, hp, xl[r & 1].u(), true, ln, E, la_out, !loc));
+      }
+      if (loc) {
+        if (int rc = gather(sD, sl, 8 * sizeof(Fq12))) return rc;
+        TPST_HIP(ctx, gt_prod_final(sD, (const Fq12*)sl.recv, W, 8, (Fq12*)LAo[r & 1].p));
       }
       TPST_HIP(ctx, mipp_sq_tables(sD, (Fq12*)LAo[r & 1].p, (Fq12*)SqT[r & 1].p, (Fq12*)SqG[r & 1].p));
       TPST_HIP(ctx, hipEventRecord(ev_la(r), sD));
     }
 
     const double hd = open_trace() ? host_us() : 0.0;
-    if (r == 0)
+    if (r == 0 && lead)
       if (int rc = pst_q()) return rc;
 
     const double hp = open_trace() ? host_us() : 0.0;
-    // -- C: h^(r) prepared at odd r for the look-aheads of rounds r+2, r+3
-    if ((r & 1) && r + 4 <= m) {
+    // -- C: h^(r) prepared at odd r for the look-aheads of rounds r+2, r+3:
+    // at this rank's positions (sharded look-aheads) and / or at all
+    const bool c_glob = shd ? (bool)need_glob[r] : ((r & 1) && r + 4 <= m);
+    if (need_loc[r] || c_glob) {
       TPST_HIP(ctx, hipStreamWaitEvent(sC, ev_up(r), 0));
       if (r >= 5) TPST_HIP(ctx, hipStreamWaitEvent(sC, ev_la(r - 1), 0));  // last reader of h^(r-4)'s slot
+    }
+    if (need_loc[r]) {
+      const size_t ln = len / W;
+      TPST_HIP(ctx, mipp_scalars(sC, dWi, nullptr, len, 0, Cl, ScC.u(), W, rho));
+      FbGroups g;
+      g.groups = ln;
+      g.members = C / len;
+      g.L = ln;
+      g.D = 1;
+      TPST_HIP(ctx, fbt_msm<Fq2>(arC, sC, tHl, ScC.u(), g, (Xyzz<Fq2>*)xh.p));
+      TPST_HIP(ctx, xyzz_to_affine_mont<Fq2>(sC, (Xyzz<Fq2>*)xh.p, Hbl[(r >> 1) & 1].u(), ln));
+      TPST_HIP(ctx, g2_prepare_batch(sC, Hbl[(r >> 1) & 1].u(), ln, (LineCoeff*)Lbl[(r >> 1) & 1].p,
+                                     st->prep_scratch.u()));
+      TPST_HIP(ctx, hipEventRecord(ev_cl(r), sC));
+      last_c = r;
+    }
+    if (c_glob) {
       TPST_HIP(ctx, mipp_scalars(sC, dWi, nullptr, len, 0, C, ScC.u()));
       FbGroups g;
       g.groups = len;
@@ -1488,8 +1757,8 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     // -- host: transcript (mipp.rs:56, 97-101) and the challenge
     if (!have_U) {
       TPST_HIP(ctx, hipEventSynchronize(ev[EV_U]));
-      if (p->has_u)
-        memcpy(proof->U, p->U, 96);
+      if (U_given)
+        memcpy(proof->U, U_given, 96);
       else
         xyzz_to_canonical_host<Fq>(pin + dn_U, 1, proof->U);
       uint8_t b[96];
@@ -1524,10 +1793,10 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     const Fr c = fr_inv(c_inv);  // mipp.rs:106
     if (open_trace())
       fprintf(stderr,
-              "open round %d: enqueue %.0f (B %.0f A %.0f D %.0f pst %.0f C %.0f) wait_u %.0f absorb_u %.0f wait_t %.0f "
+              "open round %d%s: enqueue %.0f (B %.0f A %.0f D %.0f pst %.0f C %.0f) wait_u %.0f absorb_u %.0f wait_t %.0f "
               "absorb_t %.0f challenge %.0f inv %.0f us\n",
-              r, h0 - hq, hb - hq, ha - hb, hd - ha, hp - hd, h0 - hp, h1 - h0, h2 - h1, h3 - h2, h4 - h3, h5 - h4,
-              host_us() - h5);
+              r, loc ? " (sharded)" : "", h0 - hq, hb - hq, ha - hb, hd - ha, hp - hd, h0 - hp, h1 - h0, h2 - h1,
+              h3 - h2, h4 - h3, h5 - h4, host_us() - h5);
     xs_inv.push_back(c_inv);
     cprev = c_inv;
     cprev_c = c;
@@ -1543,8 +1812,8 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   }
   if (!have_U) {
     TPST_HIP(ctx, hipEventSynchronize(ev[EV_U]));
-    if (p->has_u)
-      memcpy(proof->U, p->U, 96);
+    if (U_given)
+      memcpy(proof->U, U_given, 96);
     else
       xyzz_to_canonical_host<Fq>(pin + dn_U, 1, proof->U);
     uint8_t b[96];
@@ -1574,16 +1843,18 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
   const uint32_t* dWim = Wiall.u() + 8 * (C - 1);
   TPST_HIP(ctx, hipEventRecord(ev[EV_FINAL_UP], sA));
   TPST_HIP(ctx, hipStreamWaitEvent(sA, ev[EV_TABLE], 0));
-  {  // final_a = a^(m)_0 (one group over all C bases)
+  if (ev_t1) TPST_HIP(ctx, hipStreamWaitEvent(sA, ev_t1, 0));
+  {  // final_a = a^(m)_0 (one group over the a-side bases: all C, or the gathered a^(r1))
     FbGroups g;
-    g.members = C;
-    TPST_HIP(ctx, mipp_scalars(sA, dWm, nullptr, 1, 0, C, ScA.u()));
+    g.members = Ca;
+    TPST_HIP(ctx, mipp_scalars(sA, dWm, nullptr, 1, 0, Ca, ScA.u()));
     g.glv = true;
     TPST_HIP(ctx, fbt_msm<Fq>(arA, sA, tA, ScA.u(), g, (Xyzz<Fq>*)xa.p));
     TPST_HIP(ctx, hipMemcpyAsync(pin + dn_final, xa.p, X1, hipMemcpyDeviceToHost, sA));
   }
   TPST_HIP(ctx, hipStreamWaitEvent(sCe, ev[EV_FINAL_UP], 0));
   if (last_c >= 0) TPST_HIP(ctx, hipStreamWaitEvent(sCe, ev_c(last_c), 0));  // xh / ScC / arC reuse
+  if (last_c >= 0 && need_loc[last_c]) TPST_HIP(ctx, hipStreamWaitEvent(sCe, ev_cl(last_c), 0));
   {  // final_h = h^(m)_0
     FbGroups g;
     g.members = C;
@@ -1609,12 +1880,52 @@ extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, 
     pf.end(ST_SQRT_OPEN, sA);
   }
   for (hipStream_t s2 : {sA, sB, sLA[0], sLA[1]}) TPST_HIP(ctx, hipStreamSynchronize(s2));
+  if (shd) TPST_HIP(ctx, hipStreamSynchronize(ctx->comm));
   xyzz_to_canonical_host<Fq>(pin + dn_final, 1, proof->final_a);
   xyzz_to_canonical_host<Fq2>(pin + dn_fh, 1, proof->final_h);
   if (m > 0) memcpy(proof->pst_proof_h, pin + dn_ph, (size_t)m * 96);
   memcpy(proof->pst_proof, pin + dn_pst, (size_t)k * 192);
   sp.store(tr);
   return TPST_OK;
+}
+
+extern "C" int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, const uint64_t* comms,
+                              const uint64_t* point, const uint64_t* T, tpst_open_proof* proof) {
+  (void)T;  // the reference passes T but the prover does not use it (mipp.rs:38)
+  if (!ctx || !p || !tr || !comms || !point || !proof) return fail(ctx, TPST_E_ARG, "null argument");
+  return poly_open(ctx, p, tr, p->n, comms, point, proof, nullptr);
+}
+
+extern "C" int tpst_poly_open_sharded(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, const uint64_t* comms,
+                                      const uint64_t* point, const uint64_t* U, const tpst_exchange* x,
+                                      tpst_open_proof* proof) {
+  if (!ctx || !tr || !comms || !point || !U || !x) return fail(ctx, TPST_E_ARG, "null argument");
+  if (x->world < 1 || (x->world & (x->world - 1)) || x->rank < 0 || x->rank >= x->world)
+    return fail(ctx, TPST_E_ARG, "world must be a power of two and 0 <= rank < world");
+  if (x->rank == 0 && (!p || !proof)) return fail(ctx, TPST_E_ARG, "rank 0 needs the opening handle and the proof");
+  if (p && p->n != n) return fail(ctx, TPST_E_ARG, "handle num_vars != n");
+  if (!point_valid<Fq>(U)) return fail(ctx, TPST_E_ARG, "c_u is not a valid G1 point");
+  for (int i = 0; i < n; i++)
+    if (!fr_ok(point + 4 * i)) return fail(ctx, TPST_E_ARG, "point coordinate >= r");
+  const int m = n / 2;
+  if (shard_rounds(m, x->world) == 0) {  // too few rows to split: rank 0 opens alone
+    if (x->rank != 0) return TPST_OK;
+    const bool had = p->has_u;
+    uint64_t keep[12];
+    memcpy(keep, p->U, 96);
+    memcpy(p->U, U, 96);
+    p->has_u = true;
+    const int rc = poly_open(ctx, p, tr, n, comms, point, proof, nullptr);
+    memcpy(p->U, keep, 96);
+    p->has_u = had;
+    return rc;
+  }
+  Shard sh;
+  sh.W = x->world;
+  sh.rank = x->rank;
+  sh.x = x;
+  sh.U = U;
+  return poly_open(ctx, p, tr, n, comms, point, proof, &sh);
 }
 
 // -------------------------------------------------------------- verify ---

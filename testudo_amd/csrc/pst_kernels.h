@@ -38,12 +38,16 @@ hipError_t compress_points(hipStream_t s, uint32_t* d_v, size_t split, const uin
 hipError_t compress_fr(hipStream_t s, uint32_t* d_y, size_t split, const uint32_t* d_kmont);
 
 // MIPP scalars over the original bases (Montgomery W, y; canonical out):
-// y == nullptr: out[k] = W[k / len]; else out[k] = W[k / len] * y[(k % len + split) % len]
+// y == nullptr: out[k] = W[k / len]; else out[k] = W[k / len] * y[(k % len + split) % len].
+// sub / off: n scalars of the bases k = sub kl + off only (out[kl]; a rank's
+// rows of the row-sharded opening)
 hipError_t mipp_scalars(hipStream_t s, const uint32_t* d_W, const uint32_t* d_y, size_t len, size_t split, size_t n,
-                        uint32_t* d_out);
-// E fold sets: out[j n + k] = canonical(W[k / len] * f[j]) (Montgomery W, f)
+                        uint32_t* d_out, size_t sub = 1, size_t off = 0);
+// E fold sets: out[j n + kl] = canonical(W[k / len] * f[j]), k = sub kl + off (Montgomery W, f)
 hipError_t mipp_scalar_sets(hipStream_t s, const uint32_t* d_W, const uint32_t* d_f, int E, size_t len, size_t n,
-                            uint32_t* d_out);
+                            uint32_t* d_out, size_t sub = 1, size_t off = 0);
+// out[g] = sum_{w < W} parts[w G + g]: gathered per-rank XYZZ partials -> sums
+hipError_t xyzz_sum_groups(hipStream_t s, const Xyzz<Fq>* d_parts, size_t W, size_t G, Xyzz<Fq>* d_out);
 // round r's fold weights W_r / Wi_r (2^r Montgomery Fr at offset 2^r - 1) from
 // round r-1's and its challenge c (and c^-1), both Montgomery Fr on the device
 hipError_t mipp_weights(hipStream_t s, uint32_t* d_W, uint32_t* d_Wi, int r, const uint32_t* d_c,

@@ -19,9 +19,18 @@ Opening exchange (C3): get_q's mat-vec z_q[j] = sum_i Z_i[j] chi_i(b)
 (sqrt_pst.rs:92-95) and c_u = sum_i chi_i(b) C_i (sqrt_pst.rs:198) are sums
 over rows, so each rank computes its rows' share of both; one all-gather of
 [z_q share (2^m_row Fr) | c_u share (G1)] and a mod-r / G1 sum on rank 0 give
-q and U, and rank 0 opens from q alone (no rank holds the whole Z).  The MIPP
-rounds, the PST proof of q and the final folds are transcript-sequential and
-KB-sized: they stay on rank 0.
+q and U, and rank 0 opens from q alone (no rank holds the whole Z).
+
+Sharded opening (C4): the MIPP rounds (mipp.rs:58-120) run on every rank
+over its rows i = rank mod W (tpst_poly_open_sharded): each round's cross
+MSMs, folds, h preparations and look-ahead pairings on the rank's own rows,
+one all-gather per product (cross partials as XYZZ, Miller partials before
+the final exponentiation), every rank replaying the transcript; once a round
+is shorter than 4W the folded vector moves to rank 0, which finishes the
+rounds, the PST proof of q and the final folds.  The library calls back into
+TorchExchange for each all-gather: an RCCL all_gather_into_tensor enqueued on
+the library's comm stream (no host synchronisation), or, over gloo, a host
+round trip.
 
 Split MSM (strong scaling): one variable-base MSM (sqrt_pst.rs:198,
 mipp.rs:393) over n points is cut into equal contiguous point ranges; each
@@ -70,8 +79,8 @@ def sharded_commit(n: int, commit_rows_partial_into: Callable, finalize: Callabl
     finalize(gathered) -> T (72,) uint64 runs on rank 0 over the gathered
     (world, R * 12 + 72) device tensor.
 
-    Returns (comm_list (2^m_col, 12) uint64 on rank 0 else None, T (72,) on
-    every rank, this rank's own row commitments (R, 12))."""
+    Returns (comm_list (2^m_col, 12) uint64 on every rank, T (72,) on every
+    rank, this rank's own row commitments (R, 12))."""
     import torch
     dev = _device(dist, device)
     world, rank = dist.get_world_size(), dist.get_rank()
@@ -82,9 +91,9 @@ def sharded_commit(n: int, commit_rows_partial_into: Callable, finalize: Callabl
     got = _all_gather(dist, buf)  # C1 + C2: bytes only
     own = buf[:12 * R].cpu().numpy().view(np.uint64).reshape(R, 12).copy()
     T = torch.zeros(72, dtype=torch.int64, device=dev)
-    comm_list = None
+    # every rank holds the gathered list (the sharded opening reads all of it)
+    comm_list = got[:, :12 * R].cpu().numpy().view(np.uint64).reshape(-1, 12).copy()
     if rank == 0:
-        comm_list = got[:, :12 * R].cpu().numpy().view(np.uint64).reshape(-1, 12).copy()
         T.copy_(torch.from_numpy(np.ascontiguousarray(finalize(got), dtype=np.uint64).view(np.int64)))
     dist.broadcast(T, src=0)
     return comm_list, T.cpu().numpy().view(np.uint64).copy(), own
@@ -99,8 +108,8 @@ def sharded_open_inputs(n: int, q_partial_into: Callable, cu_partial: Callable, 
     words) with the share of z_q (canonical Fr); cu_partial(r0, r1) -> (12,)
     uint64 canonical affine share of c_u; combine_q(gathered (world, N * 4)
     tensor) -> z_q as an int64 tensor on the rank's device; combine_cu(shares
-    (world, 12) uint64) -> U (12,).  Returns (z_q, U) on rank 0, (None, None)
-    elsewhere."""
+    (world, 12) uint64) -> U (12,).  Returns (z_q, U) on rank 0, (None, U)
+    elsewhere (every rank combines U: the sharded opening absorbs it)."""
     import torch
     dev = _device(dist, device)
     world, rank = dist.get_world_size(), dist.get_rank()
@@ -111,11 +120,12 @@ def sharded_open_inputs(n: int, q_partial_into: Callable, cu_partial: Callable, 
     cu = np.ascontiguousarray(cu_partial(r0, r1), dtype=np.uint64).reshape(12)
     buf[N * 4:].copy_(torch.from_numpy(cu.view(np.int64)))
     got = _all_gather(dist, buf)
+    U = np.ascontiguousarray(combine_cu(got[:, N * 4:].cpu().numpy().view(np.uint64).copy()),
+                             dtype=np.uint64).reshape(12)
     if rank != 0:
-        return None, None
+        return None, U
     zq = combine_q(got[:, :N * 4].contiguous())
-    U = combine_cu(got[:, N * 4:].cpu().numpy().view(np.uint64).copy())
-    return zq, np.ascontiguousarray(U, dtype=np.uint64).reshape(12)
+    return zq, U
 
 
 def sharded_msm(n: int, msm_partial_into: Callable, combine: Callable, dist, device):
@@ -132,3 +142,68 @@ def sharded_msm(n: int, msm_partial_into: Callable, combine: Callable, dist, dev
     msm_partial_into(i0, i1, buf)
     got = _all_gather(dist, buf)
     return combine(got) if dist.get_rank() == 0 else None
+
+
+class TorchExchange:
+    """tpst_exchange over torch.distributed for tpst_poly_open_sharded.
+
+    The arena (sized by tpst_open_sharded_arena_bytes) is a torch allocation
+    on the rank's GPU; the library writes its send slots there and calls
+    back for each all-gather with byte offsets and its comm stream.  "nccl"
+    (RCCL): all_gather_into_tensor on uint8 views of the arena, issued with
+    the library's stream as the current stream -- stream-ordered, no host
+    synchronisation.  "gloo" (tests, shared-GPU rehearsals): the stream is
+    synchronised, the slot goes through host memory."""
+
+    def __init__(self, ctx, dist, device, n: int):
+        import torch
+        from . import _lib
+        self.dist = dist
+        self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        self.device = torch.device(device)
+        nbytes = int(ctx.lib.tpst_open_sharded_arena_bytes(n, self.world))
+        self.arena = torch.zeros(max(nbytes, 256), dtype=torch.uint8, device=self.device)
+        self.nccl = dist.get_backend() == "nccl"
+        self.calls = 0
+        self.error = None
+        self._cb = _lib.ALLGATHER_FN(self._gather)
+        self.struct = _lib.Exchange(self.world, self.rank, self._cb, None, self.arena.data_ptr(), nbytes)
+
+    def _gather(self, user, send_off, recv_off, nbytes, stream):
+        import torch
+        try:
+            self.calls += 1
+            send = self.arena[send_off:send_off + nbytes]
+            recv = self.arena[recv_off:recv_off + self.world * nbytes]
+            s = torch.cuda.ExternalStream(stream, device=self.device)
+            if self.nccl:
+                with torch.cuda.stream(s):
+                    self.dist.all_gather_into_tensor(recv, send)
+            else:
+                s.synchronize()
+                h = send.cpu()
+                parts = [torch.empty_like(h) for _ in range(self.world)]
+                self.dist.all_gather(parts, h)
+                with torch.cuda.stream(s):
+                    recv.copy_(torch.cat(parts))
+                s.synchronize()
+            return 0
+        except Exception as e:  # reported by the library as TPST_E_STATE
+            self.error = e
+            return 1
+
+
+def sharded_open(ctx, n: int, handle, comm_list, point, U, transcript, dist, device):
+    """C4: the MIPP rounds of Polynomial::open split over the ranks
+    (tpst_poly_open_sharded).  Every rank passes the whole comm_list (as
+    returned by sharded_commit), the point, U (sharded_open_inputs) and a
+    fresh transcript; rank 0 passes its opening handle (from_q) and gets
+    (U, pst_proof, MippProof), the others pass None and get None."""
+    from . import sqrt_pst as S
+    x = TorchExchange(ctx, dist, device, n)
+    try:
+        return S.open_sharded(ctx, handle if dist.get_rank() == 0 else None, transcript, n, comm_list, point, U, x)
+    except Exception:
+        if x.error is not None:
+            raise RuntimeError("exchange all-gather failed: %r" % (x.error,)) from x.error
+        raise

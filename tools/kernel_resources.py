@@ -75,7 +75,7 @@ def report(src: str) -> list:
             cur[FIELDS[m.group(1).strip()]] = int(v) if v.lstrip("-").isdigit() else v
     for row, d in zip(rows, _demangle([x["mangled"] for x in rows])):
         d = d[5:] if d.startswith("void ") else d
-        row["name"] = d.replace("tpst::", "")
+        row["name"] = d.replace("tpst::", "").replace("(anonymous namespace)::", "")
     return rows
 
 
