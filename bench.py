@@ -544,13 +544,17 @@ def sharded_leg(ctx, log_n, dist, dev, reps=5):
     rank 0, read from the gathered buffer); then each rank computes its rows'
     share of get_q's z_q and of c_u (one all-gather, summed on rank 0 -- the
     q / eval step that benches/pst.rs runs before the open timer), and rank 0
-    opens from q alone (transcript-sequential MIPP + PST open, SURVEY.md
+    opens from q with the MIPP rounds split over the ranks while a round has
+    >= 4 rows per rank (tpst_poly_open_sharded: every rank folds, pairs and
+    cross-multiplies its own rows, one all-gather per product; rank 0 alone
+    for the last rounds, the PST proof of q and the final folds; SURVEY.md
     §8(e)).  No rank holds the whole Z.  N = 1: the plain commit + open.
-    Timing as BASELINE.md:43-45: the median of `reps` warm runs (commit: max
-    over ranks), plus the H2D upload of Z; then one profiled run for the
-    device spans and K1's roofline (the dominant kernel of the commit)."""
+    Timing as BASELINE.md:43-45: the median of `reps` warm runs (commit and
+    open: max over ranks), plus the H2D upload of Z; then one profiled run for
+    the device spans and K1's roofline (the dominant kernel of the commit)."""
     from testudo_amd import sqrt_pst as S
-    from testudo_amd.distributed import shard_rows, sharded_commit, sharded_open_inputs
+    from testudo_amd.distributed import (TorchExchange, shard_rows, sharded_commit, sharded_open, sharded_open_inputs,
+                                         sharded_rounds)
     nv = (log_n + 1) // 2
     t = time.perf_counter()
     S.srs_setup(ctx, nv, SEED + 1)
@@ -570,6 +574,7 @@ def sharded_leg(ctx, log_n, dist, dev, reps=5):
     ctx.synchronize()
     h2d_s = _max_over_ranks(dist, dev, time.perf_counter() - t)
     del Z
+    xch = TorchExchange(ctx, dist, dev, log_n) if dist else None
     commits, qs, opens = [], [], []
     k1 = {}
     spans = {}
@@ -612,18 +617,25 @@ def sharded_leg(ctx, log_n, dist, dev, reps=5):
         q_el = _max_over_ranks(dist, dev, time.perf_counter() - t)
         if not prof:
             qs.append(q_el)
-        if rank == 0:
-            if prof:
-                ctx.profile_reset()
-                ctx.profile(True)
-            t = time.perf_counter()
+        if dist:  # the MIPP rounds on every rank's rows (C4), then rank 0 alone
+            dist.barrier()
+        if prof and rank == 0:
+            ctx.profile_reset()
+            ctx.profile(True)
+        t = time.perf_counter()
+        if dist:
+            out = sharded_open(ctx, log_n, pl, comms, pt, U, S.PoseidonTranscript(), dist, dev, exchange=xch)
+            if rank == 0:
+                U, pst_proof, mipp = out
+        else:
             U, pst_proof, mipp = pl.open(S.PoseidonTranscript(), comms, pt, T)
-            o_el = time.perf_counter() - t
-            if prof:
+        o_el = _max_over_ranks(dist, dev, time.perf_counter() - t)
+        if prof:
+            if rank == 0:
                 ctx.profile(False)
                 spans = _stage_ms(ctx)
-            else:
-                opens.append(o_el)
+        else:
+            opens.append(o_el)
     if dist:
         dist.barrier()
     if rank != 0:
@@ -647,8 +659,11 @@ def sharded_leg(ctx, log_n, dist, dev, reps=5):
            "ranks": world, "rows_per_rank": r1 - r0, "verified": ok, "srs_setup_s": round(setup_s, 3),
            "exchange": ("per-rank column-block upload; %s all_gather of [96-B row commitments | 576-B Miller "
                         "partial] device buffers, FE on rank 0; %s all_gather of [z_q share | c_u share], mod-r / "
-                        "G1 sum on rank 0, open from q on rank 0"
-                        % ((("RCCL" if dist.get_backend() == "nccl" else "gloo"),) * 2)) if dist else "none"}
+                        "G1 sum; sharded MIPP open: %d all_gathers (cross XYZZ partials, Miller partials) on the "
+                        "library's comm stream, the last %d rounds on rank 0"
+                        % ((("RCCL" if dist.get_backend() == "nccl" else "gloo"),) * 2
+                           + (xch.calls // (reps + 2), log_n // 2 - sharded_rounds(log_n, world))))
+                        if dist else "none"}
     if "bucket_acc" in k1:  # K1 (k_bucket_acc_chunk + fixup) over this rank's rows
         rows = r1 - r0
         npts = 1 << (log_n - log_n // 2)

@@ -73,7 +73,13 @@ def _worker(rank, world, port, n, q):
         del shard
         handle = S.Polynomial.from_q(ctx, n, pt, zq, U) if rank == 0 else None
         v = handle.eval(pt) if rank == 0 else None
-        out = sharded_open(ctx, n, handle, comms, pt, U, S.PoseidonTranscript(), dist, dev)
+        from testudo_amd.distributed import TorchExchange, sharded_rounds
+        x = TorchExchange(ctx, dist, dev, n)
+        out = sharded_open(ctx, n, handle, comms, pt, U, S.PoseidonTranscript(), dist, dev, exchange=x)
+        # every sharded round: the cross partials and the look-ahead partials;
+        # round 0's direct t_l / t_r; the hand-over of the folded vector
+        rs = sharded_rounds(n, world)
+        assert rs >= 1 and x.calls == 2 * rs + 2, (rs, x.calls)
         if rank != 0:
             assert out is None
             q.put((rank, None))

@@ -193,14 +193,24 @@ class TorchExchange:
             return 1
 
 
-def sharded_open(ctx, n: int, handle, comm_list, point, U, transcript, dist, device):
+def sharded_rounds(n: int, world: int) -> int:
+    """The MIPP rounds tpst_poly_open_sharded splits across `world` ranks
+    (length >= 4 world); rank 0 runs the remaining n // 2 - this alone."""
+    r, C = 0, 1 << (n // 2)
+    while r < n // 2 and (C >> r) >= 4 * world:
+        r += 1
+    return r
+
+
+def sharded_open(ctx, n: int, handle, comm_list, point, U, transcript, dist, device, exchange=None):
     """C4: the MIPP rounds of Polynomial::open split over the ranks
     (tpst_poly_open_sharded).  Every rank passes the whole comm_list (as
     returned by sharded_commit), the point, U (sharded_open_inputs) and a
     fresh transcript; rank 0 passes its opening handle (from_q) and gets
-    (U, pst_proof, MippProof), the others pass None and get None."""
+    (U, pst_proof, MippProof), the others pass None and get None.
+    `exchange` (a TorchExchange for this n) may be reused across calls."""
     from . import sqrt_pst as S
-    x = TorchExchange(ctx, dist, device, n)
+    x = exchange if exchange is not None else TorchExchange(ctx, dist, device, n)
     try:
         return S.open_sharded(ctx, handle if dist.get_rank() == 0 else None, transcript, n, comm_list, point, U, x)
     except Exception:
