@@ -440,7 +440,13 @@ def pst_leg(ctx, log_n, reps=5):
     ok = S.verify(ctx, S.PoseidonTranscript(), U, pt, v, pst_proof, mipp, T)
     verify_s = time.perf_counter() - t
     sizes = _wire_sizes(ctx, nv, pst_proof, mipp)
+    env_tab = os.environ.get("TPST_COMMIT_TABLE")
+    in_commit = (env_tab != "0") if env_tab is not None else (1 << (log_n // 2)) <= 2048
     return {"log_n": log_n, "commit_s": round(c, 4), "open_s": round(o, 4), **sizes,
+            "fold_table_in_commit": in_commit,
+            "fold_table_note": ("the opening's GLV fold table over comm_list is built by the commit (beside its "
+                                "IPP): open_s excludes it, commit_plus_open_s is the comparable total"
+                                if in_commit else "the opening builds its fold table (inside open_s)"),
             "commit_plus_open_s": round(co, 4), "reps": reps, "timing": "median of the warm reps",
             "h2d_s": round(h, 4), "commit_open_incl_h2d_s": round(co + h, 4),
             "device_commit_s": round(spans.get("sqrt_commit", 0.0) * 1e-3, 5),
