@@ -1,6 +1,6 @@
 """Median sqrt-PST commit time at 2^n under environment variants, one child
 process per variant (the tunables are read once per process):
-    python tools/commit_sweep.py 20 'TPST_ACC_WAVES=4' 'TPST_K1_RED=2' ..."""
+    python tools/commit_sweep.py 20 'TPST_COMMIT_TABLE=0' 'TPST_LIB_PATH=/path/to/other/libtpst.so' ..."""
 import os
 import subprocess
 import sys

@@ -1,6 +1,6 @@
 """Median sqrt-PST open time at 2^n under environment variants, one child
 process per variant (the tunables are read once per process):
-    python tools/open_sweep.py 20 'TPST_OPEN_PRIO=6' ..."""
+    python tools/open_sweep.py 20 'TPST_COMMIT_TABLE=0' 'TPST_LIB_PATH=/path/to/other/libtpst.so' ..."""
 import os
 import subprocess
 import sys
