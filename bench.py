@@ -56,8 +56,8 @@ BYTES_PER_PAIR = 128           # 32 B scalar + 96 B affine base
 LIMB_PRODUCTS_PER_FQ_MUL = 325
 MB_FQMUL_KIND = 12  # tpst_microbench kind of that product (kind 0: field.h's 12 x 32-bit product)
 SEED = 0x7E57D0
-PMC_FILE = os.path.join(ROOT, "profiles", "r04", "pmc_bucket_acc_short.json")
-PMC_FILE_K1 = os.path.join(ROOT, "profiles", "r04", "pmc_bucket_acc_chunk_2p24.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r05", "a", "pmc_bucket_acc_short.json")
+PMC_FILE_K1 = os.path.join(ROOT, "profiles", "r05", "a", "pmc_bucket_acc_chunk_2p24.json")
 if not os.path.exists(PMC_FILE):  # the latest round that has one
     PMC_FILE = os.path.join(ROOT, "profiles", "r03", "pmc_bucket_acc_short.json")
 
@@ -250,6 +250,17 @@ def main():
     ctx.profile(False)
     stages = ctx.profile_read()
     elapsed = _max_over_ranks(dist, dev, t1 - t0)
+    # one MSM alone (synchronised after each call): the latency; the timed
+    # loop above overlaps call i's latency-bound tail with call i+1
+    # (tpst_g1_msm_dev pipelining)
+    lat = []
+    for _ in range(5):
+        ctx.synchronize()
+        ta = time.perf_counter()
+        step()
+        ctx.synchronize()
+        lat.append(time.perf_counter() - ta)
+    latency_ms = sorted(lat)[len(lat) // 2] * 1e3
 
     # correctness spot check of this rank's result against the size-independent
     # property MSM(b_i G) = (sum s_i b_i) G, verified with the library's
@@ -350,6 +361,11 @@ def main():
                    "n_points": n, "curve": "BLS12-377 G1", "window_bits": c_bits,
                    "parallelism": "independent MSM per rank" if world > 1 else "1 GPU"},
         "parity_ok": parity_ok,
+        "latency_ms_single_call": round(latency_ms, 4),
+        "pipelining": ("consecutive tpst_g1_msm_dev calls overlap: call i's last-window-group tail (fixup, bucket "
+                       "reduction, window chain, affine output) runs on a tail stream while call i+1 sorts and "
+                       "accumulates with the other of two arenas; ms_per_step is the steady state, "
+                       "latency_ms_single_call one call synchronised alone"),
         "stages_ms_per_step": {k: round(v[0] / max(v[1], 1), 4) for k, v in stages.items() if v[1]},
         "roofline": {"bound": "valu-int32", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,

@@ -17,8 +17,12 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
-BUILD = os.path.join(HERE, "build")
-LIB = os.path.join(HERE, "libtpst.so")
+# A/B builds (experiments): TPST_BUILD_TAG=x builds build_x/ -> libtpst_x.so
+# with TPST_EXTRA_FLAGS added (e.g. "-DTPST_F29_2ACC=0"); load it with
+# TPST_LIB_PATH.  The product build is the untagged one.
+_TAG = os.environ.get("TPST_BUILD_TAG", "")
+BUILD = os.path.join(HERE, "build_" + _TAG if _TAG else "build")
+LIB = os.path.join(HERE, "libtpst_%s.so" % _TAG if _TAG else "libtpst.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("TPST_ARCH", "gfx950")
 
@@ -35,7 +39,7 @@ def _host_isa_flags() -> list:
 
 
 FLAGS = (["-std=c++17", "-O3", "--offload-arch=" + ARCH, "-fPIC", "-Wno-unused-result"] + _host_isa_flags() +
-         ["-I" + CSRC, "-I" + os.path.join(ROOT, "include")])
+         ["-I" + CSRC, "-I" + os.path.join(ROOT, "include")] + os.environ.get("TPST_EXTRA_FLAGS", "").split())
 
 
 def _includes(path: str, seen: set) -> None:

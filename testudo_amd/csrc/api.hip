@@ -40,6 +40,9 @@ extern "C" int tpst_create(int device, tpst_ctx** out) {
   tpst_ctx* c = new tpst_ctx();
   c->device = device;
   c->arena.prof = &c->prof;
+  c->arena_msm[0].prof = c->arena_msm[1].prof = &c->prof;
+  c->arena_msm[1].aux_from = &c->arena_msm[0];  // one pair of aux streams
+  c->mu.stream = &c->stream;
   // the library stream carries every critical path (the opening's transcript
   // chain in particular); the opening's side streams (pst_api.hip) are
   // created at the lowest priority so the dispatcher favours this one
@@ -71,6 +74,15 @@ extern "C" void tpst_destroy(tpst_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->comm);
     (void)hipStreamDestroy(ctx->comm);
   }
+  if (ctx->msm_tail) {
+    (void)hipStreamSynchronize(ctx->msm_tail);
+    (void)hipStreamDestroy(ctx->msm_tail);
+  }
+  for (int i = 0; i < 2; i++) {
+    if (ctx->msm_done[i]) (void)hipEventDestroy(ctx->msm_done[i]);
+    if (ctx->msm_out[i]) (void)hipFree(ctx->msm_out[i]);
+    ctx->arena_msm[i].release();
+  }
   for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
   if (ctx->ev_wait) (void)hipEventDestroy(ctx->ev_wait);
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
@@ -101,14 +113,14 @@ static int order_streams(tpst_ctx* ctx, hipStream_t before, hipStream_t after, h
 
 extern "C" int tpst_wait_stream(tpst_ctx* ctx, void* stream) {
   if (!ctx) return TPST_E_ARG;
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   return order_streams(ctx, (hipStream_t)stream, ctx->stream, ctx->ev_wait);
 }
 
 extern "C" int tpst_join_stream(tpst_ctx* ctx, void* stream) {
   if (!ctx) return TPST_E_ARG;
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   return order_streams(ctx, ctx->stream, (hipStream_t)stream, ctx->ev_join);
 }
@@ -118,7 +130,7 @@ template <class F>
 static int msm_host(tpst_ctx* ctx, const uint64_t* bases, size_t nb, const uint64_t* scalars, size_t ns,
                     uint64_t* out) {
   if (!ctx || !out || (nb && !bases) || (ns && !scalars)) return fail(ctx, TPST_E_ARG, "null argument");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   const size_t n = nb < ns ? nb : ns;  // msm_unchecked truncates
   if (n > MSM_MAX_POINTS) return fail(ctx, TPST_E_ARG, "MSM longer than 2^27 points: split it");
@@ -174,7 +186,7 @@ static int msm_fixed_host(tpst_ctx* ctx, const uint64_t* bases, size_t n, const 
                           size_t D, uint64_t* out) {
   if (!ctx || !out || (n && (!bases || !scalars))) return fail(ctx, TPST_E_ARG, "null argument");
   if (!n || !L || !D || n % L || L % D) return fail(ctx, TPST_E_ARG, "bad group shape");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   constexpr size_t PW = 2 * Words<F>::n;
   const size_t G = L / D;
@@ -214,16 +226,44 @@ extern "C" int tpst_g2_msm_fixed(tpst_ctx* ctx, const uint64_t* bases, size_t n,
   return msm_fixed_host<Fq2>(ctx, bases, n, scalars, L, D, out);
 }
 
+// Pipelined: consecutive calls overlap.  Call i's latency-bound tail (the
+// last window group's fixup, bucket reduction and window chain, and the
+// affine output; ~0.7 ms of a few waves at 2^20) runs on ctx->msm_tail, and
+// call i+1 starts its decomposition, sort and accumulation on ctx->stream
+// with the other of two arenas at once.  Stream order is kept for the
+// caller: the next entry point of any other kind (and tpst_synchronize /
+// tpst_join_stream) first waits for the pending tails (CtxMutex::lock), and
+// a call reusing an arena waits for the tail that last used it.
 extern "C" int tpst_g1_msm_dev(tpst_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, void* d_out) {
   if (!ctx || !d_out || (n && (!d_bases || !d_scalars))) return fail(ctx, TPST_E_ARG, "null argument");
   if (n > MSM_MAX_POINTS) return fail(ctx, TPST_E_ARG, "MSM longer than 2^27 points: split it");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  tpst::CtxKeep lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
-  ctx->io.reset();
-  TPST_HIP(ctx, ctx->io.reserve(Arena::need(1, sizeof(Xyzz<Fq>)) + 256));
-  Xyzz<Fq>* d_r = ctx->io.take<Xyzz<Fq>>(1);
-  TPST_HIP(ctx, msm_var<Fq>(ctx->arena, ctx->stream, (const uint32_t*)d_bases, (const uint32_t*)d_scalars, n, d_r));
-  TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(ctx->stream, d_r, (uint32_t*)d_out, 1));
+  if (!ctx->msm_tail) {
+    int least = 0, greatest = 0;
+    TPST_HIP(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
+    TPST_HIP(ctx, hipStreamCreateWithPriority(&ctx->msm_tail, hipStreamNonBlocking, greatest));
+    for (int i = 0; i < 2; i++) {
+      TPST_HIP(ctx, hipEventCreateWithFlags(&ctx->msm_done[i], hipEventDisableTiming));
+      TPST_HIP(ctx, hipMalloc(&ctx->msm_out[i], sizeof(Xyzz<Fq>)));
+    }
+  }
+  const int k = ctx->msm_slot;
+  ctx->msm_slot ^= 1;
+  Arena& ar = ctx->arena_msm[k];
+  // the tail that last used this arena (its buckets, bounds, output slot)
+  if (ctx->msm_done_set[k]) TPST_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->msm_done[k], 0));
+  bool on_tail = false;
+  Xyzz<Fq>* d_r = (Xyzz<Fq>*)ctx->msm_out[k];
+  TPST_HIP(ctx, msm_var<Fq>(ar, ctx->stream, (const uint32_t*)d_bases, (const uint32_t*)d_scalars, n, d_r,
+                            ctx->msm_tail, &on_tail));
+  hipStream_t t = on_tail ? ctx->msm_tail : ctx->stream;
+  TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(t, d_r, (uint32_t*)d_out, 1));
+  TPST_HIP(ctx, hipEventRecord(ctx->msm_done[k], t));
+  ctx->msm_done_set[k] = true;
+  bool listed = false;
+  for (hipEvent_t e : ctx->mu.pending) listed |= e == ctx->msm_done[k];
+  if (!listed) ctx->mu.pending.push_back(ctx->msm_done[k]);
   return TPST_OK;
 }
 
@@ -233,7 +273,7 @@ extern "C" int tpst_g1_msm_xyzz_dev(tpst_ctx* ctx, const void* d_bases, const vo
                                     void* d_out_xyzz) {
   if (!ctx || !d_out_xyzz || (n && (!d_bases || !d_scalars))) return fail(ctx, TPST_E_ARG, "null argument");
   if (n > MSM_MAX_POINTS) return fail(ctx, TPST_E_ARG, "MSM longer than 2^27 points: split it");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   TPST_HIP(ctx, msm_var<Fq>(ctx->arena, ctx->stream, (const uint32_t*)d_bases, (const uint32_t*)d_scalars, n,
                             (Xyzz<Fq>*)d_out_xyzz));
@@ -253,7 +293,7 @@ extern "C" int tpst_g1_xyzz_sum_dev(tpst_ctx* ctx, const void* d_parts, size_t k
   // k_xyzz_sum reads each share with 16-byte vector loads
   if (k && (stride_bytes < sizeof(Xyzz<Fq>) || stride_bytes % 16 || ((uintptr_t)d_parts & 15)))
     return fail(ctx, TPST_E_ARG, "shares must be 16-byte aligned with a 16-byte-multiple stride");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   ctx->io.reset();
   TPST_HIP(ctx, ctx->io.reserve(Arena::need(1, sizeof(Xyzz<Fq>)) + 256));
@@ -268,7 +308,7 @@ extern "C" int tpst_g1_xyzz_sum_dev(tpst_ctx* ctx, const void* d_parts, size_t k
 extern "C" int tpst_multi_pairing(tpst_ctx* ctx, const uint64_t* g1, const uint64_t* g2, size_t n,
                                   uint64_t* out_gt) {
   if (!ctx || !out_gt || (n && (!g1 || !g2))) return fail(ctx, TPST_E_ARG, "null argument");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
   ctx->io.reset();
@@ -319,7 +359,7 @@ __global__ void __launch_bounds__(64, 1) k_mul_gen(const uint32_t* __restrict__ 
 template <class F>
 static int mul_gen_host(tpst_ctx* ctx, const uint64_t* scalars, size_t n, uint64_t* out) {
   if (!ctx || (n && (!scalars || !out))) return fail(ctx, TPST_E_ARG, "null argument");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   if (!n) return TPST_OK;
   constexpr size_t PW = 2 * Words<F>::n;
@@ -346,7 +386,7 @@ extern "C" int tpst_g2_mul_generator(tpst_ctx* ctx, const uint64_t* scalars, siz
 
 extern "C" int tpst_g1_mul_generator_dev(tpst_ctx* ctx, const void* d_scalars, size_t n, void* d_out_mont) {
   if (!ctx || (n && (!d_scalars || !d_out_mont))) return fail(ctx, TPST_E_ARG, "null argument");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   if (!n) return TPST_OK;
   k_mul_gen<Fq><<<grid_for(n, 64), 64, 0, ctx->stream>>>((const uint32_t*)d_scalars, n, (uint32_t*)d_out_mont, 0);
@@ -357,14 +397,14 @@ extern "C" int tpst_g1_mul_generator_dev(tpst_ctx* ctx, const void* d_scalars, s
 // ------------------------------------------------------ stage profiling ----
 extern "C" int tpst_profile_enable(tpst_ctx* ctx, int on) {
   if (!ctx) return TPST_E_ARG;
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   ctx->prof.on = on != 0;
   return TPST_OK;
 }
 
 extern "C" int tpst_profile_reset(tpst_ctx* ctx) {
   if (!ctx) return TPST_E_ARG;
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->prof.collect();
   ctx->prof.reset();
@@ -373,7 +413,7 @@ extern "C" int tpst_profile_reset(tpst_ctx* ctx) {
 
 extern "C" int tpst_profile_read(tpst_ctx* ctx, int stage, double* total_ms, uint64_t* launches) {
   if (!ctx || !total_ms || !launches || stage < 0 || stage >= N_STAGES) return fail(ctx, TPST_E_ARG, "bad stage");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->prof.collect();
   *total_ms = ctx->prof.total_ms[stage];

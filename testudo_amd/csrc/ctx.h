@@ -7,10 +7,46 @@
 #include "msm.h"
 #include "pairing_kernels.h"
 
+namespace tpst {
+// The per-context lock.  lock() also orders the context stream after any
+// work a previous call left running off it (the pipelined device MSM's tail,
+// tpst_g1_msm_dev): every entry point sees the results of every earlier call
+// in stream order, as if it had all run on `stream`.  lock_keep() (the
+// pipelined MSM itself) leaves that work pending.
+struct CtxMutex {
+  std::mutex m;
+  hipStream_t* stream = nullptr;
+  std::vector<hipEvent_t> pending;
+  void lock() {
+    m.lock();
+    if (stream && *stream)
+      for (hipEvent_t e : pending) (void)hipStreamWaitEvent(*stream, e, 0);
+    pending.clear();
+  }
+  void lock_keep() { m.lock(); }
+  void unlock() { m.unlock(); }
+};
+struct CtxKeep {  // lock_guard of lock_keep()
+  CtxMutex& mu;
+  explicit CtxKeep(CtxMutex& m) : mu(m) { mu.lock_keep(); }
+  ~CtxKeep() { mu.unlock(); }
+};
+}  // namespace tpst
+
 struct tpst_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  std::mutex mu;
+  tpst::CtxMutex mu;
+  // pipelined device MSMs (tpst_g1_msm_dev): two arenas used alternately;
+  // call i's latency-bound tail (last window group's fixup, reduction, window
+  // chain, affine output) runs on msm_tail while call i+1 sorts and
+  // accumulates on `stream` with the other arena
+  tpst::Arena arena_msm[2];
+  hipStream_t msm_tail = nullptr;
+  hipEvent_t msm_done[2] = {nullptr, nullptr};
+  void* msm_out[2] = {nullptr, nullptr};  // each slot's XYZZ result
+  bool msm_done_set[2] = {false, false};
+  int msm_slot = 0;
   std::string err;
   tpst::Arena arena;   // kernel scratch (reset per primitive)
   tpst::Arena io;      // staging for host-pointer entry points

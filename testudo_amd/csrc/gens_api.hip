@@ -119,7 +119,7 @@ extern "C" int tpst_gens_load(tpst_ctx* ctx, const uint64_t* G, size_t n, const 
   if (n >= ((size_t)1 << 26)) return fail(ctx, TPST_E_ARG, "too many generators");
   if (!points_canonical(G, 2 * n) || (h && !points_canonical(h, 2)))
     return fail(ctx, TPST_E_ARG, "generator coordinate >= p");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
   auto g = new tpst_gens();
@@ -155,7 +155,7 @@ extern "C" void tpst_gens_free(tpst_gens* g) { delete g; }
 extern "C" int tpst_g1_msm_batch(tpst_ctx* ctx, const tpst_gens* g, const uint64_t* scalars, size_t rows,
                                  size_t cols, size_t row_stride, size_t col_stride, uint64_t* out) {
   if (!ctx || !g || (rows && !out)) return fail(ctx, TPST_E_ARG, "null argument");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   return host_batch(ctx, g, scalars, rows, cols, row_stride, col_stride, nullptr, out);
 }
@@ -165,7 +165,7 @@ extern "C" int tpst_g1_msm_batch_dev(tpst_ctx* ctx, const tpst_gens* g, const vo
   if (!ctx || !g || (rows && (!d_out || (g->n && !d_scalars)))) return fail(ctx, TPST_E_ARG, "null argument");
   if (cols != g->n) return fail(ctx, TPST_E_ARG, "cols != number of generators");
   if (g->n && rows && !strided_span(rows, cols, row_stride, col_stride)) return fail(ctx, TPST_E_ARG, "bad strides");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   if (!rows) return TPST_OK;
   return batch_commit(ctx, g, (const uint32_t*)d_scalars, rows, row_stride, col_stride, nullptr, nullptr,
@@ -176,7 +176,7 @@ extern "C" int tpst_pedersen_commit_slice(tpst_ctx* ctx, const tpst_gens* g, con
                                           const uint64_t* blind, uint64_t* out) {
   if (!ctx || !g || !blind || !out) return fail(ctx, TPST_E_ARG, "null argument");
   if (!g->has_h) return fail(ctx, TPST_E_STATE, "generator set has no blinding base h");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   return host_batch(ctx, g, scalars, 1, n, n, 1, blind, out);
 }
@@ -187,7 +187,7 @@ extern "C" int tpst_pedersen_commit_rows(tpst_ctx* ctx, const tpst_gens* g, cons
   if (!g->has_h) return fail(ctx, TPST_E_STATE, "generator set has no blinding base h");
   if (!n_rows || n_z % n_rows) return fail(ctx, TPST_E_ARG, "L_size * R_size != |Z| (dense_mlpoly.rs:320)");
   const size_t R = n_z / n_rows;
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   return host_batch(ctx, g, Z, n_rows, R, R, 1, blinds, out);
 }

@@ -344,7 +344,7 @@ extern "C" int tpst_gens_new(tpst_ctx* ctx, size_t n, const uint8_t* label, size
   static const SqrtConsts K = sqrt_consts();
   std::vector<uint64_t> pts(12 * (n + 1));
   {
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
     TPST_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
     void *d_seeds = nullptr, *d_out = nullptr;

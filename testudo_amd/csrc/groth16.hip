@@ -330,7 +330,7 @@ extern "C" int tpst_groth16_setup(tpst_ctx* ctx, tpst_r1cs* R, const uint64_t* t
     const uint64_t* t = toxic + 4 * k;
     if (!(t[0] | t[1] | t[2] | t[3])) return setup_fail(ctx, "toxic waste value is zero");
   }
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
   std::unique_ptr<tpst_groth16_pk> P(new tpst_groth16_pk());
@@ -464,7 +464,7 @@ extern "C" int tpst_groth16_vk(tpst_ctx* ctx, const tpst_groth16_pk* pk, uint64_
   if (!ctx || !pk || !alpha_g1 || !beta_g2 || !gamma_g2 || !delta_g2 || !gamma_abc_g1)
     return fail(ctx, TPST_E_ARG, "null argument");
   if (pk->owner != ctx) return fail(ctx, TPST_E_ARG, "proving key belongs to another context");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
   Buf o;
@@ -537,7 +537,7 @@ extern "C" int tpst_groth16_witness_map(tpst_ctx* ctx, tpst_groth16_pk* pk, tpst
                                         const uint64_t* inputs, uint64_t* h) {
   if (!ctx || !pk || !R || !vars || (R->num_inputs && !inputs) || !h) return fail(ctx, TPST_E_ARG, "null argument");
   if (int rc = check_inputs(ctx, pk, R, vars, inputs)) return rc;
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   if (int rc = upload_assignment(ctx, pk, vars, inputs)) return rc;
   TPST_HIP(ctx, witness_map(pk, R, ctx->stream));
@@ -553,7 +553,7 @@ extern "C" int tpst_groth16_prove(tpst_ctx* ctx, tpst_groth16_pk* pk, tpst_r1cs*
     return fail(ctx, TPST_E_ARG, "null argument");
   if (int rc = check_inputs(ctx, pk, R, vars, inputs)) return rc;
   if (!fr_ok_host(rs) || !fr_ok_host(rs + 4)) return fail(ctx, TPST_E_ARG, "r or s >= r");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
   tpst_groth16_pk* P = pk;

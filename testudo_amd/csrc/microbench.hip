@@ -271,7 +271,7 @@ __global__ void __launch_bounds__(64) k_selftest_inv(const uint32_t* __restrict_
 extern "C" int tpst_selftest_inv(tpst_ctx* ctx, size_t n, const uint64_t* in, uint64_t* out_lane, uint64_t* out_wave) {
   if (!ctx || (n && (!in || !out_lane || !out_wave))) return fail(ctx, TPST_E_ARG, "bad argument");
   if (!n) return TPST_OK;
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   ctx->io.reset();
   TPST_HIP(ctx, ctx->io.reserve(3 * Arena::need(n * 12, 4)));
@@ -419,7 +419,7 @@ __device__ __forceinline__ void mb_rns_body(const LT& L, uint32_t* s_slots, uint
 
 extern "C" int tpst_microbench_wave_phases(tpst_ctx* ctx, int op, int iters, uint64_t* cycles5) {
   if (!ctx || !cycles5 || op < 0 || op >= wave::N_OPS || iters <= 0) return fail(ctx, TPST_E_ARG, "bad argument");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   ctx->io.reset();
   TPST_HIP(ctx, ctx->io.reserve(256));
@@ -434,7 +434,7 @@ extern "C" int tpst_microbench_wave_phases(tpst_ctx* ctx, int op, int iters, uin
 
 extern "C" int tpst_microbench(tpst_ctx* ctx, int kind, size_t threads, int iters, double* ms) {
   if (!ctx || !ms || threads == 0 || iters <= 0) return fail(ctx, TPST_E_ARG, "bad argument");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   const bool rnsk = kind >= 64 && kind < 96;
   const unsigned bs = rnsk ? 768u : (threads < 256 ? (unsigned)threads : 256u);

@@ -62,6 +62,7 @@ struct Arena {
   hipStream_t aux[N_AUX] = {};
   hipEvent_t aux_ev[N_AUX_EV] = {};
   bool aux_ready = false;
+  Arena* aux_from = nullptr;  // borrow that arena's aux streams (own events only)
   hipError_t aux_init();
   hipError_t reserve(size_t bytes);
   void reset() { off = 0; }
@@ -87,9 +88,13 @@ int msm_window_bits(size_t n);
 // Variable-base MSM over device buffers.  bases: n affine points,
 // Montgomery form (24 / 48 u32 each); scalars: n canonical Fr (8 u32 each).
 // Writes one XYZZ point to d_out.  Returns hipSuccess or the first error.
+// tail != nullptr: the last window group's fixup, reduction and window chain
+// (the latency-bound tail) may run on `tail` instead of s -- then *on_tail is
+// set and d_out is final in `tail`'s order (s is free for the next call's
+// decomposition and accumulation; the caller keeps the arena until then).
 template <class F>
 hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint32_t* d_scalars,
-                   size_t n, Xyzz<F>* d_out);
+                   size_t n, Xyzz<F>* d_out, hipStream_t tail = nullptr, bool* on_tail = nullptr);
 
 // Fixed-base tables for K1: T[w][j] = 2^(c w) * B_j (affine, Montgomery).
 struct BatchTables {

@@ -1294,7 +1294,8 @@ static void msm_group_bounds(int W, int NG, int* wb) {
 
 template <class F>
 hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint32_t* d_scalars, size_t n,
-                   Xyzz<F>* d_out) {
+                   Xyzz<F>* d_out, hipStream_t tail, bool* on_tail) {
+  if (on_tail) *on_tail = false;
   if (n == 0) {
     Xyzz<F> inf = Xyzz<F>::inf();
     return hipMemcpyAsync(d_out, &inf, sizeof(inf), hipMemcpyHostToDevice, s);
@@ -1422,6 +1423,9 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   // group g > 0 run on an aux stream (a separate low-priority accumulation
   // stream measured slower: 4+ streams share the hardware queues)
   hipStream_t bulk = s;
+  // the last group's tail: on `tail` when the caller pipelines calls
+  const hipStream_t t0 = (tail && NG > 1) ? tail : s;
+  if (on_tail) *on_tail = t0 != s;
   pf->begin(ST_BUCKET_ACC, bulk);
   for (int g = NG - 1; g >= 0; g--) {  // top windows first: their chains are the longest
     const int wlo = wb[g], whi = wb[g + 1];
@@ -1448,7 +1452,7 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
     TPST_TRY(hipGetLastError());
     if (g == 0) pf->end(ST_BUCKET_ACC, bulk);
     const size_t b0 = (size_t)wlo * nb, b1 = (size_t)whi * nb;
-    hipStream_t a = g ? ar.aux[g % Arena::N_AUX] : s;
+    hipStream_t a = g ? ar.aux[g % Arena::N_AUX] : t0;
     if (NG > 1) {
       TPST_TRY(hipEventRecord(ar.aux_ev[2 * g], bulk));
       TPST_TRY(hipStreamWaitEvent(a, ar.aux_ev[2 * g], 0));
@@ -1475,14 +1479,14 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
     TPST_TRY(hipEventRecord(ar.aux_ev[2 * g + 1], a));
   }
   const int w1 = wb[1];  // group 0 = windows [0, w1)
-  pf->begin(ST_REDUCE, s);
-  TPST_TRY(reduce_buckets<F>(ar, s, buckets, (size_t)w1, nb, win));  // the latency-bound short-segment one
-  pf->end(ST_REDUCE, s);
-  pf->begin(ST_COMBINE, s);
-  for (int g = 1; g < NG; g++) TPST_TRY(hipStreamWaitEvent(s, ar.aux_ev[2 * g + 1], 0));
-  k_window_chain<F><<<1, 64, 0, s>>>(win, 0, w1, c, contrib + 1, NG - 1, d_out);
+  pf->begin(ST_REDUCE, t0);
+  TPST_TRY(reduce_buckets<F>(ar, t0, buckets, (size_t)w1, nb, win));  // the latency-bound short-segment one
+  pf->end(ST_REDUCE, t0);
+  pf->begin(ST_COMBINE, t0);
+  for (int g = 1; g < NG; g++) TPST_TRY(hipStreamWaitEvent(t0, ar.aux_ev[2 * g + 1], 0));
+  k_window_chain<F><<<1, 64, 0, t0>>>(win, 0, w1, c, contrib + 1, NG - 1, d_out);
   TPST_TRY(hipGetLastError());
-  pf->end(ST_COMBINE, s);
+  pf->end(ST_COMBINE, t0);
   return hipSuccess;
 }
 
@@ -1552,7 +1556,7 @@ void Arena::release() {
   if (aux_ready) {
     for (auto& st : aux) {
       (void)hipStreamSynchronize(st);
-      (void)hipStreamDestroy(st);
+      if (!aux_from) (void)hipStreamDestroy(st);
       st = nullptr;
     }
     for (auto& e : aux_ev) {
@@ -1567,7 +1571,12 @@ hipError_t Arena::aux_init() {
   if (aux_ready) return hipSuccess;
   int least = 0, greatest = 0;
   if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
-  for (auto& st : aux) TPST_TRY(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, greatest));
+  if (aux_from) {
+    TPST_TRY(aux_from->aux_init());
+    for (int i = 0; i < N_AUX; i++) aux[i] = aux_from->aux[i];
+  } else {
+    for (auto& st : aux) TPST_TRY(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, greatest));
+  }
   for (auto& e : aux_ev) TPST_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   aux_ready = true;
   return hipSuccess;
@@ -1910,13 +1919,15 @@ hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint3
 }
 
 // explicit instantiations (G1)
-template hipError_t msm_var<Fq>(Arena&, hipStream_t, const uint32_t*, const uint32_t*, size_t, Xyzz<Fq>*);
+template hipError_t msm_var<Fq>(Arena&, hipStream_t, const uint32_t*, const uint32_t*, size_t, Xyzz<Fq>*, hipStream_t,
+                                bool*);
 template hipError_t points_to_mont<Fq>(hipStream_t, const uint32_t*, uint32_t*, size_t);
 template hipError_t affine_from_mont<Fq>(hipStream_t, const uint32_t*, uint32_t*, size_t);
 template hipError_t xyzz_to_affine_canonical<Fq>(hipStream_t, const Xyzz<Fq>*, uint32_t*, size_t);
 #else
 // explicit instantiations (G2)
-template hipError_t msm_var<Fq2>(Arena&, hipStream_t, const uint32_t*, const uint32_t*, size_t, Xyzz<Fq2>*);
+template hipError_t msm_var<Fq2>(Arena&, hipStream_t, const uint32_t*, const uint32_t*, size_t, Xyzz<Fq2>*,
+                                 hipStream_t, bool*);
 template hipError_t points_to_mont<Fq2>(hipStream_t, const uint32_t*, uint32_t*, size_t);
 template hipError_t affine_from_mont<Fq2>(hipStream_t, const uint32_t*, uint32_t*, size_t);
 template hipError_t xyzz_to_affine_canonical<Fq2>(hipStream_t, const Xyzz<Fq2>*, uint32_t*, size_t);

@@ -325,7 +325,7 @@ extern "C" uint64_t tpst_fr_stream(uint64_t seed, size_t n, uint64_t start, uint
 // powers_of_g[i][x] = g^{eq(t[i..], x)} (LSB-first), g_mask[i] = g^{t_i}
 extern "C" int tpst_srs_setup(tpst_ctx* ctx, int nv, uint64_t seed) {
   if (!ctx || nv <= 0 || nv > 28) return fail(ctx, TPST_E_ARG, "bad nv");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   std::vector<uint64_t> vals(4 * (nv + 2));
   tpst_fr_stream(seed, nv + 2, 0, vals.data());
@@ -409,7 +409,7 @@ extern "C" int tpst_srs_setup(tpst_ctx* ctx, int nv, uint64_t seed) {
 
 extern "C" int tpst_srs_load(tpst_ctx* ctx, int nv, const uint64_t* flat) {
   if (!ctx || !flat || nv <= 0 || nv > 28) return fail(ctx, TPST_E_ARG, "bad argument");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   return srs_install(ctx, nv, flat);
 }
@@ -519,7 +519,7 @@ extern "C" int tpst_poly_from_evaluations(tpst_ctx* ctx, const uint64_t* Z, int 
   if (!ctx || !Z || !out) return fail(ctx, TPST_E_ARG, "null argument");
   auto p = std::make_unique<tpst_poly>();
   if (poly_dims(n, p->m_col, p->m_row, p->odd)) return fail(ctx, TPST_E_ARG, "bad num_vars");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   p->ctx = ctx;
   p->n = n;
@@ -540,7 +540,7 @@ extern "C" int tpst_poly_from_evaluations_cols(tpst_ctx* ctx, const uint64_t* Z,
   if (poly_dims(n, p->m_col, p->m_row, p->odd)) return fail(ctx, TPST_E_ARG, "bad num_vars");
   const size_t C = (size_t)1 << p->m_col, N = (size_t)1 << p->m_row;
   if (c0 >= c1 || c1 > C) return fail(ctx, TPST_E_ARG, "bad column range");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   p->ctx = ctx;
   p->n = n;
@@ -619,7 +619,7 @@ static int poly_get_q(tpst_ctx* ctx, tpst_poly* p, const uint64_t* point) {
 
 extern "C" int tpst_poly_eval(tpst_ctx* ctx, tpst_poly* p, const uint64_t* point, uint64_t* out_v) {
   if (!ctx || !p || !point || !out_v) return fail(ctx, TPST_E_ARG, "null argument");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   if (int rc = poly_need_q_source(ctx, p)) return rc;
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   if (!p->has_q) {
@@ -695,7 +695,7 @@ static int poly_commit_dev(tpst_ctx* ctx, tpst_poly* p, uint32_t* d_comms_mont, 
 extern "C" int tpst_poly_commit(tpst_ctx* ctx, tpst_poly* p, uint64_t* comms, uint64_t* T) {
   if (!ctx || !p || !comms || !T) return fail(ctx, TPST_E_ARG, "null argument");
   TraceRange tr("sqrt_commit");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   if (int rc = poly_need_full(ctx, p)) return rc;
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   const size_t C = (size_t)1 << p->m_col;
@@ -726,7 +726,7 @@ extern "C" int tpst_poly_commit(tpst_ctx* ctx, tpst_poly* p, uint64_t* comms, ui
 // device-resident commit: d_comms canonical affine (C*96 B), d_T canonical GT
 extern "C" int tpst_poly_commit_dev(tpst_ctx* ctx, tpst_poly* p, void* d_comms, void* d_T) {
   if (!ctx || !p || !d_comms || !d_T) return fail(ctx, TPST_E_ARG, "null argument");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   if (int rc = poly_need_full(ctx, p)) return rc;
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   const size_t C = (size_t)1 << p->m_col;
@@ -745,7 +745,7 @@ extern "C" int tpst_poly_commit_dev(tpst_ctx* ctx, tpst_poly* p, void* d_comms, 
 // i.e. this rank's block of columns of Z.  comms: (r1-r0) canonical affine G1.
 extern "C" int tpst_poly_commit_rows(tpst_ctx* ctx, tpst_poly* p, size_t r0, size_t r1, uint64_t* comms) {
   if (!ctx || !p || !comms || r1 < r0) return fail(ctx, TPST_E_ARG, "bad argument");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   SrsState* st = srs_of(ctx);
   if (!st) return fail(ctx, TPST_E_STATE, "no SRS loaded");
@@ -772,7 +772,7 @@ extern "C" int tpst_poly_ipp(tpst_ctx* ctx, int n, const uint64_t* comms, uint64
   if (!ctx || !comms || !T) return fail(ctx, TPST_E_ARG, "null argument");
   int m_col, m_row, odd;
   if (poly_dims(n, m_col, m_row, odd)) return fail(ctx, TPST_E_ARG, "bad num_vars");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   SrsState* st = srs_of(ctx);
   if (!st) return fail(ctx, TPST_E_STATE, "no SRS loaded");
@@ -804,7 +804,7 @@ extern "C" int tpst_poly_ipp(tpst_ctx* ctx, int n, const uint64_t* comms, uint64
 static int commit_rows_partial(tpst_ctx* ctx, tpst_poly* p, size_t r0, size_t r1, uint64_t* comms, uint64_t* miller,
                                void* d_out) {
   if (!ctx || !p || ((!comms || !miller) && !d_out) || r1 < r0) return fail(ctx, TPST_E_ARG, "bad argument");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   SrsState* st = srs_of(ctx);
   if (!st) return fail(ctx, TPST_E_STATE, "no SRS loaded");
@@ -867,7 +867,7 @@ extern "C" int tpst_poly_commit_rows_partial_dev(tpst_ctx* ctx, tpst_poly* p, si
 static int final_exp_product(tpst_ctx* ctx, const uint64_t* partials, const void* d_partials, size_t stride,
                              size_t k, uint64_t* T) {
   if (!ctx || (!partials && !d_partials && k) || !T) return fail(ctx, TPST_E_ARG, "null argument");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
   DevBuf up, out;
@@ -923,7 +923,7 @@ static int chi_b_table(tpst_ctx* ctx, int m_col, int m_row, const uint64_t* poin
 static int poly_q_partial(tpst_ctx* ctx, tpst_poly* p, const uint64_t* point, size_t r0, size_t r1, void* d_out,
                           uint64_t* h_out) {
   if (!ctx || !p || !point || (!d_out && !h_out) || r1 < r0) return fail(ctx, TPST_E_ARG, "bad argument");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   if (p->q_only) return fail(ctx, TPST_E_STATE, "opening-only handle holds no evaluations");
   for (int i = 0; i < p->n; i++)
@@ -962,7 +962,7 @@ extern "C" int tpst_poly_get_q_partial_dev(tpst_ctx* ctx, tpst_poly* p, const ui
 
 extern "C" int tpst_fr_sum_dev(tpst_ctx* ctx, const void* d_parts, size_t k, size_t n, void* d_out) {
   if (!ctx || (n && (!d_parts || !d_out))) return fail(ctx, TPST_E_ARG, "null argument");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   TPST_HIP(ctx, fr_sum_parts(ctx->stream, (const uint32_t*)d_parts, k, n, (uint32_t*)d_out));
   TPST_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -980,7 +980,7 @@ extern "C" int tpst_poly_cu_partial(tpst_ctx* ctx, int n, const uint64_t* point,
     if (!fr_ok(point + 4 * i)) return fail(ctx, TPST_E_ARG, "point coordinate >= r");
   std::vector<uint64_t> sc((r1 - r0) * 4 + 4);
   {
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
     TPST_HIP(ctx, hipSetDevice(ctx->device));
     DevBuf chis;
     if (int rc = chi_b_table(ctx, m_col, m_row, point, chis)) return rc;
@@ -1008,7 +1008,7 @@ extern "C" int tpst_poly_from_q_dev(tpst_ctx* ctx, int n, const uint64_t* point,
   for (int i = 0; i < n; i++)
     if (!fr_ok(point + 4 * i)) return fail(ctx, TPST_E_ARG, "point coordinate >= r");
   if (U && !point_valid<Fq>(U)) return fail(ctx, TPST_E_ARG, "c_u is not a valid G1 point");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   p->ctx = ctx;
   p->n = n;
@@ -1220,7 +1220,7 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
   const bool shd = sh != nullptr;
   const int W = shd ? sh->W : 1, rho = shd ? sh->rank : 0;
   const bool lead = rho == 0;  // produces the proof (and the PST proof of q)
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   if (lead)
     if (int rc = poly_need_q_source(ctx, p)) return rc;
   TPST_HIP(ctx, hipSetDevice(ctx->device));
@@ -2062,7 +2062,7 @@ static int mlpc_args(tpst_ctx* ctx, SrsState* st, int nv) {
 template <class F>
 static int mlpc_commit_impl(tpst_ctx* ctx, const uint64_t* evals, int nv, uint64_t* out) {
   if (!ctx || !evals || !out) return fail(ctx, TPST_E_ARG, "null argument");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   SrsState* st = srs_of(ctx);
   int rc = mlpc_args(ctx, st, nv);
@@ -2100,7 +2100,7 @@ extern "C" int tpst_mlpc_commit_g2(tpst_ctx* ctx, const uint64_t* evals, int nv,
 template <class F>
 static int mlpc_open_impl(tpst_ctx* ctx, const uint64_t* evals, int nv, const uint64_t* point, uint64_t* proofs) {
   if (!ctx || !evals || !point || !proofs) return fail(ctx, TPST_E_ARG, "null argument");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   SrsState* st = srs_of(ctx);
   int rc = mlpc_args(ctx, st, nv);
@@ -2142,7 +2142,7 @@ extern "C" int tpst_mlpc_open_g1(tpst_ctx* ctx, const uint64_t* evals, int nv, c
 extern "C" int tpst_mlpc_check(tpst_ctx* ctx, int nv, const uint64_t* comm, const uint64_t* point,
                                const uint64_t* value, const uint64_t* proofs) {
   if (!ctx || !comm || !point || !value || (nv && !proofs)) return fail(ctx, TPST_E_ARG, "null argument");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   SrsState* st = srs_of(ctx);
   int rc = mlpc_args(ctx, st, nv);
@@ -2156,7 +2156,7 @@ extern "C" int tpst_mlpc_check(tpst_ctx* ctx, int nv, const uint64_t* comm, cons
 extern "C" int tpst_mlpc_check_2(tpst_ctx* ctx, int nv, const uint64_t* comm_h, const uint64_t* point,
                                  const uint64_t* value, const uint64_t* proofs) {
   if (!ctx || !comm_h || !point || !value || (nv && !proofs)) return fail(ctx, TPST_E_ARG, "null argument");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   SrsState* st = srs_of(ctx);
   int rc = mlpc_args(ctx, st, nv);
@@ -2201,7 +2201,7 @@ extern "C" int tpst_pst_verify(tpst_ctx* ctx, tpst_transcript* tr, int n, const 
   if (!ctx || !tr || !point || !v || !T || !proof) return fail(ctx, TPST_E_ARG, "null argument");
   int m_col, m_row, odd;
   if (poly_dims(n, m_col, m_row, odd)) return fail(ctx, TPST_E_ARG, "bad num_vars");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   SrsState* st = srs_of(ctx);
   if (!st) return fail(ctx, TPST_E_STATE, "no SRS loaded");

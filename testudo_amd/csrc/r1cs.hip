@@ -383,7 +383,7 @@ extern "C" int tpst_r1cs_load(tpst_ctx* ctx, size_t num_cons, size_t num_vars, s
                               const uint64_t* const* vals, tpst_r1cs** out) {
   if (!ctx || !nnz || !rows || !cols || !vals || !out) return fail(ctx, TPST_E_ARG, "null argument");
   if (int rc = r1cs_dims(ctx, num_cons, num_vars, num_inputs)) return rc;
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   std::unique_ptr<tpst_r1cs> R(new tpst_r1cs());
   R->owner = ctx;
@@ -428,7 +428,7 @@ extern "C" int tpst_r1cs_synthetic(tpst_ctx* ctx, size_t num_cons, size_t num_va
   Z[4 * num_vars] = 1;  // the constant term
   memcpy(vars, Z.data(), num_vars * 32);
   if (num_inputs) memcpy(inputs, &Z[4 * (num_vars + 1)], num_inputs * 32);
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   std::unique_ptr<tpst_r1cs> R(new tpst_r1cs());
   R->owner = ctx;
@@ -480,7 +480,7 @@ extern "C" int tpst_eq_evals(tpst_ctx* ctx, const uint64_t* r, int ell, uint64_t
     rm[j] = frc(r + 4 * j);
   }
   const size_t n = (size_t)1 << ell;
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
   Buf dr, dt;
@@ -592,7 +592,7 @@ extern "C" int tpst_r1cs_prove(tpst_ctx* ctx, tpst_r1cs* R, const uint64_t* vars
   Fr fin1[4], fin2[2];
   Fr rA, rB, rC;
   {
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
     TPST_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
     const size_t M = R->num_cons, Nz = R->ncols;
@@ -693,7 +693,7 @@ extern "C" int tpst_r1cs_commit(tpst_ctx* ctx, tpst_r1cs* R, const uint8_t* labe
   if (3 * N >= ((size_t)1 << 31)) return fail(ctx, TPST_E_ARG, "instance too large");
   Buf ops, mem;
   {
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    std::lock_guard<tpst::CtxMutex> lk(ctx->mu);
     TPST_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
     const size_t M3 = 3 * N;
