@@ -132,25 +132,16 @@ TPST_HD Fq29 mul3(const Fq29& a) { return add(dbl(a), a); }
 // a_i b_j and m_i p_j (i < k) in one 64-bit accumulator (<= 26 terms < 2^58
 // each), then the reduction word m_k = -acc mod 2^29 (p_0 = 1) for k < 13 or
 // the output limb, and the carry acc >> 29 moves to the next column.
-// TPST_F29_2ACC (default): a column's a_i b_j terms and its m_i p_j terms
-// go to two independent 64-bit accumulators, joined once per column -- two
-// dependency chains of v_mad_u64_u32 instead of one chain of up to 26
-// (the accumulation kernels run at 2 waves per SIMD, where one chain per
-// wave leaves the SIMD idle on the multiply-add latency)
-#ifndef TPST_F29_2ACC
-#define TPST_F29_2ACC 1
-#endif
+// (Two accumulators per column -- the a_i b_j and the m_i p_j terms as two
+// dependency chains -- measured neutral: 2^20 MSM 219.6 vs 218.7 Mscalar/s,
+// product latency 0.91 us either way; a lone wave is issue-bound, not
+// latency-bound, profiles/r05/ab1.)
 TPST_HD Fq29 mul(const Fq29& a, const Fq29& b) {
   constexpr int N = r29::N;
   uint32_t m[N], t[N];
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 2 * N - 1; k++) {
-#if TPST_F29_2ACC
-    uint64_t acc2 = 0;
-#else
-    uint64_t& acc2 = acc;
-#endif
 #pragma unroll
     for (int i = 0; i < N; i++) {
       const int j = k - i;
@@ -159,11 +150,8 @@ TPST_HD Fq29 mul(const Fq29& a, const Fq29& b) {
 #pragma unroll
     for (int i = 0; i < N; i++) {
       const int j = k - i;
-      if (i < k && j >= 1 && j < N) acc2 += (uint64_t)m[i] * r29::P[j];
+      if (i < k && j >= 1 && j < N) acc += (uint64_t)m[i] * r29::P[j];
     }
-#if TPST_F29_2ACC
-    acc += acc2;
-#endif
     if (k < N) {
       m[k] = (0u - (uint32_t)acc) & r29::M;
       acc += m[k];
@@ -195,19 +183,11 @@ TPST_HD Fq29 sqr(const Fq29& a) {
     }
     acc += cr << 1;  // <= 13 cross terms < 2^58: doubled < 2^63
     if ((k & 1) == 0 && (k >> 1) < N) acc += (uint64_t)a.v[k >> 1] * a.v[k >> 1];
-#if TPST_F29_2ACC
-    uint64_t acc2 = 0;
-#else
-    uint64_t& acc2 = acc;
-#endif
 #pragma unroll
     for (int i = 0; i < N; i++) {
       const int j = k - i;
-      if (i < k && j >= 1 && j < N) acc2 += (uint64_t)m[i] * r29::P[j];
+      if (i < k && j >= 1 && j < N) acc += (uint64_t)m[i] * r29::P[j];
     }
-#if TPST_F29_2ACC
-    acc += acc2;
-#endif
     if (k < N) {
       m[k] = (0u - (uint32_t)acc) & r29::M;
       acc += m[k];

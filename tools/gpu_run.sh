@@ -7,6 +7,7 @@
 #   prof    rocprofv3 kernel traces + stats: MSM bench, 2^20 and 2^24 commit+open
 #   pmc     PMC passes (FETCH_SIZE, WRITE_SIZE, VALU, stall counters) on the MSM bench
 #   k1pmc   PMC passes (FETCH_SIZE, WRITE_SIZE, VALU) on the 2^24 commit (K1)
+#   solo    per-rank latency of the sharded opening (tools/shard_open_solo.py, W = 2/4/8)
 #   list    rocprofv3 -L (available counters)
 # Every GPU step runs under its own time limit; the first failure ends the script.
 set -o pipefail
@@ -47,6 +48,9 @@ for step in "$@"; do
       timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/k1_write -o run -- python3 $K1 > $OUT/k1_write.log 2>&1 || exit 1
       timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES --output-format csv -d $OUT/k1_valu -o run -- python3 $K1 > $OUT/k1_valu.log 2>&1 || exit 1
       cd $R && python tools/pmc_k1.py $OUT/pmc_bucket_acc_chunk_2p24.json $OUT/k1_fetch $OUT/k1_write $OUT/k1_valu $OUT/prof_open24 > $OUT/pmc_k1.log 2>&1 ;;
+    solo)
+      cd $R && for w in 2 4 8; do timeout -k 10 300 python -u tools/shard_open_solo.py 24 $w 5 >> $OUT/shard_open_solo.jsonl 2>> $OUT/shard_open_solo.err || exit 1; done
+      cd $R && timeout -k 10 300 python -u tools/shard_open_solo.py 20 8 5 >> $OUT/shard_open_solo.jsonl 2>> $OUT/shard_open_solo.err || exit 1 ;;
     list)
       cd /tmp && timeout -s KILL 60 rocprofv3 -L > $OUT/counters.txt 2>&1 || exit 1 ;;
     *)
