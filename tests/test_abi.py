@@ -69,3 +69,20 @@ def test_product_stream_matches_oracle():
     a, k1 = fr_stream(0x7E57D0, 50)
     b, k2 = orc.fr_stream(0x7E57D0, 50)
     assert np.array_equal(a, b) and k1 == k2
+
+
+def test_one_hip_runtime_per_process():
+    """Loading libtpst pulls torch's HIP runtime in first (testudo_amd/_lib.py),
+    so the library and torch share one libamdhip64 / libhsa-runtime64: two
+    runtimes in one process leave torch without a GPU and make device
+    pointers and streams unshareable."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from testudo_amd import _lib; _lib.load()\n"
+            "maps = open('/proc/self/maps').read().splitlines()\n"
+            "libs = sorted(set(l.split()[-1] for l in maps if 'libamdhip64' in l))\n"
+            "print(len(libs), libs)\n") % ROOT
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.startswith("1 "), r.stdout

@@ -185,6 +185,15 @@ def load() -> C.CDLL:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError("libtpst.so not built (%s); run testudo_amd/build.py" % LIB_PATH)
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7 /
+    # libhsa-runtime64.so.1.  Loaded first, it satisfies libtpst's
+    # dependencies by soname; loaded after libtpst (which links /opt/rocm's),
+    # both runtimes would initialise the device and torch finds no GPU --
+    # and device pointers / streams could not be shared across the two.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(LIB_PATH)
     for name, res, args in PROTOTYPES:
         fn = getattr(lib, name)
