@@ -457,7 +457,7 @@ def pst_leg(ctx, log_n, reps=5):
     verify_s = time.perf_counter() - t
     sizes = _wire_sizes(ctx, nv, pst_proof, mipp)
     env_tab = os.environ.get("TPST_COMMIT_TABLE")
-    in_commit = (env_tab != "0") if env_tab is not None else (1 << (log_n // 2)) <= 2048
+    in_commit = env_tab != "0"
     return {"log_n": log_n, "commit_s": round(c, 4), "open_s": round(o, 4), **sizes,
             "fold_table_in_commit": in_commit,
             "fold_table_note": ("the opening's GLV fold table over comm_list is built by the commit (beside its "

@@ -5,9 +5,8 @@ fixtures / the CPU oracle:
 
 * TPST_OPEN_TRACE=1 -- diagnostics only: the per-round trace is printed and
   the n = 20 proof is unchanged (fixture fullsize_n20.json);
-* TPST_COMMIT_TABLE=0 at n = 20 (the opening builds the fold table itself)
-  and =1 at n = 24 (the commit prebuilds it for 4096 rows) -- same proofs as
-  the fixtures;
+* TPST_COMMIT_TABLE=0 at n = 20 and n = 24 (the opening builds the fold
+  table itself instead of the commit) -- same proofs as the fixtures;
 * TPST_ACC_LDS=1 -- the LDS-staged MSM accumulation, 2^17 + 37 points vs the
   oracle.
 """
@@ -81,8 +80,8 @@ def test_open_trace_leaves_proof_unchanged():
     assert err.count("open round") == 10, err[-2000:]
 
 
-@pytest.mark.parametrize("n,val", [(20, "0"), (24, "1")])
-def test_commit_table_forced_off_and_on(n, val):
+@pytest.mark.parametrize("n,val", [(20, "0"), (24, "0")])
+def test_commit_table_forced_off(n, val):
     ok, _ = _run(_OPEN % {"root": ROOT, "n": n}, {"TPST_COMMIT_TABLE": val})
     assert all(ok.values()), ok
 

@@ -98,7 +98,7 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
 
 // Fixed-base tables for K1: T[w][j] = 2^(c w) * B_j (affine, Montgomery).
 struct BatchTables {
-  uint32_t* d_table = nullptr;  // W * N affine G1 points
+  uint32_t* d_table = nullptr;  // W * N points T[w][j], 128-byte radix-2^29 records (msm.hip fetch_rec29)
   size_t N = 0;
   int c = 0;
   int W = 0;

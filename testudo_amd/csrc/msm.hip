@@ -521,6 +521,33 @@ static __global__ void __launch_bounds__(SORTB_THREADS)
   for (uint32_t p = nz + t; p < len; p += SORTB_THREADS) keys[s + p] = sent;
 }
 
+// K1 window-table record (msm_batch): one affine point already in the
+// accumulation field (field29.h radix 2^29, canonical), x (13 words) | y
+// (13 words) | 6 pad words = 128 bytes, so a gather is ONE aligned 128-byte
+// line (a 96-byte field.h point straddles two lines 3 times in 4) and needs
+// no conversion in the accumulation loop
+constexpr int REC29_WORDS = 32;
+__device__ __forceinline__ Affine<Fq29> fetch_rec29(const uint32_t* table, uint32_t v) {
+  const uint4* r = reinterpret_cast<const uint4*>(table + (size_t)(v & 0x7fffffffu) * REC29_WORDS);
+  uint32_t w[28];
+#pragma unroll
+  for (int i = 0; i < 7; i++) {
+    const uint4 q = r[i];
+    w[4 * i] = q.x;
+    w[4 * i + 1] = q.y;
+    w[4 * i + 2] = q.z;
+    w[4 * i + 3] = q.w;
+  }
+  Affine<Fq29> p;
+#pragma unroll
+  for (int i = 0; i < r29::N; i++) {
+    p.x.v[i] = w[i];
+    p.y.v[i] = w[r29::N + i];
+  }
+  if (v >> 31) p.y = neg(p.y);
+  return p;
+}
+
 template <class F>
 __device__ __forceinline__ Affine<F> fetch_point(const uint32_t* bases, const uint32_t* phib, uint32_t nbase,
                                                 uint32_t v) {
@@ -541,7 +568,8 @@ __device__ __forceinline__ Affine<F> fetch_point(const uint32_t* bases, const ui
 // (its owner's partial goes to bpart[workgroup]), so the fixup runs one thread
 // per workgroup instead of one per bucket.  The next point is loaded before
 // the current mixed add runs (software prefetch).
-template <class F, int MINW = (sizeof(F) > 48 ? 1 : 2)>
+// REC29: `bases` is a K1 window table of fetch_rec29 records (Fq only)
+template <class F, int MINW = (sizeof(F) > 48 ? 1 : 2), bool REC29 = false>
 __global__ void __launch_bounds__(ACC_BLOCK, MINW)
     k_bucket_acc_chunk(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals, size_t m_all,
                        const uint32_t* __restrict__ mend, uint32_t sent, const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend,
@@ -560,15 +588,21 @@ __global__ void __launch_bounds__(ACC_BLOCK, MINW)
   Xyzz<C> acc = Xyzz<C>::inf();
   if (c0 < m) {
     const size_t c1 = (c0 + ((size_t)1 << lg) < m) ? c0 + ((size_t)1 << lg) : m;
+    auto fetch = [&](uint32_t v) -> Affine<C> {
+      if constexpr (REC29)
+        return fetch_rec29(bases, v);
+      else
+        return A::in(fetch_point<F>(bases, phib, nbase, v));
+    };
     uint32_t key = keys[c0];
     Affine<C> pt;
-    if (key < sent) pt = A::in(fetch_point<F>(bases, phib, nbase, vals[c0]));
+    if (key < sent) pt = fetch(vals[c0]);
     for (size_t e = c0; e < c1; e++) {
       uint32_t key_n = sent;
       Affine<C> pt_n;
       if (e + 1 < c1) {
         key_n = keys[e + 1];
-        if (key_n < sent) pt_n = A::in(fetch_point<F>(bases, phib, nbase, vals[e + 1]));
+        if (key_n < sent) pt_n = fetch(vals[e + 1]);
       }
       if (key < sent) {
         acc = add_affine(acc, pt);
@@ -1608,7 +1642,15 @@ __global__ void __launch_bounds__(64, 1) k_build_tables(const uint32_t* __restri
   if (j >= N) return;
   G1A p = load_affine<Fq>(bases, j);
   for (int w = 0; w < W; w++) {
-    store_affine(table, (size_t)w * N + j, p);
+    {  // fetch_rec29 record (an infinity base stays all-zero: x = y = 0)
+      const Fq29 x = from_std(p.x), y = from_std(p.y);
+      uint32_t rec[REC29_WORDS];
+#pragma unroll
+      for (int i = 0; i < REC29_WORDS; i++) rec[i] = i < r29::N ? x.v[i] : i < 2 * r29::N ? y.v[i - r29::N] : 0u;
+      uint4* dst = reinterpret_cast<uint4*>(table + ((size_t)w * N + j) * REC29_WORDS);
+#pragma unroll
+      for (int i = 0; i < REC29_WORDS / 4; i++) dst[i] = make_uint4(rec[4 * i], rec[4 * i + 1], rec[4 * i + 2], rec[4 * i + 3]);
+    }
     if (w + 1 < W) {
       Xyzz<Fq> x = to_xyzz(p);
       for (int i = 0; i < c; i++) x = dbl(x);
@@ -1622,7 +1664,7 @@ hipError_t batch_tables_build(hipStream_t s, const uint32_t* d_bases, size_t N, 
   t.N = N;
   t.c = c;
   t.W = num_windows(c);
-  TPST_TRY(hipMalloc(&t.d_table, (size_t)t.W * N * 24 * sizeof(uint32_t)));
+  TPST_TRY(hipMalloc(&t.d_table, (size_t)t.W * N * REC29_WORDS * sizeof(uint32_t)));
   k_build_tables<<<grid_for(N, 64), 64, 0, s>>>(d_bases, N, c, t.W, t.d_table);
   return hipGetLastError();
 }
@@ -1899,9 +1941,9 @@ hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint3
   TPST_TRY(hipGetLastError());
   pf->end(ST_BATCH_SORT, s);
   pf->begin(ST_BUCKET_ACC, s);
-  k_bucket_acc_chunk<Fq><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys, entries, m, nullptr, (uint32_t)nbk, bstart, bend,
-                                                               t.d_table, nullptr, 0x7fffffffu, lg, buckets, part,
-                                                               bpart);
+  k_bucket_acc_chunk<Fq, 2, true><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys, entries, m, nullptr, (uint32_t)nbk, bstart,
+                                                                        bend, t.d_table, nullptr, 0x7fffffffu, lg,
+                                                                        buckets, part, bpart);
   TPST_TRY(hipGetLastError());
   k_bucket_fixup<Fq><<<grid_for(nblk, 64), 64, 0, s>>>(keys, m, nullptr, (uint32_t)nbk, bstart, bend, lg, nblk,
                                                        part, bpart, buckets);

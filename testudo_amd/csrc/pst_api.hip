@@ -703,14 +703,14 @@ extern "C" int tpst_poly_commit(tpst_ctx* ctx, tpst_poly* p, uint64_t* comms, ui
   TPST_HIP(ctx, cm.alloc(C * 96));
   TPST_HIP(ctx, tt.alloc(sizeof(Fq12)));
   TPST_HIP(ctx, out.alloc(C * 96 + 576));
-  // the table build fits beside the IPP up to C = 2048 row commitments (2^20:
-  // commit + open 21.7 -> 21.2 ms); at C = 4096 it outlasts the IPP and only
-  // moves ~2 ms from the open to the commit (2^24: 109.3 vs 109.8 ms)
+  // the table build runs beside the IPP (2^20: commit + open 21.7 -> 21.2
+  // ms); at C = 4096 it outlasts the IPP by ~2 ms but leaves the opening's
+  // first round free of it.  TPST_COMMIT_TABLE=0: the opening builds it
   static const int table_env = [] {
     const char* e = getenv("TPST_COMMIT_TABLE");
     return e ? atoi(e) : -1;
   }();
-  const bool prebuild = table_env < 0 ? C <= 2048 : table_env != 0;
+  const bool prebuild = table_env != 0;
   int rc = poly_commit_dev(ctx, p, cm.u(), (Fq12*)tt.p, prebuild);
   if (rc) return rc;
   hipStream_t s = ctx->stream;
