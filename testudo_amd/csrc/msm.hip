@@ -157,13 +157,32 @@ __device__ __forceinline__ void glv_phi_point(const uint32_t* __restrict__ bases
   store_affine(out, i, p);
 }
 
+// K2 (G1, GLV) gather records: P_i at index i and phi(P_i) at n + i in the
+// accumulation field, fetch_rec29's 128-byte layout (written by the
+// decomposition; TPST_K2_REC29=0 builds keep field.h points + phi(P) only)
+#ifndef TPST_K2_REC29
+#define TPST_K2_REC29 1
+#endif
+constexpr int REC29_WORDS = 32;
+__device__ __forceinline__ void store_rec29(uint32_t* table, size_t idx, const Affine<Fq>& p) {
+  const Fq29 x = from_std(p.x), y = from_std(p.y);
+  uint32_t rec[REC29_WORDS];
+#pragma unroll
+  for (int i = 0; i < REC29_WORDS; i++) rec[i] = i < r29::N ? x.v[i] : i < 2 * r29::N ? y.v[i - r29::N] : 0u;
+  uint4* dst = reinterpret_cast<uint4*>(table + idx * REC29_WORDS);
+#pragma unroll
+  for (int i = 0; i < REC29_WORDS / 4; i++) dst[i] = make_uint4(rec[4 * i], rec[4 * i + 1], rec[4 * i + 2], rec[4 * i + 3]);
+}
+
 // one tile of scalars: signed digits (arkworks make_digits over the GLV
 // halves), entries at slot (h W + w) n + i, bin counts, and phi of the bases
+// (or, rec != nullptr, the gather records of P and phi(P))
 template <class F>
 static __global__ void __launch_bounds__(SORT_THREADS)
     k_decompose_hist(const uint32_t* __restrict__ scalars, size_t n, int c, int W, int glv, uint32_t sent, int lo,
                      uint32_t nbins, size_t tile, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                     uint32_t* __restrict__ tab, const uint32_t* __restrict__ bases, uint32_t* __restrict__ phib) {
+                     uint32_t* __restrict__ tab, const uint32_t* __restrict__ bases, uint32_t* __restrict__ phib,
+                     uint32_t* __restrict__ rec) {
   extern __shared__ uint32_t hist[];
   for (uint32_t b = threadIdx.x; b < nbins; b += SORT_THREADS) hist[b] = 0;
   __syncthreads();
@@ -192,6 +211,15 @@ static __global__ void __launch_bounds__(SORT_THREADS)
         keys[slot] = key;
         vals[slot] = val;
         atomicAdd(&hist[key >> lo], 1u);
+      }
+    }
+    if constexpr (sizeof(F) == sizeof(Fq)) {
+      if (rec) {
+        Affine<Fq> p = load_affine<Fq>(bases, i);
+        store_rec29(rec, i, p);
+        if (!is_inf(p)) p.x = mul(p.x, Fq::from_limbs(params::G1_BETA));
+        store_rec29(rec, n + i, p);
+        continue;
       }
     }
     if (glv) glv_phi_point<F>(bases, i, phib);
@@ -526,7 +554,6 @@ static __global__ void __launch_bounds__(SORTB_THREADS)
 // (13 words) | 6 pad words = 128 bytes, so a gather is ONE aligned 128-byte
 // line (a 96-byte field.h point straddles two lines 3 times in 4) and needs
 // no conversion in the accumulation loop
-constexpr int REC29_WORDS = 32;
 __device__ __forceinline__ Affine<Fq29> fetch_rec29(const uint32_t* table, uint32_t v) {
   const uint4* r = reinterpret_cast<const uint4*>(table + (size_t)(v & 0x7fffffffu) * REC29_WORDS);
   uint32_t w[28];
@@ -672,7 +699,7 @@ __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
 // (range[w] = first sorted entry of window w, device-side): chunk indices stay
 // global (t = entry >> lg) so a chunk straddling two window groups is split
 // between their launches without sharing a part[] slot.
-template <class F, int MINW = (sizeof(F) > 48 ? 1 : 2)>
+template <class F, int MINW = (sizeof(F) > 48 ? 1 : 2), bool REC29 = false>
 __global__ void __launch_bounds__(64, MINW)
     k_bucket_acc_short(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
                        const uint32_t* __restrict__ range, int wlo, int whi, uint32_t sent,
@@ -687,16 +714,22 @@ __global__ void __launch_bounds__(64, MINW)
   if (c0 < e_lo) c0 = e_lo;
   using A = AccField<F>;
   using C = typename A::T;
+  auto fetch = [&](uint32_t v) -> Affine<C> {
+    if constexpr (REC29)
+      return fetch_rec29(bases, v);
+    else
+      return A::in(fetch_point<F>(bases, phib, nbase, v));
+  };
   uint32_t key = keys[c0];
   Affine<C> pt;
-  if (key < sent) pt = A::in(fetch_point<F>(bases, phib, nbase, vals[c0]));
+  if (key < sent) pt = fetch(vals[c0]);
   Xyzz<C> acc = Xyzz<C>::inf();
   for (size_t e = c0; e < c1; e++) {
     uint32_t key_n = sent;
     Affine<C> pt_n;
     if (e + 1 < c1) {
       key_n = keys[e + 1];
-      if (key_n < sent) pt_n = A::in(fetch_point<F>(bases, phib, nbase, vals[e + 1]));
+      if (key_n < sent) pt_n = fetch(vals[e + 1]);
     }
     if (key < sent) {
       acc = add_affine(acc, pt);
@@ -721,14 +754,17 @@ __global__ void __launch_bounds__(64, MINW)
 // destination), runs the current mixed add meanwhile, and reads the staged
 // point back with six ds_read_b128.  Frees the prefetched point's VGPRs
 // (occupancy) and moves the gathers off the register file.  TPST_ACC_LDS=1.
-template <int MINW>
+template <int MINW, bool REC29>
 __global__ void __launch_bounds__(64, MINW)
     k_bucket_acc_short_lds(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
                            const uint32_t* __restrict__ range, int wlo, int whi, uint32_t sent,
                            const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend,
                            const uint32_t* __restrict__ bases, const uint32_t* __restrict__ phib, uint32_t nbase,
                            int lg, Xyzz<Fq>* __restrict__ buckets, Xyzz<Fq>* __restrict__ part) {
-  __shared__ uint4 stage[2][6][64];  // 12 KB: double-buffered 96-byte points, piece-major
+  // double-buffered points, piece-major: 96-byte field.h points or the
+  // first 112 bytes of a 128-byte record (REC29)
+  constexpr int NP = REC29 ? 7 : 6;
+  __shared__ uint4 stage[2][NP][64];
   using A = AccField<Fq>;
   using C = typename A::T;
   const int lane = threadIdx.x;
@@ -743,26 +779,39 @@ __global__ void __launch_bounds__(64, MINW)
   // lanes without a point load bases[0]
   auto stage_load = [&](int buf, uint32_t v, bool want) {
     const uint32_t idx = v & 0x7fffffffu;
-    const uint32_t* src = want ? ((idx < nbase) ? bases + 24 * (size_t)idx : phib + 24 * (size_t)(idx - nbase)) : bases;
+    const uint32_t* src = !want ? bases
+                          : REC29 ? bases + (size_t)REC29_WORDS * idx
+                                  : ((idx < nbase) ? bases + 24 * (size_t)idx : phib + 24 * (size_t)(idx - nbase));
 #pragma unroll
-    for (int j = 0; j < 6; j++)
+    for (int j = 0; j < NP; j++)
       __builtin_amdgcn_global_load_lds((const void*)(src + 4 * j),
                                        (__attribute__((address_space(3))) void*)&stage[buf][j][0], 16, 0, 0);
   };
   auto stage_read = [&](int buf, uint32_t v) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint32_t w[24];
+    uint32_t w[4 * NP];
 #pragma unroll
-    for (int j = 0; j < 6; j++) {
+    for (int j = 0; j < NP; j++) {
       const uint4 q = stage[buf][j][lane];
       w[4 * j] = q.x;
       w[4 * j + 1] = q.y;
       w[4 * j + 2] = q.z;
       w[4 * j + 3] = q.w;
     }
-    Affine<Fq> p = {Fq::from_limbs(w), Fq::from_limbs(w + 12)};
-    if (v >> 31) p.y = neg(p.y);
-    return A::in(p);
+    if constexpr (REC29) {
+      Affine<C> p;
+#pragma unroll
+      for (int i = 0; i < r29::N; i++) {
+        p.x.v[i] = w[i];
+        p.y.v[i] = w[r29::N + i];
+      }
+      if (v >> 31) p.y = neg(p.y);
+      return p;
+    } else {
+      Affine<Fq> p = {Fq::from_limbs(w), Fq::from_limbs(w + 12)};
+      if (v >> 31) p.y = neg(p.y);
+      return A::in(p);
+    }
   };
   uint32_t key = active ? keys[c0] : sent;
   uint32_t val = active && key < sent ? vals[c0] : 0u;
@@ -1336,6 +1385,9 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   }
   if (n > MSM_MAX_POINTS) return hipErrorInvalidValue;
   const bool glv = n >= 64;  // phi(x, y) = (beta x, y) on G1, (beta^2 x, y) on G2
+  // G1 with GLV: gather records of P and phi(P) (fetch_rec29) instead of phi(P) alone
+  constexpr bool g1 = std::is_same<F, Fq>::value;
+  const bool rec29 = TPST_K2_REC29 && glv && g1;
   constexpr size_t PW = 2 * Words<F>::n;
   const int c = msm_window_bits(glv ? 2 * n : n);
   const int W = glv ? num_windows_bits(c, 128) : num_windows(c);
@@ -1370,7 +1422,8 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   size_t need = Arena::need(m, 4) * 4 + Arena::need(nbk, 4) * 2 + Arena::need(nbk, sizeof(Xyzz<F>)) +
                 Arena::need(2 * nchunk, sizeof(Xyzz<F>)) + Arena::need(nblk, sizeof(Xyzz<F>)) + red_need +
                 Arena::need(W, sizeof(Xyzz<F>)) + Arena::need(NG, sizeof(Xyzz<F>)) + Arena::need(W + 1, 4) +
-                Arena::need(glv ? n * PW : 1, 4) + Arena::need((size_t)sp.ntile * sp.nbins, 4) +
+                Arena::need(glv && !rec29 ? n * PW : 1, 4) + Arena::need(rec29 ? 2 * n * REC29_WORDS : 1, 4) +
+                Arena::need((size_t)sp.ntile * sp.nbins, 4) +
                 Arena::need(sp.nbins, 4) + Arena::need(sp.nbins + 1, 4) + Arena::need(NG, 4) +
                 Arena::need((size_t)NG * (m / ((size_t)LONG_PARTS << lg) + 1), 4) + 8192;
   ar.reset();
@@ -1387,7 +1440,10 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   Xyzz<F>* win = ar.take<Xyzz<F>>(W);
   Xyzz<F>* contrib = ar.take<Xyzz<F>>(NG);
   uint32_t* range = ar.take<uint32_t>(W + 1);
-  uint32_t* phib = ar.take<uint32_t>(glv ? n * PW : 1);
+  uint32_t* phib = ar.take<uint32_t>(glv && !rec29 ? n * PW : 1);
+  uint32_t* rec = rec29 ? ar.take<uint32_t>(2 * n * REC29_WORDS) : nullptr;
+  const uint32_t* gb = rec29 ? rec : d_bases;  // what the accumulation gathers
+  const uint32_t gnb = rec29 ? 0x7fffffffu : (uint32_t)n;
   uint32_t* tab = ar.take<uint32_t>((size_t)sp.ntile * sp.nbins);
   uint32_t* btot = ar.take<uint32_t>(sp.nbins);
   uint32_t* bin0 = ar.take<uint32_t>(sp.nbins + 1);
@@ -1404,7 +1460,8 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   pf->begin(ST_DECOMPOSE, s);
   if (short_chunks) TPST_TRY(hipMemsetAsync(lcnt, 0, NG * sizeof(uint32_t), s));
   k_decompose_hist<F><<<sp.ntile, SORT_THREADS, sp.nbins * 4, s>>>(d_scalars, n, c, W, glv ? 1 : 0, sent, sp.lo,
-                                                                  sp.nbins, sp.tile, keys, vals, tab, d_bases, phib);
+                                                                  sp.nbins, sp.tile, keys, vals, tab, d_bases, phib,
+                                                                  rec);
   TPST_TRY(hipGetLastError());
   pf->end(ST_DECOMPOSE, s);
   pf->begin(ST_SORT, s);
@@ -1437,8 +1494,18 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   pf->end(ST_SORT, s);
   if (!short_chunks) {  // one launch, long chunks (more than ~2^21 points)
     pf->begin(ST_BUCKET_ACC, s);
-    k_bucket_acc_chunk<F><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys, vals, m, range + W, sent, bstart, bend,
-                                                                d_bases, phib, (uint32_t)n, lg, buckets, part, bpart);
+    bool done = false;
+    if constexpr (g1) {
+      if (rec29) {
+        k_bucket_acc_chunk<Fq, 2, true><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys, vals, m, range + W, sent, bstart,
+                                                                              bend, gb, nullptr, gnb, lg, buckets,
+                                                                              part, bpart);
+        done = true;
+      }
+    }
+    if (!done)
+      k_bucket_acc_chunk<F><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys, vals, m, range + W, sent, bstart, bend,
+                                                                  d_bases, phib, (uint32_t)n, lg, buckets, part, bpart);
     TPST_TRY(hipGetLastError());
     k_bucket_fixup<F><<<grid_for(nblk, 64), 64, 0, s>>>(keys, m, range + W, sent, bstart, bend, lg, nblk, part, bpart,
                                                         buckets);
@@ -1476,9 +1543,15 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
         return e && atoi(e) != 0;
       }();
       const unsigned grid = grid_for(gchunks, 64);
-      if (lds)
-        k_bucket_acc_short_lds<2><<<grid, 64, 0, bulk>>>(keys, vals, range, wlo, whi, sent, bstart, bend, d_bases,
-                                                          phib, (uint32_t)n, lg, buckets, part);
+      if (lds && rec29)
+        k_bucket_acc_short_lds<2, true><<<grid, 64, 0, bulk>>>(keys, vals, range, wlo, whi, sent, bstart, bend, gb,
+                                                                nullptr, gnb, lg, buckets, part);
+      else if (lds)
+        k_bucket_acc_short_lds<2, false><<<grid, 64, 0, bulk>>>(keys, vals, range, wlo, whi, sent, bstart, bend,
+                                                                 d_bases, phib, (uint32_t)n, lg, buckets, part);
+      else if (rec29)
+        k_bucket_acc_short<F, 2, true><<<grid, 64, 0, bulk>>>(keys, vals, range, wlo, whi, sent, bstart, bend, gb,
+                                                               nullptr, gnb, lg, buckets, part);
       else
         k_bucket_acc_short<F><<<grid, 64, 0, bulk>>>(keys, vals, range, wlo, whi, sent, bstart, bend, d_bases, phib,
                                                       (uint32_t)n, lg, buckets, part);
@@ -1642,15 +1715,7 @@ __global__ void __launch_bounds__(64, 1) k_build_tables(const uint32_t* __restri
   if (j >= N) return;
   G1A p = load_affine<Fq>(bases, j);
   for (int w = 0; w < W; w++) {
-    {  // fetch_rec29 record (an infinity base stays all-zero: x = y = 0)
-      const Fq29 x = from_std(p.x), y = from_std(p.y);
-      uint32_t rec[REC29_WORDS];
-#pragma unroll
-      for (int i = 0; i < REC29_WORDS; i++) rec[i] = i < r29::N ? x.v[i] : i < 2 * r29::N ? y.v[i - r29::N] : 0u;
-      uint4* dst = reinterpret_cast<uint4*>(table + ((size_t)w * N + j) * REC29_WORDS);
-#pragma unroll
-      for (int i = 0; i < REC29_WORDS / 4; i++) dst[i] = make_uint4(rec[4 * i], rec[4 * i + 1], rec[4 * i + 2], rec[4 * i + 3]);
-    }
+    store_rec29(table, (size_t)w * N + j, p);  // an infinity base stays all-zero: x = y = 0
     if (w + 1 < W) {
       Xyzz<Fq> x = to_xyzz(p);
       for (int i = 0; i < c; i++) x = dbl(x);
