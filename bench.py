@@ -362,10 +362,11 @@ def main():
                    "parallelism": "independent MSM per rank" if world > 1 else "1 GPU"},
         "parity_ok": parity_ok,
         "latency_ms_single_call": round(latency_ms, 4),
-        "pipelining": ("consecutive tpst_g1_msm_dev calls overlap: call i's last-window-group tail (fixup, bucket "
-                       "reduction, window chain, affine output) runs on a tail stream while call i+1 sorts and "
-                       "accumulates with the other of two arenas; ms_per_step is the steady state, "
-                       "latency_ms_single_call one call synchronised alone"),
+        "pipelining": ("consecutive tpst_g1_msm_dev calls overlap on three library streams with two arenas: "
+                       "call i+1's scalar decomposition and sort run under call i's bucket accumulation, its "
+                       "accumulation under call i's last-window-group tail (fixup, bucket reduction, window chain, "
+                       "affine output); ms_per_step is the steady state, latency_ms_single_call one call "
+                       "synchronised alone"),
         "stages_ms_per_step": {k: round(v[0] / max(v[1], 1), 4) for k, v in stages.items() if v[1]},
         "roofline": {"bound": "valu-int32", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,

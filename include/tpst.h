@@ -73,7 +73,11 @@ int tpst_g1_msm(tpst_ctx* ctx, const uint64_t* bases, size_t n_bases, const uint
 int tpst_g2_msm(tpst_ctx* ctx, const uint64_t* bases, size_t n_bases, const uint64_t* scalars,
                 size_t n_scalars, uint64_t* out);
 /* device-resident form: d_bases Montgomery affine (24 u32 each), d_scalars
- * canonical Fr (8 u32 each), d_out one canonical affine G1 */
+ * canonical Fr (8 u32 each), d_out one canonical affine G1.  Pipelined:
+ * consecutive calls overlap on the library's internal streams (call i+1 sorts
+ * while call i accumulates); every call starts after the work already queued
+ * on tpst_stream, and the next call of any other entry point,
+ * tpst_synchronize and tpst_join_stream wait for it. */
 int tpst_g1_msm_dev(tpst_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, void* d_out);
 /* One MSM split over ranks (sqrt_pst.rs:198 / mipp.rs:393 at 1/2/4/8 GPUs):
  * each rank's share of the points as the raw XYZZ sum (192 B: X, Y, ZZ, ZZZ,

@@ -218,6 +218,44 @@ def test_split_msm_shares_combine(ctx, world, lg):
     assert np.array_equal(out, ref) and np.array_equal(out2, ref)
 
 
+def test_msm_dev_pipelined_calls(ctx):
+    """Back-to-back tpst_g1_msm_dev calls overlap (api.hip: call i+1's sort
+    under call i's accumulation, its accumulation under call i's tail, two
+    arenas alternating): five calls of mixed sizes -- window-grouped (tail
+    off the bulk stream), single-group, empty -- into five outputs with no
+    synchronisation in between, an entry point of another kind in the middle
+    (it must see the pending results), then one tpst_synchronize.  Each output is
+    (sum s_i k_i) G (bases k_i G)."""
+    import torch
+    n = (1 << 17) + 3
+    k, _ = orc.fr_stream(81, n)
+    dev = torch.device("cuda", 0)
+    d_k = torch.from_numpy(k.view(np.int64)).to(dev)
+    d_b = torch.empty(n * 12, dtype=torch.int64, device=dev)
+    sets = [orc.fr_stream(82 + j, n)[0] for j in range(3)]
+    d_s = [torch.from_numpy(s.view(np.int64)).to(dev) for s in sets]
+    outs = torch.zeros((6, 12), dtype=torch.int64, device=dev)
+    ctx.torch_to_lib()
+    ctx.g1_mul_generator_dev(d_k.data_ptr(), n, d_b.data_ptr())
+    calls = [(0, n), (1, 1000), (2, n), (0, 0), (1, n)]
+    for o, (j, m) in enumerate(calls):
+        ctx.g1_msm_dev(d_b.data_ptr(), d_s[j].data_ptr(), m, outs[o].data_ptr())
+        if o == 2:  # another entry point between pipelined calls
+            mid = ctx.g1_msm(orc.g1_mul_gen(k[:64]), sets[2][:64])
+    ctx.g1_msm_dev(d_b.data_ptr(), d_s[2].data_ptr(), n, outs[5].data_ptr())
+    ctx.synchronize()  # waits for the pending pipelined calls, not only the context stream
+    got = outs.cpu().numpy().view(np.uint64)
+    ki = [limbs_to_int(r) for r in k]
+
+    def ref(j, m):
+        si = [limbs_to_int(r) for r in sets[j][:m]]
+        return orc.g1_mul_gen(fr_array([sum(a * b for a, b in zip(si, ki)) % O.R]))[0]
+
+    for o, (j, m) in enumerate(calls + [(2, n)]):
+        assert np.array_equal(got[o], ref(j, m)), (o, j, m)
+    assert np.array_equal(mid, orc.g1_msm(orc.g1_mul_gen(k[:64]), sets[2][:64]))
+
+
 def test_xyzz_sum_rejects_misaligned_shares(ctx):
     """k_xyzz_sum reads shares with 16-byte loads: a share pointer or stride
     that is not 16-byte aligned is an argument error, not a misread."""

@@ -79,6 +79,7 @@ extern "C" void tpst_destroy(tpst_ctx* ctx) {
     (void)hipStreamDestroy(ctx->msm_tail);
   }
   for (int i = 0; i < 2; i++) {
+    if (ctx->msm_in[i]) (void)hipEventDestroy(ctx->msm_in[i]);
     if (ctx->msm_done[i]) (void)hipEventDestroy(ctx->msm_done[i]);
     if (ctx->msm_out[i]) (void)hipFree(ctx->msm_out[i]);
     ctx->arena_msm[i].release();
@@ -98,6 +99,8 @@ extern "C" void* tpst_stream(tpst_ctx* ctx) { return ctx ? (void*)ctx->stream : 
 
 extern "C" int tpst_synchronize(tpst_ctx* ctx) {
   if (!ctx) return TPST_E_ARG;
+  std::lock_guard<tpst::CtxMutex> lk(ctx->mu);  // the stream waits for pending pipelined MSMs
+  TPST_HIP(ctx, hipSetDevice(ctx->device));
   TPST_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return TPST_OK;
 }
@@ -226,14 +229,16 @@ extern "C" int tpst_g2_msm_fixed(tpst_ctx* ctx, const uint64_t* bases, size_t n,
   return msm_fixed_host<Fq2>(ctx, bases, n, scalars, L, D, out);
 }
 
-// Pipelined: consecutive calls overlap.  Call i's latency-bound tail (the
-// last window group's fixup, bucket reduction and window chain, and the
-// affine output; ~0.7 ms of a few waves at 2^20) runs on ctx->msm_tail, and
-// call i+1 starts its decomposition, sort and accumulation on ctx->stream
-// with the other of two arenas at once.  Stream order is kept for the
-// caller: the next entry point of any other kind (and tpst_synchronize /
-// tpst_join_stream) first waits for the pending tails (CtxMutex::lock), and
-// a call reusing an arena waits for the tail that last used it.
+// Pipelined: consecutive calls overlap.  Call i decomposes and sorts its
+// scalars on ctx->side[0], accumulates on ctx->side[1] and runs its
+// latency-bound tail (the last window group's fixup, bucket reduction and
+// window chain, and the affine output; ~0.7 ms of a few waves at 2^20) on
+// ctx->msm_tail, with one of two arenas: call i+1's sort runs under call i's
+// accumulation, its accumulation under call i's tail.  Stream order is kept
+// for the caller: each call starts after the work already on ctx->stream (its
+// inputs), the next entry point of any other kind (and tpst_synchronize /
+// tpst_join_stream) first waits for the pending tails (CtxMutex::lock), and a
+// call reusing an arena waits for the tail that last used it.
 extern "C" int tpst_g1_msm_dev(tpst_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, void* d_out) {
   if (!ctx || !d_out || (n && (!d_bases || !d_scalars))) return fail(ctx, TPST_E_ARG, "null argument");
   if (n > MSM_MAX_POINTS) return fail(ctx, TPST_E_ARG, "MSM longer than 2^27 points: split it");
@@ -242,8 +247,11 @@ extern "C" int tpst_g1_msm_dev(tpst_ctx* ctx, const void* d_bases, const void* d
   if (!ctx->msm_tail) {
     int least = 0, greatest = 0;
     TPST_HIP(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
+    for (int i = 0; i < 2; i++)  // as pst_api.hip open_streams creates them
+      if (!ctx->side[i]) TPST_HIP(ctx, hipStreamCreateWithPriority(&ctx->side[i], hipStreamNonBlocking, least));
     TPST_HIP(ctx, hipStreamCreateWithPriority(&ctx->msm_tail, hipStreamNonBlocking, greatest));
     for (int i = 0; i < 2; i++) {
+      TPST_HIP(ctx, hipEventCreateWithFlags(&ctx->msm_in[i], hipEventDisableTiming));
       TPST_HIP(ctx, hipEventCreateWithFlags(&ctx->msm_done[i], hipEventDisableTiming));
       TPST_HIP(ctx, hipMalloc(&ctx->msm_out[i], sizeof(Xyzz<Fq>)));
     }
@@ -251,13 +259,18 @@ extern "C" int tpst_g1_msm_dev(tpst_ctx* ctx, const void* d_bases, const void* d
   const int k = ctx->msm_slot;
   ctx->msm_slot ^= 1;
   Arena& ar = ctx->arena_msm[k];
-  // the tail that last used this arena (its buckets, bounds, output slot)
-  if (ctx->msm_done_set[k]) TPST_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->msm_done[k], 0));
+  // the caller's inputs, and the tail that last used this arena (its
+  // buckets, bounds, output slot)
+  TPST_HIP(ctx, hipEventRecord(ctx->msm_in[k], ctx->stream));
+  const hipStream_t front = ctx->side[0], bulk = ctx->side[1];
+  TPST_HIP(ctx, hipStreamWaitEvent(front, ctx->msm_in[k], 0));
+  if (ctx->msm_done_set[k]) TPST_HIP(ctx, hipStreamWaitEvent(front, ctx->msm_done[k], 0));
   bool on_tail = false;
   Xyzz<Fq>* d_r = (Xyzz<Fq>*)ctx->msm_out[k];
-  TPST_HIP(ctx, msm_var<Fq>(ar, ctx->stream, (const uint32_t*)d_bases, (const uint32_t*)d_scalars, n, d_r,
-                            ctx->msm_tail, &on_tail));
-  hipStream_t t = on_tail ? ctx->msm_tail : ctx->stream;
+  TPST_HIP(ctx, hipStreamWaitEvent(bulk, ctx->msm_in[k], 0));  // n = 0: no front work
+  TPST_HIP(ctx, msm_var<Fq>(ar, bulk, (const uint32_t*)d_bases, (const uint32_t*)d_scalars, n, d_r, ctx->msm_tail,
+                            &on_tail, front));
+  hipStream_t t = on_tail ? ctx->msm_tail : bulk;
   TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(t, d_r, (uint32_t*)d_out, 1));
   TPST_HIP(ctx, hipEventRecord(ctx->msm_done[k], t));
   ctx->msm_done_set[k] = true;

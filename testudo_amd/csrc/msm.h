@@ -92,9 +92,13 @@ int msm_window_bits(size_t n);
 // (the latency-bound tail) may run on `tail` instead of s -- then *on_tail is
 // set and d_out is final in `tail`'s order (s is free for the next call's
 // decomposition and accumulation; the caller keeps the arena until then).
+// front != nullptr: the scalar decomposition and the sort run on `front`
+// (ordered before s's accumulation by an event) -- so a pipelining caller's
+// next call sorts while this one accumulates.
 template <class F>
 hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint32_t* d_scalars,
-                   size_t n, Xyzz<F>* d_out, hipStream_t tail = nullptr, bool* on_tail = nullptr);
+                   size_t n, Xyzz<F>* d_out, hipStream_t tail = nullptr, bool* on_tail = nullptr,
+                   hipStream_t front = nullptr);
 
 // Fixed-base tables for K1: T[w][j] = 2^(c w) * B_j (affine, Montgomery).
 struct BatchTables {

@@ -1377,7 +1377,7 @@ static void msm_group_bounds(int W, int NG, int* wb) {
 
 template <class F>
 hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint32_t* d_scalars, size_t n,
-                   Xyzz<F>* d_out, hipStream_t tail, bool* on_tail) {
+                   Xyzz<F>* d_out, hipStream_t tail, bool* on_tail, hipStream_t front) {
   if (on_tail) *on_tail = false;
   if (n == 0) {
     Xyzz<F> inf = Xyzz<F>::inf();
@@ -1457,17 +1457,18 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   Profiler* pf = ar.prof;
   Profiler dummy;
   if (!pf) pf = &dummy;
-  pf->begin(ST_DECOMPOSE, s);
-  if (short_chunks) TPST_TRY(hipMemsetAsync(lcnt, 0, NG * sizeof(uint32_t), s));
-  k_decompose_hist<F><<<sp.ntile, SORT_THREADS, sp.nbins * 4, s>>>(d_scalars, n, c, W, glv ? 1 : 0, sent, sp.lo,
+  const hipStream_t fs = front ? front : s;
+  pf->begin(ST_DECOMPOSE, fs);
+  if (short_chunks) TPST_TRY(hipMemsetAsync(lcnt, 0, NG * sizeof(uint32_t), fs));
+  k_decompose_hist<F><<<sp.ntile, SORT_THREADS, sp.nbins * 4, fs>>>(d_scalars, n, c, W, glv ? 1 : 0, sent, sp.lo,
                                                                   sp.nbins, sp.tile, keys, vals, tab, d_bases, phib,
                                                                   rec);
   TPST_TRY(hipGetLastError());
-  pf->end(ST_DECOMPOSE, s);
-  pf->begin(ST_SORT, s);
-  k_sort_colscan<<<grid_for(sp.nbins, 64), 1024, 0, s>>>(tab, sp.ntile, sp.nbins, btot);
+  pf->end(ST_DECOMPOSE, fs);
+  pf->begin(ST_SORT, fs);
+  k_sort_colscan<<<grid_for(sp.nbins, 64), 1024, 0, fs>>>(tab, sp.ntile, sp.nbins, btot);
   TPST_TRY(hipGetLastError());
-  k_sort_binscan<<<1, 1024, 0, s>>>(btot, sp.nbins, bin0);
+  k_sort_binscan<<<1, 1024, 0, fs>>>(btot, sp.nbins, bin0);
   TPST_TRY(hipGetLastError());
   const int halves = glv ? 2 : 1;
   const uint32_t bpw = nb >> sp.lo;
@@ -1476,22 +1477,27 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   const int E = scat_lds(4) <= 60 * 1024 ? 4 : (scat_lds(2) <= 60 * 1024 ? 2 : 0);
   if (sp.lo <= c - 1 && E) {  // bins aligned to windows, stage fits
     if (E == 4)
-      k_sort_scatter_win<4><<<sp.ntile, SORT_THREADS, scat_lds(4), s>>>(keys, vals, n, halves, W, sent, sp.lo,
+      k_sort_scatter_win<4><<<sp.ntile, SORT_THREADS, scat_lds(4), fs>>>(keys, vals, n, halves, W, sent, sp.lo,
                                                                        sp.nbins, bpw, sp.tile, tab, bin0, keys2, vals2);
     else
-      k_sort_scatter_win<2><<<sp.ntile, SORT_THREADS, scat_lds(2), s>>>(keys, vals, n, halves, W, sent, sp.lo,
+      k_sort_scatter_win<2><<<sp.ntile, SORT_THREADS, scat_lds(2), fs>>>(keys, vals, n, halves, W, sent, sp.lo,
                                                                        sp.nbins, bpw, sp.tile, tab, bin0, keys2, vals2);
   } else {
-    k_sort_scatter<<<sp.ntile, SORT_THREADS, sp.nbins * 4, s>>>(keys, vals, n, (uint32_t)(halves * W), sp.lo,
+    k_sort_scatter<<<sp.ntile, SORT_THREADS, sp.nbins * 4, fs>>>(keys, vals, n, (uint32_t)(halves * W), sp.lo,
                                                                 sp.nbins, sp.tile, tab, bin0, keys2, vals2);
   }
   TPST_TRY(hipGetLastError());
   // sorted entries back into keys / vals; bucket bounds, empty buckets, range
-  k_sort_bin<<<sp.nbins, SORTB_THREADS, (2u << sp.lo) * 4 + SORTB_CAP * 4, s>>>(
+  k_sort_bin<<<sp.nbins, SORTB_THREADS, (2u << sp.lo) * 4 + SORTB_CAP * 4, fs>>>(
       keys2, vals2, bin0, sp.lo, sent, nb, W, keys, vals, bstart, bend, reinterpret_cast<uint4*>(buckets),
       (uint32_t)(sizeof(Xyzz<F>) / 16), range);
   TPST_TRY(hipGetLastError());
-  pf->end(ST_SORT, s);
+  pf->end(ST_SORT, fs);
+  if (fs != s) {  // the accumulation waits for the sort
+    TPST_TRY(ar.aux_init());
+    TPST_TRY(hipEventRecord(ar.aux_ev[Arena::N_AUX_EV - 1], fs));
+    TPST_TRY(hipStreamWaitEvent(s, ar.aux_ev[Arena::N_AUX_EV - 1], 0));
+  }
   if (!short_chunks) {  // one launch, long chunks (more than ~2^21 points)
     pf->begin(ST_BUCKET_ACC, s);
     bool done = false;
@@ -2027,14 +2033,14 @@ hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint3
 
 // explicit instantiations (G1)
 template hipError_t msm_var<Fq>(Arena&, hipStream_t, const uint32_t*, const uint32_t*, size_t, Xyzz<Fq>*, hipStream_t,
-                                bool*);
+                                bool*, hipStream_t);
 template hipError_t points_to_mont<Fq>(hipStream_t, const uint32_t*, uint32_t*, size_t);
 template hipError_t affine_from_mont<Fq>(hipStream_t, const uint32_t*, uint32_t*, size_t);
 template hipError_t xyzz_to_affine_canonical<Fq>(hipStream_t, const Xyzz<Fq>*, uint32_t*, size_t);
 #else
 // explicit instantiations (G2)
 template hipError_t msm_var<Fq2>(Arena&, hipStream_t, const uint32_t*, const uint32_t*, size_t, Xyzz<Fq2>*,
-                                 hipStream_t, bool*);
+                                 hipStream_t, bool*, hipStream_t);
 template hipError_t points_to_mont<Fq2>(hipStream_t, const uint32_t*, uint32_t*, size_t);
 template hipError_t affine_from_mont<Fq2>(hipStream_t, const uint32_t*, uint32_t*, size_t);
 template hipError_t xyzz_to_affine_canonical<Fq2>(hipStream_t, const Xyzz<Fq2>*, uint32_t*, size_t);

@@ -8,8 +8,10 @@ compiler's occupancy (waves per SIMD) and LDS bytes per workgroup.
   python tools/kernel_resources.py [--out profiles/r05/kernel_resources.txt]
                                    [--only msm.hip,...] [--check]
 
---check exits non-zero when a kernel listed in HOT has spills or scratch
-(the accumulation / fixup / reduction kernels of the MSMs and the commit).
+--check exits non-zero when a kernel listed in HOT has VGPR spills or private
+scratch (the accumulation / fixup / reduction kernels of the MSMs and the
+commit).  SGPR spills are listed apart: they go to VGPR lanes
+(v_writelane / v_readlane), no memory.
 CPU only: cross-compiles, needs no GPU.
 """
 from __future__ import annotations
@@ -30,8 +32,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # accumulations of the variable-base MSM (K2) and of the commit (K1), their
 # fixups and the bucket reductions
 HOT = [
-    "k_bucket_acc_short<Fp<FqCfg>, 2>",
-    "k_bucket_acc_chunk<Fp<FqCfg>, 2>",
+    "k_bucket_acc_short<Fp<FqCfg>, 2, true>",
+    "k_bucket_acc_short_lds<2, true>",
+    "k_bucket_acc_chunk<Fp<FqCfg>, 2, true>",
     "k_bucket_fixup_short<Fp<FqCfg> >",
     "k_bucket_fixup_quad<Fp<FqCfg> >",
     "k_bucket_fixup_long<Fp<FqCfg> >",
@@ -107,20 +110,25 @@ def main() -> int:
     hdr = "%-14s %-72s %5s %4s %5s %6s %6s %7s %4s %7s" % (
         "file", "kernel", "vgpr", "agpr", "sgpr", "vspill", "sspill", "scratch", "occ", "lds")
     lines = [hdr, "-" * len(hdr)]
-    bad = []
+    bad, lanes = [], []
     for r in rows:
         k = short(r["name"])
         lines.append("%-14s %-72s %5s %4s %5s %6s %6s %7s %4s %7s" % (
             r["file"], k[:72], r.get("vgpr"), r.get("agpr"), r.get("sgpr"), r.get("vspill"), r.get("sspill"),
             r.get("scratch"), r.get("occ"), r.get("lds")))
-        if k in HOT and (r.get("vspill") or r.get("sspill") or r.get("scratch")):
+        if k in HOT and (r.get("vspill") or r.get("scratch")):
             bad.append(k)
+        elif k in HOT and r.get("sspill"):
+            lanes.append("%s (%s)" % (k, r.get("sspill")))
     text = "\n".join(lines) + "\n"
     seen = {short(r["name"]) for r in rows}
     missing = [h for h in HOT if h not in seen] if not a.only or "msm.hip" in a.only else []
     if missing:
         text += "\nHOT kernels not found (renamed?):\n" + "\n".join("  " + m for m in missing) + "\n"
         bad += missing
+    if lanes:
+        text += ("\nHOT kernels with SGPR spills (to VGPR lanes: v_writelane / v_readlane, no scratch memory):\n" +
+                 "\n".join("  " + b for b in lanes) + "\n")
     if bad:
         text += "\nHOT kernels with spills or scratch:\n" + "\n".join("  " + b for b in bad) + "\n"
     else:
