@@ -362,7 +362,7 @@ def main():
                    "parallelism": "independent MSM per rank" if world > 1 else "1 GPU"},
         "parity_ok": parity_ok,
         "latency_ms_single_call": round(latency_ms, 4),
-        "pipelining": ("consecutive tpst_g1_msm_dev calls overlap on three library streams with two arenas: "
+        "pipelining": ("consecutive tpst_g1_msm_dev calls overlap on three library streams with three arenas: "
                        "call i+1's scalar decomposition and sort run under call i's bucket accumulation, its "
                        "accumulation under call i's last-window-group tail (fixup, bucket reduction, window chain, "
                        "affine output); ms_per_step is the steady state, latency_ms_single_call one call "

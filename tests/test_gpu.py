@@ -220,8 +220,8 @@ def test_split_msm_shares_combine(ctx, world, lg):
 
 def test_msm_dev_pipelined_calls(ctx):
     """Back-to-back tpst_g1_msm_dev calls overlap (api.hip: call i+1's sort
-    under call i's accumulation, its accumulation under call i's tail, two
-    arenas alternating): five calls of mixed sizes -- window-grouped (tail
+    under call i's accumulation, its accumulation under call i's tail, three
+    arenas in turn): five calls of mixed sizes -- window-grouped (tail
     off the bulk stream), single-group, empty -- into five outputs with no
     synchronisation in between, an entry point of another kind in the middle
     (it must see the pending results), then one tpst_synchronize.  Each output is

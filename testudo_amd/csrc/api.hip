@@ -40,8 +40,10 @@ extern "C" int tpst_create(int device, tpst_ctx** out) {
   tpst_ctx* c = new tpst_ctx();
   c->device = device;
   c->arena.prof = &c->prof;
-  c->arena_msm[0].prof = c->arena_msm[1].prof = &c->prof;
-  c->arena_msm[1].aux_from = &c->arena_msm[0];  // one pair of aux streams
+  for (int i = 0; i < tpst_ctx::MSM_SLOTS; i++) {
+    c->arena_msm[i].prof = &c->prof;
+    if (i) c->arena_msm[i].aux_from = &c->arena_msm[0];  // one pair of aux streams
+  }
   c->mu.stream = &c->stream;
   // the library stream carries every critical path (the opening's transcript
   // chain in particular); the opening's side streams (pst_api.hip) are
@@ -78,7 +80,7 @@ extern "C" void tpst_destroy(tpst_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->msm_tail);
     (void)hipStreamDestroy(ctx->msm_tail);
   }
-  for (int i = 0; i < 2; i++) {
+  for (int i = 0; i < tpst_ctx::MSM_SLOTS; i++) {
     if (ctx->msm_in[i]) (void)hipEventDestroy(ctx->msm_in[i]);
     if (ctx->msm_done[i]) (void)hipEventDestroy(ctx->msm_done[i]);
     if (ctx->msm_out[i]) (void)hipFree(ctx->msm_out[i]);
@@ -233,8 +235,10 @@ extern "C" int tpst_g2_msm_fixed(tpst_ctx* ctx, const uint64_t* bases, size_t n,
 // scalars on ctx->side[0], accumulates on ctx->side[1] and runs its
 // latency-bound tail (the last window group's fixup, bucket reduction and
 // window chain, and the affine output; ~0.7 ms of a few waves at 2^20) on
-// ctx->msm_tail, with one of two arenas: call i+1's sort runs under call i's
-// accumulation, its accumulation under call i's tail.  Stream order is kept
+// ctx->msm_tail, with one of three arenas: call i+1's sort runs under call
+// i's accumulation, its accumulation under call i's tail (with two arenas the
+// sort of call i+1 waited for call i-1's tail, itself stretched by call i's
+// accumulation: 0.85 ms idle between accumulations, profiles/r05/f).  Stream order is kept
 // for the caller: each call starts after the work already on ctx->stream (its
 // inputs), the next entry point of any other kind (and tpst_synchronize /
 // tpst_join_stream) first waits for the pending tails (CtxMutex::lock), and a
@@ -250,14 +254,14 @@ extern "C" int tpst_g1_msm_dev(tpst_ctx* ctx, const void* d_bases, const void* d
     for (int i = 0; i < 2; i++)  // as pst_api.hip open_streams creates them
       if (!ctx->side[i]) TPST_HIP(ctx, hipStreamCreateWithPriority(&ctx->side[i], hipStreamNonBlocking, least));
     TPST_HIP(ctx, hipStreamCreateWithPriority(&ctx->msm_tail, hipStreamNonBlocking, greatest));
-    for (int i = 0; i < 2; i++) {
+    for (int i = 0; i < tpst_ctx::MSM_SLOTS; i++) {
       TPST_HIP(ctx, hipEventCreateWithFlags(&ctx->msm_in[i], hipEventDisableTiming));
       TPST_HIP(ctx, hipEventCreateWithFlags(&ctx->msm_done[i], hipEventDisableTiming));
       TPST_HIP(ctx, hipMalloc(&ctx->msm_out[i], sizeof(Xyzz<Fq>)));
     }
   }
   const int k = ctx->msm_slot;
-  ctx->msm_slot ^= 1;
+  ctx->msm_slot = (k + 1) % tpst_ctx::MSM_SLOTS;
   Arena& ar = ctx->arena_msm[k];
   // the caller's inputs, and the tail that last used this arena (its
   // buckets, bounds, output slot)

@@ -37,18 +37,19 @@ struct tpst_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   tpst::CtxMutex mu;
-  // pipelined device MSMs (tpst_g1_msm_dev): two arenas used alternately;
+  // pipelined device MSMs (tpst_g1_msm_dev): three arenas used in turn;
   // call i+1 decomposes and sorts on side[0] while call i accumulates on
   // side[1], and call i's latency-bound tail (last window group's fixup,
   // reduction, window chain, affine output) runs on msm_tail.  (The side
   // streams are shared with the opening: two more streams of their own cost
   // the commit's IPP 0.7 ms at 2^20 -- more HIP streams than hardware queues.)
-  tpst::Arena arena_msm[2];
+  static constexpr int MSM_SLOTS = 3;  // call i+1's sort must not wait for call i-1's tail
+  tpst::Arena arena_msm[MSM_SLOTS];
   hipStream_t msm_tail = nullptr;
-  hipEvent_t msm_in[2] = {nullptr, nullptr};  // the caller's inputs ready (on `stream`)
-  hipEvent_t msm_done[2] = {nullptr, nullptr};
-  void* msm_out[2] = {nullptr, nullptr};  // each slot's XYZZ result
-  bool msm_done_set[2] = {false, false};
+  hipEvent_t msm_in[MSM_SLOTS] = {};  // the caller's inputs ready (on `stream`)
+  hipEvent_t msm_done[MSM_SLOTS] = {};
+  void* msm_out[MSM_SLOTS] = {};  // each slot's XYZZ result
+  bool msm_done_set[MSM_SLOTS] = {};
   int msm_slot = 0;
   std::string err;
   tpst::Arena arena;   // kernel scratch (reset per primitive)

@@ -108,9 +108,13 @@ __device__ __forceinline__ void set_wave_prio(int prio) {
 //    infinity) the buckets without entries and the window starts range[w].
 // Entries of one bucket land in an unspecified order: the bucket sum is a
 // group element, so the MSM result does not depend on it.
-constexpr int SORT_THREADS = 1024;                   // decomposition / scatter workgroup
+// Workgroups of at most 256 threads (one wave per SIMD of a CU): a pipelined
+// caller's next MSM decomposes and sorts while this one accumulates, and the
+// accumulation's 2 waves per SIMD at ~200 VGPRs leave room for one more wave
+// of <= 104 VGPRs per SIMD -- a wider workgroup waits for a whole CU to drain.
+constexpr int SORT_THREADS = 256;                    // decomposition / scatter workgroup
 constexpr uint32_t SORT_MAX_BINS = 16384;            // LDS histogram of a tile
-constexpr int SORTB_THREADS = 512;                   // bin-sort workgroup
+constexpr int SORTB_THREADS = 256;                   // bin-sort workgroup
 constexpr int SORTB_IT = 24;                         // entries per thread kept in registers
 constexpr int SORTB_CAP = SORTB_THREADS * SORTB_IT;  // largest bin sorted in LDS
 constexpr int SORTB_LO_MAX = 10;  // bin-sort LDS: 2^(lo+3) + 4 SORTB_CAP bytes <= 64 KB
@@ -230,14 +234,15 @@ static __global__ void __launch_bounds__(SORT_THREADS)
 }
 
 // per bin: exclusive scan of the tiles' counts (in place: tab[t][bin] becomes
-// tile t's first slot inside the bin) and the bin total.  64 bins x 16 tile
-// chunks per workgroup.
-static __global__ void __launch_bounds__(1024) k_sort_colscan(uint32_t* __restrict__ tab, uint32_t ntile,
-                                                              uint32_t nbins, uint32_t* __restrict__ tot) {
-  __shared__ uint32_t part[16][64];
+// tile t's first slot inside the bin) and the bin total.  64 bins x
+// COLSCAN_CH tile chunks per workgroup.
+constexpr int COLSCAN_CH = 4;
+static __global__ void __launch_bounds__(64 * COLSCAN_CH) k_sort_colscan(uint32_t* __restrict__ tab, uint32_t ntile,
+                                                                         uint32_t nbins, uint32_t* __restrict__ tot) {
+  __shared__ uint32_t part[COLSCAN_CH][64];
   const uint32_t lane = threadIdx.x & 63, ch = threadIdx.x >> 6;
   const uint32_t bin = blockIdx.x * 64 + lane;
-  const uint32_t per = (ntile + 15) / 16;
+  const uint32_t per = (ntile + COLSCAN_CH - 1) / COLSCAN_CH;
   const uint32_t t0 = (ch * per < ntile) ? ch * per : ntile;
   const uint32_t t1 = (t0 + per < ntile) ? t0 + per : ntile;
   uint32_t sum = 0;
@@ -247,7 +252,7 @@ static __global__ void __launch_bounds__(1024) k_sort_colscan(uint32_t* __restri
   __syncthreads();
   if (ch == 0) {
     uint32_t acc = 0;
-    for (int k = 0; k < 16; k++) {
+    for (int k = 0; k < COLSCAN_CH; k++) {
       const uint32_t v = part[k][lane];
       part[k][lane] = acc;
       acc += v;
@@ -267,18 +272,19 @@ static __global__ void __launch_bounds__(1024) k_sort_colscan(uint32_t* __restri
 }
 
 // start[b] = sum of the totals of bins < b, start[nbins] = entry count (one workgroup)
-static __global__ void __launch_bounds__(1024) k_sort_binscan(const uint32_t* __restrict__ tot, uint32_t nbins,
-                                                              uint32_t* __restrict__ start) {
-  __shared__ uint32_t ws[1024];
+constexpr int BINSCAN_THREADS = 256;
+static __global__ void __launch_bounds__(BINSCAN_THREADS) k_sort_binscan(const uint32_t* __restrict__ tot,
+                                                                         uint32_t nbins, uint32_t* __restrict__ start) {
+  __shared__ uint32_t ws[BINSCAN_THREADS];
   const uint32_t t = threadIdx.x;
-  const uint32_t per = (nbins + 1023) / 1024;
+  const uint32_t per = (nbins + BINSCAN_THREADS - 1) / BINSCAN_THREADS;
   const uint32_t b0 = t * per;
   uint32_t sum = 0;
   for (uint32_t k = 0; k < per; k++)
     if (b0 + k < nbins) sum += tot[b0 + k];
   ws[t] = sum;
   __syncthreads();
-  for (uint32_t off = 1; off < 1024; off <<= 1) {
+  for (uint32_t off = 1; off < BINSCAN_THREADS; off <<= 1) {
     const uint32_t v = t >= off ? ws[t - off] : 0u;
     __syncthreads();
     ws[t] += v;
@@ -290,7 +296,7 @@ static __global__ void __launch_bounds__(1024) k_sort_binscan(const uint32_t* __
       start[b0 + k] = acc;
       acc += tot[b0 + k];
     }
-  if (t == 1023) start[nbins] = ws[1023];
+  if (t == BINSCAN_THREADS - 1) start[nbins] = ws[BINSCAN_THREADS - 1];
 }
 
 // tile -> bins: each entry takes the next slot of its bin from the tile's
@@ -1466,9 +1472,9 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   TPST_TRY(hipGetLastError());
   pf->end(ST_DECOMPOSE, fs);
   pf->begin(ST_SORT, fs);
-  k_sort_colscan<<<grid_for(sp.nbins, 64), 1024, 0, fs>>>(tab, sp.ntile, sp.nbins, btot);
+  k_sort_colscan<<<grid_for(sp.nbins, 64), 64 * COLSCAN_CH, 0, fs>>>(tab, sp.ntile, sp.nbins, btot);
   TPST_TRY(hipGetLastError());
-  k_sort_binscan<<<1, 1024, 0, fs>>>(btot, sp.nbins, bin0);
+  k_sort_binscan<<<1, BINSCAN_THREADS, 0, fs>>>(btot, sp.nbins, bin0);
   TPST_TRY(hipGetLastError());
   const int halves = glv ? 2 : 1;
   const uint32_t bpw = nb >> sp.lo;
