@@ -1,7 +1,8 @@
 // Host check of field29.h (radix-2^29 Fq, R = 2^377) against Python integers
 // (tests/test_field29.py): per input line "a b" (field.h Montgomery words,
 // 12 x u32 hex, possibly unreduced below 64 p) print
-//   mul, sqr, add, sub, to_std(from_std(a)), inv(a)        for reduced a, b
+//   mul, sqr, add, sub, to_std(from_std(a)), inv(a),
+//   mul_sum(a, b, a, a) = ab + a^2, mul_sub(a, b, b, b) = ab - b^2  for reduced a, b
 //   the wave engine's stage product / square               for wide a, b
 #include <cstdio>
 #include <cstring>
@@ -38,6 +39,8 @@ int main() {
       put(to_std(sub(x, y)));
       put(to_std(x));
       put(inv(a));
+      put(to_std(mul_sum(x, y, x, x)));
+      put(to_std(mul_sub(x, y, y, y)));
     }
   }
   return 0;

@@ -66,6 +66,12 @@ TPST_NI bool on_curve(const Affine<F>& a) {
 }
 
 // --------------------------------------------------------------- XYZZ ----
+// a b - c d; field29.h overloads it for Fq29 with one Montgomery reduction
+template <class F>
+TPST_HD F mul_sub(const F& a, const F& b, const F& c, const F& d) {
+  return sub(mul(a, b), mul(c, d));
+}
+
 // dbl-2008-s-1 (a = 0)
 template <class F>
 TPST_HD Xyzz<F> dbl(const Xyzz<F>& p) {
@@ -77,7 +83,7 @@ TPST_HD Xyzz<F> dbl(const Xyzz<F>& p) {
   const F M = mul3(sqr(p.X));
   Xyzz<F> r;
   r.X = sub(sqr(M), dbl(S));
-  r.Y = sub(mul(M, sub(S, r.X)), mul(W, p.Y));
+  r.Y = mul_sub(M, sub(S, r.X), W, p.Y);
   r.ZZ = mul(V, p.ZZ);
   r.ZZZ = mul(W, p.ZZZ);
   return r;
@@ -94,7 +100,7 @@ TPST_HD Xyzz<F> dbl_affine(const Affine<F>& q) {
   const F M = mul3(sqr(q.x));
   Xyzz<F> r;
   r.X = sub(sqr(M), dbl(S));
-  r.Y = sub(mul(M, sub(S, r.X)), mul(W, q.y));
+  r.Y = mul_sub(M, sub(S, r.X), W, q.y);
   r.ZZ = V;
   r.ZZZ = W;
   return r;
@@ -118,7 +124,7 @@ TPST_HD Xyzz<F> add_affine(const Xyzz<F>& p, const Affine<F>& q) {
   const F Q = mul(p.X, PP);
   Xyzz<F> r;
   r.X = sub(sub(sqr(R), PPP), dbl(Q));
-  r.Y = sub(mul(R, sub(Q, r.X)), mul(p.Y, PPP));
+  r.Y = mul_sub(R, sub(Q, r.X), p.Y, PPP);
   r.ZZ = mul(p.ZZ, PP);
   r.ZZZ = mul(p.ZZZ, PPP);
   return r;
@@ -147,7 +153,7 @@ TPST_HD Xyzz<F> add(const Xyzz<F>& p, const Xyzz<F>& q) {
   const F Q = mul(U1, PP);
   Xyzz<F> r;
   r.X = sub(sub(sqr(R), PPP), dbl(Q));
-  r.Y = sub(mul(R, sub(Q, r.X)), mul(S1, PPP));
+  r.Y = mul_sub(R, sub(Q, r.X), S1, PPP);
   r.ZZ = mul(mul(p.ZZ, q.ZZ), PP);
   r.ZZZ = mul(mul(p.ZZZ, q.ZZZ), PPP);
   return r;

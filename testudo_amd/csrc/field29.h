@@ -75,17 +75,20 @@ TPST_HD bool eq(const Fq29& a, const Fq29& b) {
   return acc == 0;
 }
 
-// t - p if t >= p (t < 2p, limbs normalised except the top one, < 2^30)
+// t - p if t >= p (limbs normalised except the top one, < 2^30; the top
+// limb of t - p is kept whole, so t < 2.7 p takes two calls)
 TPST_HD void reduce_once(Fq29& t) {
   uint32_t s[r29::N];
   int32_t br = 0;
 #pragma unroll
-  for (int i = 0; i < r29::N; i++) {
+  for (int i = 0; i < r29::N - 1; i++) {
     const int32_t d = (int32_t)t.v[i] - (int32_t)r29::P[i] + br;
     s[i] = (uint32_t)d & r29::M;
     br = d >> 29;  // 0 or -1
   }
-  const bool take = br == 0;
+  const int32_t dt = (int32_t)t.v[r29::N - 1] - (int32_t)r29::P[r29::N - 1] + br;
+  s[r29::N - 1] = (uint32_t)dt;
+  const bool take = dt >= 0;
 #pragma unroll
   for (int i = 0; i < r29::N; i++) t.v[i] = take ? s[i] : t.v[i];
 }
@@ -167,6 +170,48 @@ TPST_HD Fq29 mul(const Fq29& a, const Fq29& b) {
   reduce_once(r);
   return r;
 }
+
+// a b + c d (Montgomery) with ONE reduction for both products: column k
+// gathers the a_i b_j, the c_i d_j and the m_i p_j (<= 38 terms < 2^58, with
+// the carry < 2^64); canonical inputs (< p) only -- the sum is < (2 p^2 +
+// R p) / R < 2.7 p, so two conditional subtractions.  A point addition's
+// Y3 = R (Q - X3) - S PPP is one such sum (with p - PPP): one Montgomery
+// reduction (156 multiply-adds) fewer per mixed add.
+TPST_HD Fq29 mul_sum(const Fq29& a, const Fq29& b, const Fq29& c, const Fq29& d) {
+  constexpr int N = r29::N;
+  uint32_t m[N], t[N];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; k++) {
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < N) acc += (uint64_t)a.v[i] * b.v[j] + (uint64_t)c.v[i] * d.v[j];
+    }
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      const int j = k - i;
+      if (i < k && j >= 1 && j < N) acc += (uint64_t)m[i] * r29::P[j];
+    }
+    if (k < N) {
+      m[k] = (0u - (uint32_t)acc) & r29::M;
+      acc += m[k];
+    } else {
+      t[k - N] = (uint32_t)acc & r29::M;
+    }
+    acc >>= 29;
+  }
+  t[N - 1] = (uint32_t)acc;  // < 2^31: t < 2.7 p
+  Fq29 r;
+#pragma unroll
+  for (int i = 0; i < N; i++) r.v[i] = t[i];
+  reduce_once(r);
+  reduce_once(r);
+  return r;
+}
+
+// a b - c d for canonical operands: one reduction (mul_sum with p - d)
+TPST_HD Fq29 mul_sub(const Fq29& a, const Fq29& b, const Fq29& c, const Fq29& d) { return mul_sum(a, b, c, neg(d)); }
 
 // square: cross products a_i a_j (i < j) once, doubled per column
 TPST_HD Fq29 sqr(const Fq29& a) {

@@ -1412,7 +1412,7 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   int lg;
   if (NG > 1) {  // per-group launches: keep >= 4 waves per SIMD in each
     static const size_t simds = device_simds();
-    lg = 4;
+    lg = 4;  // 16-entry chunks: 8 / 32 / 64 measured 4 / 7 / 18 % slower (profiles/r05/g)
     while (lg < 8 && ((m / NG) >> (lg + 1)) >= (size_t)4 * 64 * simds) lg++;
   } else {
     lg = acc_chunk_lg(m);
