@@ -72,9 +72,10 @@ extern "C" void tpst_destroy(tpst_ctx* ctx) {
     }
     ctx->arena_side[i].release();
   }
-  if (ctx->comm) {
-    (void)hipStreamSynchronize(ctx->comm);
-    (void)hipStreamDestroy(ctx->comm);
+  for (hipStream_t st : {ctx->comm, ctx->side_c}) {
+    if (!st) continue;
+    (void)hipStreamSynchronize(st);
+    (void)hipStreamDestroy(st);
   }
   if (ctx->msm_tail) {
     (void)hipStreamSynchronize(ctx->msm_tail);

@@ -61,6 +61,7 @@ struct tpst_ctx {
   hipStream_t side[3] = {nullptr, nullptr, nullptr};
   tpst::Arena arena_side[3];
   hipStream_t comm = nullptr;      // the row-sharded opening's all-gathers (tpst_poly_open_sharded)
+  hipStream_t side_c = nullptr;    // the opening's per-round h preparation (greatest priority)
   std::vector<hipEvent_t> events;  // timing-free event pool of the opening
   hipEvent_t ev_wait = nullptr;    // tpst_wait_stream / tpst_join_stream
   hipEvent_t ev_join = nullptr;

@@ -1123,6 +1123,9 @@ static int open_streams(tpst_ctx* ctx, size_t n_events, size_t pinned_bytes, boo
     if (!ctx->side[i]) TPST_HIP(ctx, hipStreamCreateWithPriority(&ctx->side[i], hipStreamNonBlocking, least));
   // the row-sharded opening's collectives, in one issue order on every rank
   if (comm && !ctx->comm) TPST_HIP(ctx, hipStreamCreateWithPriority(&ctx->comm, hipStreamNonBlocking, greatest));
+  // the per-round h preparation of the opening (its own hardware queue: on
+  // stream A it delayed the next round's t; 2^20 open 13.0 -> 11.4 ms)
+  if (!ctx->side_c) TPST_HIP(ctx, hipStreamCreateWithPriority(&ctx->side_c, hipStreamNonBlocking, greatest));
   while (ctx->events.size() < n_events) {
     hipEvent_t e;
     TPST_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1279,17 +1282,18 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
   const size_t n_ev = 8 + 6 * (size_t)m + (shd ? 8 * (size_t)m + 8 : 0);
   if (int rc = open_streams(ctx, n_ev, up_bytes + dn_bytes, shd)) return rc;
   uint8_t* pin = (uint8_t*)ctx->pinned;
-  // four hardware queues: A (critical), B (cross terms), and two look-ahead
-  // streams for alternating rounds -- consecutive look-aheads overlap, each
-  // taking longer than a round.  h is prepared (G2 fold + G2Prepared lines,
-  // ~1.3 ms) only at odd rounds: look-ahead r pairs E = 2^(r - s) fold sets of
-  // a^(r) against the prepared h^(s), s = r - 2 (r odd) or r - 3 (r even),
-  // s = 0 for r <= 2.  That round work "C" rides on stream A: A's own round
-  // work is two short table products, so C delays t^(r+1) by less than the
-  // cross MSMs of stream B take, whereas on B it delayed every even round's
-  // comms_u by ~1 ms; the epilogue's final h fold runs on the first
-  // look-ahead stream (idle by then), beside final_a (A) and pst_proof_h (B)
-  const hipStream_t sA = ctx->stream, sB = ctx->side[0], sC = ctx->stream;
+  // five streams: A (critical), B (cross terms), two look-ahead streams for
+  // alternating rounds (consecutive look-aheads overlap, each taking longer
+  // than a round) and C, the h preparation, at the greatest priority.  h^(r)
+  // (G2 fold + G2Prepared lines) is prepared in every round r >= 1 that a
+  // look-ahead needs: look-ahead r pairs E = 2^(r - s) fold sets of a^(r)
+  // against the prepared h^(s), s = r - 1 (prepared one round earlier: E = 2),
+  // s = 0 for r <= 1.  Preparing at odd rounds only (s = r - 2 / r - 3, E =
+  // 4 / 8) paired two to four times as many pairs; C on stream A delayed the
+  // next round's t (2^24 open 26.6 -> 25.5 ms, 2^20 13.0 -> 11.4 ms with both,
+  // profiles/r05/i).  The epilogue's final h fold runs on the first look-ahead
+  // stream (idle by then), beside final_a (A) and pst_proof_h (B)
+  const hipStream_t sA = ctx->stream, sB = ctx->side[0], sC = ctx->side_c;
   const hipStream_t sCe = ctx->side[1];
   hipStream_t sLA[2] = {ctx->side[1], ctx->side[2]};
   Arena &arA = ctx->arena, &arB = ctx->arena_side[0], &arC = ctx->arena2;
@@ -1305,7 +1309,7 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
   hipEvent_t* xev = ev + 8 + 6 * m;                         // exchange events (sharded form)
   int last_c = -1;  // the last odd round that issued h work "C"
   // the prepared h the look-ahead of round r pairs against (see above)
-  auto la_src = [](int r) { return r <= 2 ? 0 : (r & 1) ? r - 2 : r - 3; };
+  auto la_src = [](int r) { return r <= 1 ? 0 : r - 1; };
   // which odd rounds prepare h: for a look-ahead on the rank's own positions
   // (local, sharded rounds) or on every position (global)
   std::vector<char> need_loc(m + 1, 0), need_glob(m + 1, 0);
@@ -1353,8 +1357,8 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
   // ---- device buffers (allocated before any stream runs: no hipFree mid-open)
   const size_t Ch = C > 1 ? C / 2 : 1;
   const size_t Ca0 = shd ? Cl : C;  // a-side bases resident: own rows or all
-  DevBuf up, A, P, Y, chiC, ScA, ScB, ScC, ScD[2], xa, xb, xd, xh, xp, xl[2], LAo[2], Hb[2], Lb[2], gts, canA, canC,
-      canD, pstA, pstB, Wall, Wiall, SqT[2], SqG[2], SqM, chis_own, tLoc, A1x, A1, tA1, Hbl[2], Lbl[2];
+  DevBuf up, A, P, Y, chiC, ScA, ScB, ScC, ScD[2], xa, xb, xd, xh, xp, xl[2], LAo[2], Hb[3], Lb[3], gts, canA, canC,
+      canD, pstA, pstB, Wall, Wiall, SqT[2], SqG[2], SqM, chis_own, tLoc, A1x, A1, tA1, Hbl[3], Lbl[3];
   TPST_HIP(ctx, up.alloc(up_bytes));
   TPST_HIP(ctx, Wall.alloc(2 * C * 32));  // round r's 2^r fold weights at offset 2^r - 1
   TPST_HIP(ctx, Wiall.alloc(2 * C * 32));
@@ -1370,7 +1374,7 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
   TPST_HIP(ctx, xd.alloc((k + 1) * sizeof(Xyzz<Fq2>)));
   TPST_HIP(ctx, xh.alloc(C * sizeof(Xyzz<Fq2>)));
   TPST_HIP(ctx, xp.alloc(((size_t)m + 1) * sizeof(Xyzz<Fq>)));
-  for (int i = 0; i < 2; i++) {
+  for (int i = 0; i < 3; i++) {  // prepared h^(r) in slot r % 3
     TPST_HIP(ctx, Hb[i].alloc(Ch * 192));
     TPST_HIP(ctx, Lb[i].alloc(Ch * N_LINE_COEFFS * sizeof(LineCoeff)));
     if (shd) {
@@ -1404,7 +1408,7 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
     TPST_HIP(ctx, A1.alloc(len1 * 96));
     TPST_HIP(ctx, tA1.alloc(fbt_words<Fq>(len1) * 4));
   }
-  {  // G2 preparation scratch: h^(r) at odd rounds (global: <= C / 2 points, a rank's: <= C / 2W)
+  {  // G2 preparation scratch: the prepared h^(r) (global: <= C / 2 points, a rank's: <= C / 2W)
     size_t mx = 0;
     for (int r = 1; r <= m; r++) {
       if (need_glob[r]) mx = std::max(mx, C >> r);
@@ -1579,7 +1583,7 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
       TPST_HIP(ctx, fbt_msm<Fq>(arB, sB, tA, ScB.u(), g, (Xyzz<Fq>*)sl.send));
       if (int rc = gather(sB, sl, per * X1)) return rc;
       if (!lead) {  // this rank's part is done
-        for (hipStream_t s2 : {sA, sB, sLA[0], sLA[1], ctx->comm}) TPST_HIP(ctx, hipStreamSynchronize(s2));
+        for (hipStream_t s2 : {sA, sB, sLA[0], sLA[1], sC, ctx->comm}) TPST_HIP(ctx, hipStreamSynchronize(s2));
         sp.store(tr);
         return TPST_OK;
       }
@@ -1699,8 +1703,8 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
         const LineCoeff* lp = loc ? L0l : L0;
         if (src > 0) {
           TPST_HIP(ctx, hipStreamWaitEvent(sD, loc ? ev_cl(src) : ev_c(src), 0));
-          hp = (loc ? Hbl : Hb)[(src >> 1) & 1].u();
-          lp = (const LineCoeff*)(loc ? Lbl : Lb)[(src >> 1) & 1].p;
+          hp = (loc ? Hbl : Hb)[src % 3].u();
+          lp = (const LineCoeff*)(loc ? Lbl : Lb)[src % 3].p;
         }
         TPST_HIP(ctx, mipp_lookahead(arD, sD, lp, (size_t)E * ln, hp, xl[r & 1].u(), true, ln, E, la_out, !loc));
       }
@@ -1717,12 +1721,12 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
       if (int rc = pst_q()) return rc;
 
     const double hp = open_trace() ? host_us() : 0.0;
-    // -- C: h^(r) prepared at odd r for the look-aheads of rounds r+2, r+3:
-    // at this rank's positions (sharded look-aheads) and / or at all
-    const bool c_glob = shd ? (bool)need_glob[r] : ((r & 1) && r + 4 <= m);
+    // -- C: h^(r) prepared for the look-ahead of round r+1: at this rank's
+    // positions (sharded look-aheads) and / or at all
+    const bool c_glob = need_glob[r];
     if (need_loc[r] || c_glob) {
       TPST_HIP(ctx, hipStreamWaitEvent(sC, ev_up(r), 0));
-      if (r >= 5) TPST_HIP(ctx, hipStreamWaitEvent(sC, ev_la(r - 1), 0));  // last reader of h^(r-4)'s slot
+      if (r >= 3) TPST_HIP(ctx, hipStreamWaitEvent(sC, ev_la(r - 2), 0));  // last reader of h^(r-3)'s slot
     }
     if (need_loc[r]) {
       const size_t ln = len / W;
@@ -1733,8 +1737,8 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
       g.L = ln;
       g.D = 1;
       TPST_HIP(ctx, fbt_msm<Fq2>(arC, sC, tHl, ScC.u(), g, (Xyzz<Fq2>*)xh.p));
-      TPST_HIP(ctx, xyzz_to_affine_mont<Fq2>(sC, (Xyzz<Fq2>*)xh.p, Hbl[(r >> 1) & 1].u(), ln));
-      TPST_HIP(ctx, g2_prepare_batch(sC, Hbl[(r >> 1) & 1].u(), ln, (LineCoeff*)Lbl[(r >> 1) & 1].p,
+      TPST_HIP(ctx, xyzz_to_affine_mont<Fq2>(sC, (Xyzz<Fq2>*)xh.p, Hbl[r % 3].u(), ln));
+      TPST_HIP(ctx, g2_prepare_batch(sC, Hbl[r % 3].u(), ln, (LineCoeff*)Lbl[r % 3].p,
                                      st->prep_scratch.u()));
       TPST_HIP(ctx, hipEventRecord(ev_cl(r), sC));
       last_c = r;
@@ -1747,8 +1751,8 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
       g.L = len;
       g.D = 1;
       TPST_HIP(ctx, fbt_msm<Fq2>(arC, sC, tH, ScC.u(), g, (Xyzz<Fq2>*)xh.p));
-      TPST_HIP(ctx, xyzz_to_affine_mont<Fq2>(sC, (Xyzz<Fq2>*)xh.p, Hb[(r >> 1) & 1].u(), len));
-      TPST_HIP(ctx, g2_prepare_batch(sC, Hb[(r >> 1) & 1].u(), len, (LineCoeff*)Lb[(r >> 1) & 1].p,
+      TPST_HIP(ctx, xyzz_to_affine_mont<Fq2>(sC, (Xyzz<Fq2>*)xh.p, Hb[r % 3].u(), len));
+      TPST_HIP(ctx, g2_prepare_batch(sC, Hb[r % 3].u(), len, (LineCoeff*)Lb[r % 3].p,
                                      st->prep_scratch.u()));
       TPST_HIP(ctx, hipEventRecord(ev_c(r), sC));
       last_c = r;
@@ -1879,7 +1883,7 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
     pf.end(ST_MIPP_PROVE, sA);
     pf.end(ST_SQRT_OPEN, sA);
   }
-  for (hipStream_t s2 : {sA, sB, sLA[0], sLA[1]}) TPST_HIP(ctx, hipStreamSynchronize(s2));
+  for (hipStream_t s2 : {sA, sB, sLA[0], sLA[1], sC}) TPST_HIP(ctx, hipStreamSynchronize(s2));
   if (shd) TPST_HIP(ctx, hipStreamSynchronize(ctx->comm));
   xyzz_to_canonical_host<Fq>(pin + dn_final, 1, proof->final_a);
   xyzz_to_canonical_host<Fq2>(pin + dn_fh, 1, proof->final_h);
