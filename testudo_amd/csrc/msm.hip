@@ -1752,12 +1752,21 @@ void batch_tables_free(BatchTables& t) {
   t.N = 0;
 }
 
+// an empty bucket of the row MSMs = infinity (ZZ = 0): written by the sort,
+// which knows the empty ones (no memset of all buckets)
+__device__ __forceinline__ void zero_bucket(uint4* zb, size_t key) {
+  constexpr int Q = sizeof(Xyzz<Fq>) / 16;
+#pragma unroll
+  for (int i = 0; i < Q; i++) zb[key * Q + i] = make_uint4(0, 0, 0, 0);
+}
+
 // one workgroup per row: LDS counting sort of the row's N*W signed digits
 // by bucket; writes the row's entries and bucket bounds.
 __global__ void __launch_bounds__(256) k_batch_sort(const uint32_t* __restrict__ scalars, size_t rows, size_t N,
                                                     size_t row_stride, size_t col_stride, int c, int W,
                                                     uint32_t* __restrict__ keys, uint32_t* __restrict__ entries,
-                                                    uint32_t* __restrict__ bstart, uint32_t* __restrict__ bend) {
+                                                    uint32_t* __restrict__ bstart, uint32_t* __restrict__ bend,
+                                                    uint4* __restrict__ zb) {
   extern __shared__ uint32_t cnt[];  // nb counters
   // XCD-aware: consecutive rows on the same XCD (blocks b, b+8, ... share one)
   const size_t nblk = gridDim.x;
@@ -1800,6 +1809,7 @@ __global__ void __launch_bounds__(256) k_batch_sort(const uint32_t* __restrict__
   uint32_t run = part[threadIdx.x];
   for (uint32_t b = b0; b < b0 + per && b < nb; b++) {
     const uint32_t v = cnt[b];
+    if (!v) zero_bucket(zb, r * nb + b);
     bstart[r * nb + b] = (uint32_t)(rowbase + run);
     bend[r * nb + b] = (uint32_t)(rowbase + run + v);
     cnt[b] = run;
@@ -1843,12 +1853,18 @@ constexpr int SB_SPT = 4;                 // scalars per thread: N <= 4096
 constexpr uint32_t SB_NB = 2048;          // buckets per row (c <= 12)
 constexpr uint32_t SB_STAGE = 15 * 1024;  // staged entries per pass (120 KB)
 
+// WC > 0 (c = 12, W = WC = 22: the commit's row MSMs): the window loop is
+// unrolled, so every digit is a funnel shift at a constant bit offset; with a
+// runtime W the offset is runtime and the word select a chain of conditional
+// moves over the scalar's 8 words (x 7 passes over every digit of the row)
+template <int WC>
 __global__ void __launch_bounds__(SB_THREADS) k_batch_sort_staged(const uint32_t* __restrict__ scalars, size_t rows,
                                                                  size_t N, size_t row_stride, size_t col_stride, int c,
                                                                  int W, uint32_t* __restrict__ keys,
                                                                  uint32_t* __restrict__ entries,
                                                                  uint32_t* __restrict__ bstart,
-                                                                 uint32_t* __restrict__ bend) {
+                                                                 uint32_t* __restrict__ bend,
+                                                                 uint4* __restrict__ zb) {
   __shared__ uint32_t start[SB_NB + 1];
   __shared__ uint32_t cur[SB_NB];
   __shared__ uint2 stage[SB_STAGE];
@@ -1868,9 +1884,17 @@ __global__ void __launch_bounds__(SB_THREADS) k_batch_sort_staged(const uint32_t
     uint32_t sc[8];
     load_scalar(scalars + 8 * (r * row_stride + j * col_stride), sc);
     uint32_t carry = 0;
-    for (int w = 0; w < W; w++) {
-      const int d = signed_digit(sc, 8, w, c, W, carry);
-      if (d) atomicAdd(&cur[abs(d) - 1], 1u);
+    if constexpr (WC > 0) {
+#pragma unroll
+      for (int w = 0; w < WC; w++) {
+        const int d = signed_digit(sc, 8, w, 12, WC, carry);
+        if (d) atomicAdd(&cur[abs(d) - 1], 1u);
+      }
+    } else {
+      for (int w = 0; w < W; w++) {
+        const int d = signed_digit(sc, 8, w, c, W, carry);
+        if (d) atomicAdd(&cur[abs(d) - 1], 1u);
+      }
     }
   }
   __syncthreads();
@@ -1908,6 +1932,7 @@ __global__ void __launch_bounds__(SB_THREADS) k_batch_sort_staged(const uint32_t
   __syncthreads();
   const size_t rowbase = r * N * (size_t)W;
   for (uint32_t b = tid; b < nb; b += SB_THREADS) {
+    if (start[b + 1] == start[b]) zero_bucket(zb, r * nb + b);
     bstart[r * nb + b] = (uint32_t)(rowbase + start[b]);
     bend[r * nb + b] = (uint32_t)(rowbase + start[b + 1]);
     cur[b] = start[b];
@@ -1938,25 +1963,30 @@ __global__ void __launch_bounds__(SB_THREADS) k_batch_sort_staged(const uint32_t
     if (lo >= nb) break;
     const uint32_t p0 = start[lo], cnt = start[hi] - p0;
     const bool direct = cnt > SB_STAGE;  // one oversized bucket
+    auto place = [&](int d, int w, size_t j) {
+      if (!d) return;
+      const uint32_t b = (uint32_t)abs(d) - 1;
+      if (b < lo || b >= hi) return;
+      const uint32_t pos = atomicAdd(&cur[b], 1u);
+      const uint2 e = make_uint2((uint32_t)(r * nb + b), (uint32_t)(w * N + j) | (d < 0 ? 0x80000000u : 0u));
+      if (direct) {
+        keys[rowbase + pos] = e.x;
+        entries[rowbase + pos] = e.y;
+      } else {
+        stage[pos - p0] = e;
+      }
+    };
     for (int k = 0; k < SB_SPT; k++) {
       const size_t j = (size_t)tid + (size_t)k * SB_THREADS;
       if (j >= N) break;
       uint32_t sc[8];
       load_scalar(scalars + 8 * (r * row_stride + j * col_stride), sc);
       uint32_t carry = 0;
-      for (int w = 0; w < W; w++) {
-        const int d = signed_digit(sc, 8, w, c, W, carry);
-        if (!d) continue;
-        const uint32_t b = (uint32_t)abs(d) - 1;
-        if (b < lo || b >= hi) continue;
-        const uint32_t pos = atomicAdd(&cur[b], 1u);
-        const uint2 e = make_uint2((uint32_t)(r * nb + b), (uint32_t)(w * N + j) | (d < 0 ? 0x80000000u : 0u));
-        if (direct) {
-          keys[rowbase + pos] = e.x;
-          entries[rowbase + pos] = e.y;
-        } else {
-          stage[pos - p0] = e;
-        }
+      if constexpr (WC > 0) {
+#pragma unroll
+        for (int w = 0; w < WC; w++) place(signed_digit(sc, 8, w, 12, WC, carry), w, j);
+      } else {
+        for (int w = 0; w < W; w++) place(signed_digit(sc, 8, w, c, W, carry), w, j);
       }
     }
     __syncthreads();
@@ -2008,13 +2038,15 @@ hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint3
   Profiler dummy;
   if (!pf) pf = &dummy;
   pf->begin(ST_BATCH_SORT, s);
-  TPST_TRY(hipMemsetAsync(buckets, 0, nbk * sizeof(Xyzz<Fq>), s));  // ZZ = 0 == infinity
-  if (N <= (size_t)SB_THREADS * SB_SPT && nb <= SB_NB)
-    k_batch_sort_staged<<<nrow_blk, SB_THREADS, 0, s>>>(d_scalars, rows, N, row_stride, col_stride, c, W, keys,
-                                                         entries, bstart, bend);
+  if (N <= (size_t)SB_THREADS * SB_SPT && c == 12 && W == 22)
+    k_batch_sort_staged<22><<<nrow_blk, SB_THREADS, 0, s>>>(d_scalars, rows, N, row_stride, col_stride, c, W, keys,
+                                                             entries, bstart, bend, reinterpret_cast<uint4*>(buckets));
+  else if (N <= (size_t)SB_THREADS * SB_SPT && nb <= SB_NB)
+    k_batch_sort_staged<0><<<nrow_blk, SB_THREADS, 0, s>>>(d_scalars, rows, N, row_stride, col_stride, c, W, keys,
+                                                            entries, bstart, bend, reinterpret_cast<uint4*>(buckets));
   else
     k_batch_sort<<<nrow_blk, 256, nb * sizeof(uint32_t), s>>>(d_scalars, rows, N, row_stride, col_stride, c, W, keys,
-                                                          entries, bstart, bend);
+                                                          entries, bstart, bend, reinterpret_cast<uint4*>(buckets));
   TPST_TRY(hipGetLastError());
   pf->end(ST_BATCH_SORT, s);
   pf->begin(ST_BUCKET_ACC, s);
