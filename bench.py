@@ -56,8 +56,8 @@ BYTES_PER_PAIR = 128           # 32 B scalar + 96 B affine base
 LIMB_PRODUCTS_PER_FQ_MUL = 325
 MB_FQMUL_KIND = 12  # tpst_microbench kind of that product (kind 0: field.h's 12 x 32-bit product)
 SEED = 0x7E57D0
-PMC_FILE = os.path.join(ROOT, "profiles", "r05", "d", "pmc_bucket_acc_short.json")
-PMC_FILE_K1 = os.path.join(ROOT, "profiles", "r05", "d", "pmc_bucket_acc_chunk_2p24.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r05", "final", "pmc_bucket_acc_short.json")
+PMC_FILE_K1 = os.path.join(ROOT, "profiles", "r05", "final", "pmc_bucket_acc_chunk_2p24.json")
 if not os.path.exists(PMC_FILE):  # the latest round that has one
     PMC_FILE = os.path.join(ROOT, "profiles", "r03", "pmc_bucket_acc_short.json")
 
