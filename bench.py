@@ -20,7 +20,7 @@ and the Miller loops of their IPP pairs, one RCCL all-gather moves [row
 commitments | Miller partial], rank 0 runs the final exponentiation and the
 (transcript-sequential) open.
 
-roofline: the dominant kernel is bucket accumulation (k_bucket_acc_short, one
+roofline: the dominant kernel is bucket accumulation (k_bucket_acc_short_lds, one
 launch per window group, msm.hip msm_groups); its duration per MSM (all group
 launches, back to back on the library's own stream, with the earlier groups'
 reductions running beside them on aux streams) is measured with HIP events on
@@ -327,7 +327,7 @@ def main():
     madds = 2 * n * windows
     fq_per_madd = fq_mults_per_madd(pmc)
     achieved_fqmul = madds * fq_per_madd / (acc_avg_ms * 1e-3)
-    compute = {"bound": "valu-int32", "kernel": "k_bucket_acc_short<Fq>",
+    compute = {"bound": "valu-int32", "kernel": "k_bucket_acc_short_lds<2, true>",
                "roof": "v_mad_u64_u32 issue (measured) / %d limb products per Fq product" % LIMB_PRODUCTS_PER_FQ_MUL,
                "mad_wave_insts_per_s": rates["v_mad_u64_u32"], "peak_fq_mul_per_s": mad_roof_fqmul,
                "achieved_fq_mul_per_s": achieved_fqmul, "frac": round(achieved_fqmul / mad_roof_fqmul, 4),
@@ -371,7 +371,7 @@ def main():
         "roofline": {"bound": "valu-int32", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                      "traffic_source": (os.path.relpath(PMC_FILE, ROOT) if pmc else None),
-                     "kernel": "k_bucket_acc_short<Fq> (3 window-group launches per MSM)", "alg_bytes_per_launch": alg_bytes,
+                     "kernel": "k_bucket_acc_short_lds<2, true> (G1, 128-B records staged through LDS; 3 window-group launches per MSM)", "alg_bytes_per_launch": alg_bytes,
                      "kernel_avg_ms": round(acc_avg_ms, 4),
                      "note": "HBM column secondary: the kernel is bound by 32-bit integer VALU issue"},
         "compute": compute,

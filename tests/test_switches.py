@@ -7,8 +7,8 @@ fixtures / the CPU oracle:
   the n = 20 proof is unchanged (fixture fullsize_n20.json);
 * TPST_COMMIT_TABLE=0 at n = 20 and n = 24 (the opening builds the fold
   table itself instead of the commit) -- same proofs as the fixtures;
-* TPST_ACC_LDS=1 -- the LDS-staged MSM accumulation, 2^17 + 37 points vs the
-  oracle.
+* TPST_ACC_LDS=0 -- the register-prefetch MSM accumulation instead of the
+  default LDS staging, 2^17 + 37 points vs the oracle.
 """
 import json
 import os
@@ -86,6 +86,6 @@ def test_commit_table_forced_off(n, val):
     assert all(ok.values()), ok
 
 
-def test_acc_lds_msm_vs_oracle():
-    ok, _ = _run(_MSM % {"root": ROOT}, {"TPST_ACC_LDS": "1"})
+def test_acc_register_prefetch_msm_vs_oracle():
+    ok, _ = _run(_MSM % {"root": ROOT}, {"TPST_ACC_LDS": "0"})
     assert all(ok.values()), ok

@@ -168,14 +168,16 @@ __device__ __forceinline__ void glv_phi_point(const uint32_t* __restrict__ bases
 #define TPST_K2_REC29 1
 #endif
 constexpr int REC29_WORDS = 32;
-__device__ __forceinline__ void store_rec29(uint32_t* table, size_t idx, const Affine<Fq>& p) {
-  const Fq29 x = from_std(p.x), y = from_std(p.y);
+__device__ __forceinline__ void store_rec29(uint32_t* table, size_t idx, const Fq29& x, const Fq29& y) {
   uint32_t rec[REC29_WORDS];
 #pragma unroll
   for (int i = 0; i < REC29_WORDS; i++) rec[i] = i < r29::N ? x.v[i] : i < 2 * r29::N ? y.v[i - r29::N] : 0u;
   uint4* dst = reinterpret_cast<uint4*>(table + idx * REC29_WORDS);
 #pragma unroll
   for (int i = 0; i < REC29_WORDS / 4; i++) dst[i] = make_uint4(rec[4 * i], rec[4 * i + 1], rec[4 * i + 2], rec[4 * i + 3]);
+}
+__device__ __forceinline__ void store_rec29(uint32_t* table, size_t idx, const Affine<Fq>& p) {
+  store_rec29(table, idx, from_std(p.x), from_std(p.y));
 }
 
 // one tile of scalars: signed digits (arkworks make_digits over the GLV
@@ -218,11 +220,11 @@ static __global__ void __launch_bounds__(SORT_THREADS)
       }
     }
     if constexpr (sizeof(F) == sizeof(Fq)) {
-      if (rec) {
-        Affine<Fq> p = load_affine<Fq>(bases, i);
-        store_rec29(rec, i, p);
-        if (!is_inf(p)) p.x = mul(p.x, Fq::from_limbs(params::G1_BETA));
-        store_rec29(rec, n + i, p);
+      if (rec) {  // P and phi(P) = (beta x, y) in the accumulation field (infinity: x = y = 0 both)
+        const Affine<Fq> p = load_affine<Fq>(bases, i);
+        const Fq29 x = from_std(p.x), y = from_std(p.y);
+        store_rec29(rec, i, x, y);
+        store_rec29(rec, n + i, mul(x, from_std(Fq::from_limbs(params::G1_BETA))), y);
         continue;
       }
     }
@@ -759,7 +761,8 @@ __global__ void __launch_bounds__(64, MINW)
 // next points (lane i's 16-byte piece j lands at stage[buf][j][i]; no VGPR
 // destination), runs the current mixed add meanwhile, and reads the staged
 // point back with six ds_read_b128.  Frees the prefetched point's VGPRs
-// (occupancy) and moves the gathers off the register file.  TPST_ACC_LDS=1.
+// (occupancy) and moves the gathers off the register file.  The default for
+// G1 (TPST_ACC_LDS=0: k_bucket_acc_short's register prefetch).
 template <int MINW, bool REC29>
 __global__ void __launch_bounds__(64, MINW)
     k_bucket_acc_short_lds(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
@@ -1548,11 +1551,12 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
                                                                           bstart, bend, d_bases, phib, (uint32_t)n,
                                                                           lg, buckets, part);
     } else {
-      // TPST_ACC_LDS=1: the next point staged through LDS (A/B of the
-      // coalesced staging against the register prefetch)
+      // the next point staged through LDS (default: 277-279 vs 273 Mscalar/s
+      // with the register prefetch, profiles/r05/l); TPST_ACC_LDS=0 selects
+      // the register prefetch
       static const bool lds = [] {
         const char* e = getenv("TPST_ACC_LDS");
-        return e && atoi(e) != 0;
+        return !e || atoi(e) != 0;
       }();
       const unsigned grid = grid_for(gchunks, 64);
       if (lds && rec29)

@@ -45,7 +45,7 @@ def main():
     per_msm = lambda d: sum(sum(v) for v in d.values()) / n_msm if d else None  # noqa: E731
     f_kb, w_kb = per_msm(fetch), per_msm(write) or 0.0
     res = {
-        "kernel": "k_bucket_acc_short<Fq> (bench: 2^20-point G1 MSM, GLV, c = 16, one launch per window group)",
+        "kernel": "k_bucket_acc_short[_lds]<Fq> (bench: 2^20-point G1 MSM, GLV, c = 16, one launch per window group)",
         "grids": {str(g): len(v) for g, v in fetch.items()}, "msm_calls": n_msm,
         "fetch_size_kb_per_msm": f_kb, "write_size_kb_per_msm": w_kb,
         "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE as reported; KB = 1024 B",
