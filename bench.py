@@ -698,7 +698,7 @@ def sharded_leg(ctx, log_n, dist, dev, reps=5):
                 pmc = json.load(open(PMC_FILE_K1))
             except ValueError:
                 pmc = None
-        res["roofline_k1"] = {"bound": "valu-int32 / random gathers", "kernel": "k_bucket_acc_chunk<Fq> + fixup",
+        res["roofline_k1"] = {"bound": "valu-int32 / random gathers", "kernel": "k_bucket_acc_chunk_lds<2> + fixup",
                               "achieved": round(alg / acc_s / 1e9, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(alg / acc_s / 1e9 / HBM_PEAK_GBS, 6), "alg_bytes_per_launch": alg,
                               "kernel_ms": round(k1["bucket_acc"], 4),

@@ -675,6 +675,109 @@ __global__ void __launch_bounds__(ACC_BLOCK, MINW)
     store_acc(bpart, blockIdx.x, acc);
 }
 
+// k_bucket_acc_chunk over K1's record table (REC29) with the next record
+// staged through LDS, as k_bucket_acc_short_lds: seven global_load_lds_dwordx4
+// per step land lane i's 16-byte pieces at stage[buf][j][i] while the current
+// mixed add runs; the loop runs to the wave's longest chunk (every lane
+// issues every staging load), then the same tail / owner walk
+template <int MINW>
+__global__ void __launch_bounds__(ACC_BLOCK, MINW)
+    k_bucket_acc_chunk_lds(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals, size_t m_all,
+                           const uint32_t* __restrict__ mend, uint32_t sent, const uint32_t* __restrict__ bstart,
+                           const uint32_t* __restrict__ bend, const uint32_t* __restrict__ table, int lg,
+                           Xyzz<Fq>* __restrict__ buckets, Xyzz<Fq>* __restrict__ part,
+                           Xyzz<Fq>* __restrict__ bpart) {
+  constexpr int NP = 7;  // the first 112 bytes of a 128-byte record
+  __shared__ uint4 stage[2][NP][ACC_BLOCK];
+  using A = AccField<Fq>;
+  using C = typename A::T;
+  const int lane = threadIdx.x;
+  const size_t t = (size_t)blockIdx.x * ACC_BLOCK + lane;
+  const size_t c0 = t << lg;
+  const size_t m = mend ? (size_t)*mend : m_all;
+  if ((((size_t)blockIdx.x * ACC_BLOCK) << lg) >= m) return;  // the whole workgroup (one wave) idle
+  const bool active = c0 < m;
+  const size_t c1 = active ? ((c0 + ((size_t)1 << lg) < m) ? c0 + ((size_t)1 << lg) : m) : c0;
+  auto stage_load = [&](int buf, uint32_t v, bool want) {
+    const uint32_t* src = want ? table + (size_t)REC29_WORDS * (v & 0x7fffffffu) : table;
+#pragma unroll
+    for (int j = 0; j < NP; j++)
+      __builtin_amdgcn_global_load_lds((const void*)(src + 4 * j),
+                                       (__attribute__((address_space(3))) void*)&stage[buf][j][0], 16, 0, 0);
+  };
+  auto stage_read = [&](int buf, uint32_t v) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t w[4 * NP];
+#pragma unroll
+    for (int j = 0; j < NP; j++) {
+      const uint4 q = stage[buf][j][lane];
+      w[4 * j] = q.x;
+      w[4 * j + 1] = q.y;
+      w[4 * j + 2] = q.z;
+      w[4 * j + 3] = q.w;
+    }
+    Affine<C> p;
+#pragma unroll
+    for (int i = 0; i < r29::N; i++) {
+      p.x.v[i] = w[i];
+      p.y.v[i] = w[r29::N + i];
+    }
+    if (v >> 31) p.y = neg(p.y);
+    return p;
+  };
+  uint32_t tail_key = sent;
+  Xyzz<C> acc = Xyzz<C>::inf();
+  uint32_t key = active ? keys[c0] : sent;
+  uint32_t val = active && key < sent ? vals[c0] : 0u;
+  stage_load(0, val, key < sent);
+  const size_t steps = c1 - c0;
+  const size_t maxsteps = (size_t)1 << lg;
+  for (size_t s = 0; s < maxsteps; s++) {
+    const size_t e = c0 + s;
+    const bool live = s < steps;
+    uint32_t key_n = sent, val_n = 0;
+    if (s + 1 < steps) {
+      key_n = keys[e + 1];
+      if (key_n < sent) val_n = vals[e + 1];
+    }
+    const Affine<C> pt = stage_read((int)(s & 1), val);
+    stage_load((int)((s + 1) & 1), val_n, key_n < sent);
+    if (live && key < sent) {
+      acc = add_affine(acc, pt);
+      if (key_n != key) {
+        if (bend[key] <= c1) {  // the bucket ends in this chunk
+          if (bstart[key] >= c0)
+            store_xyzz(buckets, key, A::out(acc));
+          else
+            store_xyzz(part, t, A::out(acc));
+          acc = Xyzz<C>::inf();
+        } else {  // continues: the chunk's last segment
+          tail_key = key;
+        }
+      }
+    }
+    key = key_n;
+    val = val_n;
+    if (__all(s + 1 >= steps ? 1 : 0)) break;  // wave-uniform exit
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no staging load outstanding
+  if (tail_key < sent && bstart[tail_key] < c0) {  // spans the whole chunk
+    store_xyzz(part, t, A::out(acc));
+    tail_key = sent;
+  }
+  __threadfence_block();
+  __syncthreads();
+  if (tail_key >= sent) return;
+  const size_t t1 = ((size_t)bend[tail_key] - 1) >> lg;  // chunk of the bucket's last entry
+  const size_t tb = (size_t)blockIdx.x * ACC_BLOCK + (ACC_BLOCK - 1);
+  const size_t stop = t1 < tb ? t1 : tb;
+  for (size_t u = t + 1; u <= stop; u++) acc = add(acc, load_acc(part, u));
+  if (t1 <= tb)
+    store_acc(buckets, tail_key, acc);
+  else
+    store_acc(bpart, blockIdx.x, acc);
+}
+
 // buckets crossing a workgroup boundary: thread B finishes the bucket holding
 // workgroup B's last entry when that bucket began in B -- its owner's partial
 // plus the leading pieces of the chunks after B up to the bucket's last one
@@ -2054,9 +2157,10 @@ hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint3
   TPST_TRY(hipGetLastError());
   pf->end(ST_BATCH_SORT, s);
   pf->begin(ST_BUCKET_ACC, s);
-  k_bucket_acc_chunk<Fq, 2, true><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys, entries, m, nullptr, (uint32_t)nbk, bstart,
-                                                                        bend, t.d_table, nullptr, 0x7fffffffu, lg,
-                                                                        buckets, part, bpart);
+  // the LDS-staged gathers (2^24 commit 68.7-69.3 -> 68.6-68.8 ms against
+  // k_bucket_acc_chunk<Fq, 2, true>'s register prefetch, profiles/r05/l)
+  k_bucket_acc_chunk_lds<2><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys, entries, m, nullptr, (uint32_t)nbk, bstart, bend,
+                                                                  t.d_table, lg, buckets, part, bpart);
   TPST_TRY(hipGetLastError());
   k_bucket_fixup<Fq><<<grid_for(nblk, 64), 64, 0, s>>>(keys, m, nullptr, (uint32_t)nbk, bstart, bend, lg, nblk,
                                                        part, bpart, buckets);

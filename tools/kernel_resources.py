@@ -35,6 +35,7 @@ HOT = [
     "k_bucket_acc_short<Fp<FqCfg>, 2, true>",
     "k_bucket_acc_short_lds<2, true>",
     "k_bucket_acc_chunk<Fp<FqCfg>, 2, true>",
+    "k_bucket_acc_chunk_lds<2>",
     "k_bucket_fixup_short<Fp<FqCfg> >",
     "k_bucket_fixup_quad<Fp<FqCfg> >",
     "k_bucket_fixup_long<Fp<FqCfg> >",
