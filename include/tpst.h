@@ -73,12 +73,21 @@ int tpst_g1_msm(tpst_ctx* ctx, const uint64_t* bases, size_t n_bases, const uint
 int tpst_g2_msm(tpst_ctx* ctx, const uint64_t* bases, size_t n_bases, const uint64_t* scalars,
                 size_t n_scalars, uint64_t* out);
 /* device-resident form: d_bases Montgomery affine (24 u32 each), d_scalars
- * canonical Fr (8 u32 each), d_out one canonical affine G1.  Pipelined:
- * consecutive calls overlap on the library's internal streams (call i+1 sorts
- * while call i accumulates); every call starts after the work already queued
- * on tpst_stream, and the next call of any other entry point,
- * tpst_synchronize and tpst_join_stream wait for it. */
+ * canonical Fr (8 u32 each), d_out one canonical affine G1.  Stream-ordered:
+ * the call starts after the work already queued on tpst_stream and the MSM's
+ * end is ordered before anything queued on tpst_stream after it (the host
+ * returns at once; consecutive calls run one after another on the device). */
 int tpst_g1_msm_dev(tpst_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, void* d_out);
+/* Pipelined form (opt-in): consecutive calls overlap on the library's
+ * internal streams (call i+1 decomposes and sorts while call i accumulates).
+ * The call starts after the work already queued on tpst_stream, but its work
+ * is NOT ordered before work the caller queues directly on tpst_stream
+ * afterwards.  LIFETIME RULE: d_bases, d_scalars and d_out must stay
+ * allocated and unmodified (and d_out unread) until tpst_synchronize,
+ * tpst_join_stream or the next call of any other tpst_* entry point (each of
+ * which waits for every pending pipelined MSM) -- a framework's caching
+ * allocator must not recycle them before that. */
+int tpst_g1_msm_dev_async(tpst_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, void* d_out);
 /* One MSM split over ranks (sqrt_pst.rs:198 / mipp.rs:393 at 1/2/4/8 GPUs):
  * each rank's share of the points as the raw XYZZ sum (192 B: X, Y, ZZ, ZZZ,
  * Montgomery u64 limbs; no per-rank affine inversion), gathered as bytes,
@@ -275,7 +284,16 @@ int tpst_poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, const uint6
  * polynomial) and `proof`; other ranks: p and proof may be NULL.  Every
  * rank: the whole comm_list, the point, U = c_u (canonical affine, e.g. the
  * combined tpst_poly_cu_partial shares) and its own transcript copy.  With
- * fewer than 4 world rows rank 0 opens alone (the others return at once). */
+ * fewer than 4 world rows rank 0 opens alone (the others return at once).
+ *
+ * After the call only rank 0's transcript is the reference's end state: the
+ * other ranks stop at the hand-over round and leave theirs mid-protocol (a
+ * prover that keeps using the transcript on every rank must take rank 0's).
+ * The allgather callback runs while the context's lock is held: it must not
+ * call back into libtpst on the same context.  A rank that returns an error
+ * stops issuing gathers, so its peers would wait in their next collective:
+ * on any non-OK return the caller must abort the whole group (e.g.
+ * ncclCommAbort / destroying the process group), not retry the call. */
 typedef int (*tpst_allgather_fn)(void* user, size_t send_off, size_t recv_off, size_t bytes, void* stream);
 typedef struct {
   int world, rank;

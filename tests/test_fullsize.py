@@ -96,7 +96,7 @@ def test_fullsize_commit_open_n24(ctx):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [8])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_fullsize_sharded_n24(ctx, world):
     """BASELINE configs[3] in its sharded form (sqrt_pst.rs:121-143 row MSMs +
     IPP, :198 c_u, then the opening), the world-`world` split run rank by rank

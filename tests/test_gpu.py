@@ -219,7 +219,7 @@ def test_split_msm_shares_combine(ctx, world, lg):
 
 
 def test_msm_dev_pipelined_calls(ctx):
-    """Back-to-back tpst_g1_msm_dev calls overlap (api.hip: call i+1's sort
+    """Back-to-back tpst_g1_msm_dev_async calls overlap (api.hip: call i+1's sort
     under call i's accumulation, its accumulation under call i's tail, three
     arenas in turn): five calls of mixed sizes -- window-grouped (tail
     off the bulk stream), single-group, empty -- into five outputs with no
@@ -239,10 +239,10 @@ def test_msm_dev_pipelined_calls(ctx):
     ctx.g1_mul_generator_dev(d_k.data_ptr(), n, d_b.data_ptr())
     calls = [(0, n), (1, 1000), (2, n), (0, 0), (1, n)]
     for o, (j, m) in enumerate(calls):
-        ctx.g1_msm_dev(d_b.data_ptr(), d_s[j].data_ptr(), m, outs[o].data_ptr())
+        ctx.g1_msm_dev_async(d_b.data_ptr(), d_s[j].data_ptr(), m, outs[o].data_ptr())
         if o == 2:  # another entry point between pipelined calls
             mid = ctx.g1_msm(orc.g1_mul_gen(k[:64]), sets[2][:64])
-    ctx.g1_msm_dev(d_b.data_ptr(), d_s[2].data_ptr(), n, outs[5].data_ptr())
+    ctx.g1_msm_dev_async(d_b.data_ptr(), d_s[2].data_ptr(), n, outs[5].data_ptr())
     ctx.synchronize()  # waits for the pending pipelined calls, not only the context stream
     got = outs.cpu().numpy().view(np.uint64)
     ki = [limbs_to_int(r) for r in k]
@@ -254,6 +254,41 @@ def test_msm_dev_pipelined_calls(ctx):
     for o, (j, m) in enumerate(calls + [(2, n)]):
         assert np.array_equal(got[o], ref(j, m)), (o, j, m)
     assert np.array_equal(mid, orc.g1_msm(orc.g1_mul_gen(k[:64]), sets[2][:64]))
+
+
+def test_msm_dev_stream_ordered(ctx):
+    """tpst_g1_msm_dev (the stream-safe form): work the caller
+    queues straight on tpst_stream() after the calls -- a copy of the outputs,
+    then overwriting the scalars -- is ordered after the MSMs without any
+    further tpst_* call, so the copy holds the right results."""
+    import torch
+    n = (1 << 17) + 5
+    k, _ = orc.fr_stream(91, n)
+    dev = torch.device("cuda", 0)
+    d_k = torch.from_numpy(k.view(np.int64)).to(dev)
+    d_b = torch.empty(n * 12, dtype=torch.int64, device=dev)
+    sets = [orc.fr_stream(92 + j, n)[0] for j in range(2)]
+    d_s = [torch.from_numpy(s.view(np.int64)).to(dev) for s in sets]
+    outs = torch.zeros((3, 12), dtype=torch.int64, device=dev)
+    ctx.torch_to_lib()
+    ctx.g1_mul_generator_dev(d_k.data_ptr(), n, d_b.data_ptr())
+    calls = [(0, n), (1, n), (0, 777)]
+    for o, (j, m) in enumerate(calls):
+        ctx.g1_msm_dev(d_b.data_ptr(), d_s[j].data_ptr(), m, outs[o].data_ptr())
+    lib = torch.cuda.ExternalStream(ctx.lib.tpst_stream(ctx.h), device=dev)
+    with torch.cuda.stream(lib):
+        snap = outs.clone()
+        for t in d_s:
+            t.zero_()
+        outs.zero_()
+    lib.synchronize()
+    got = snap.cpu().numpy().view(np.uint64)
+    ki = [limbs_to_int(r) for r in k]
+    for o, (j, m) in enumerate(calls):
+        si = [limbs_to_int(r) for r in sets[j][:m]]
+        ref = orc.g1_mul_gen(fr_array([sum(a * b for a, b in zip(si, ki)) % O.R]))[0]
+        assert np.array_equal(got[o], ref), (o, j, m)
+    ctx.synchronize()
 
 
 def test_xyzz_sum_rejects_misaligned_shares(ctx):

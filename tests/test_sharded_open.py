@@ -10,7 +10,8 @@ all-gather per product through testudo_amd.distributed.TorchExchange (the
 gloo host path), the hand-over of the folded vector to rank 0 once a round is
 shorter than 4 world.  Rank 0's proof must equal, byte for byte, the
 single-process tpst_poly_open of the same polynomial (n <= 13) or the
-BASELINE configs[3] fixture (n = 24, world 8), and verify.
+BASELINE configs[3] fixture (n = 24 at world 2, 4 and 8: the 1/2/4/8-GPU
+splits north_star names), and verify.
 """
 import os
 import socket
@@ -80,6 +81,8 @@ def _worker(rank, world, port, n, q):
         # round 0's direct t_l / t_r; the hand-over of the folded vector
         rs = sharded_rounds(n, world)
         assert rs >= 1 and x.calls == 2 * rs + 2, (rs, x.calls)
+        if n == 24:  # configs[3] at 2 / 4 / 8 GPUs
+            assert x.calls == {2: 22, 4: 20, 8: 18}[world], (world, x.calls)
         if rank != 0:
             assert out is None
             q.put((rank, None))
@@ -118,7 +121,7 @@ def _worker(rank, world, port, n, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n,world", [(11, 2), (12, 4), (13, 8), (24, 8)])
+@pytest.mark.parametrize("n,world", [(11, 2), (12, 4), (13, 8), (24, 2), (24, 4), (24, 8)])
 def test_sharded_open_matches_single_process(n, world):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")

@@ -29,6 +29,7 @@ PROTOTYPES = [
     ("tpst_g1_msm", C.c_int, [_vp, _u64p, _sz, _u64p, _sz, _u64p]),
     ("tpst_g2_msm", C.c_int, [_vp, _u64p, _sz, _u64p, _sz, _u64p]),
     ("tpst_g1_msm_dev", C.c_int, [_vp, _vp, _vp, _sz, _vp]),
+    ("tpst_g1_msm_dev_async", C.c_int, [_vp, _vp, _vp, _sz, _vp]),
     ("tpst_g1_msm_xyzz_dev", C.c_int, [_vp, _vp, _vp, _sz, _vp]),
     ("tpst_g1_xyzz_sum_dev", C.c_int, [_vp, _vp, _sz, _sz, _vp]),
     ("tpst_g1_multiexp", C.c_int, [_vp, _u64p, _sz, _u64p, _sz, _u64p]),

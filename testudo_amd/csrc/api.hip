@@ -81,7 +81,9 @@ extern "C" void tpst_destroy(tpst_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->msm_tail);
     (void)hipStreamDestroy(ctx->msm_tail);
   }
-  for (int i = 0; i < tpst_ctx::MSM_SLOTS; i++) {
+  // slots 1.. borrow slot 0's aux streams (aux_from): release them first, so
+  // no arena synchronizes a stream slot 0 has already destroyed
+  for (int i = tpst_ctx::MSM_SLOTS - 1; i >= 0; i--) {
     if (ctx->msm_in[i]) (void)hipEventDestroy(ctx->msm_in[i]);
     if (ctx->msm_done[i]) (void)hipEventDestroy(ctx->msm_done[i]);
     if (ctx->msm_out[i]) (void)hipFree(ctx->msm_out[i]);
@@ -232,7 +234,7 @@ extern "C" int tpst_g2_msm_fixed(tpst_ctx* ctx, const uint64_t* bases, size_t n,
   return msm_fixed_host<Fq2>(ctx, bases, n, scalars, L, D, out);
 }
 
-// Pipelined: consecutive calls overlap.  Call i decomposes and sorts its
+// Pipelined (tpst_g1_msm_dev_async): consecutive calls overlap.  Call i decomposes and sorts its
 // scalars on ctx->side[0], accumulates on ctx->side[1] and runs its
 // latency-bound tail (the last window group's fixup, bucket reduction and
 // window chain, and the affine output; ~0.7 ms of a few waves at 2^20) on
@@ -244,7 +246,13 @@ extern "C" int tpst_g2_msm_fixed(tpst_ctx* ctx, const uint64_t* bases, size_t n,
 // inputs), the next entry point of any other kind (and tpst_synchronize /
 // tpst_join_stream) first waits for the pending tails (CtxMutex::lock), and a
 // call reusing an arena waits for the tail that last used it.
-extern "C" int tpst_g1_msm_dev(tpst_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, void* d_out) {
+// tpst_g1_msm_dev (stream-safe): the same work, then ctx->stream waits for its
+// end, so work the caller queues on tpst_stream() afterwards (reading d_out,
+// overwriting the inputs, freeing them) is ordered after the MSM; consecutive
+// calls then run one after another on the device (the host still returns at
+// once).
+static int msm_dev_impl(tpst_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, void* d_out,
+                        bool async) {
   if (!ctx || !d_out || (n && (!d_bases || !d_scalars))) return fail(ctx, TPST_E_ARG, "null argument");
   if (n > MSM_MAX_POINTS) return fail(ctx, TPST_E_ARG, "MSM longer than 2^27 points: split it");
   tpst::CtxKeep lk(ctx->mu);
@@ -273,16 +281,32 @@ extern "C" int tpst_g1_msm_dev(tpst_ctx* ctx, const void* d_bases, const void* d
   bool on_tail = false;
   Xyzz<Fq>* d_r = (Xyzz<Fq>*)ctx->msm_out[k];
   TPST_HIP(ctx, hipStreamWaitEvent(bulk, ctx->msm_in[k], 0));  // n = 0: no front work
+  // n = 0 writes msm_out[k] on bulk without front work: order it after the
+  // tail of the call that last used slot k (it may still read msm_out[k])
+  if (ctx->msm_done_set[k]) TPST_HIP(ctx, hipStreamWaitEvent(bulk, ctx->msm_done[k], 0));
   TPST_HIP(ctx, msm_var<Fq>(ar, bulk, (const uint32_t*)d_bases, (const uint32_t*)d_scalars, n, d_r, ctx->msm_tail,
                             &on_tail, front));
   hipStream_t t = on_tail ? ctx->msm_tail : bulk;
   TPST_HIP(ctx, xyzz_to_affine_canonical<Fq>(t, d_r, (uint32_t*)d_out, 1));
   TPST_HIP(ctx, hipEventRecord(ctx->msm_done[k], t));
   ctx->msm_done_set[k] = true;
+  if (!async) {
+    TPST_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->msm_done[k], 0));
+    return TPST_OK;
+  }
   bool listed = false;
   for (hipEvent_t e : ctx->mu.pending) listed |= e == ctx->msm_done[k];
   if (!listed) ctx->mu.pending.push_back(ctx->msm_done[k]);
   return TPST_OK;
+}
+
+extern "C" int tpst_g1_msm_dev(tpst_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, void* d_out) {
+  return msm_dev_impl(ctx, d_bases, d_scalars, n, d_out, false);
+}
+
+extern "C" int tpst_g1_msm_dev_async(tpst_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n,
+                                     void* d_out) {
+  return msm_dev_impl(ctx, d_bases, d_scalars, n, d_out, true);
 }
 
 // strong-scaled MSM pieces: one rank's share as the raw XYZZ sum (no affine

@@ -1582,7 +1582,9 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
       const Slot sl = slot(per * X1);
       TPST_HIP(ctx, fbt_msm<Fq>(arB, sB, tA, ScB.u(), g, (Xyzz<Fq>*)sl.send));
       if (int rc = gather(sB, sl, per * X1)) return rc;
-      if (!lead) {  // this rank's part is done
+      if (!lead) {  // this rank's part is done (its transcript stops here: tpst.h)
+        pf.end(ST_MIPP_PROVE, sA);
+        pf.end(ST_SQRT_OPEN, sA);
         for (hipStream_t s2 : {sA, sB, sLA[0], sLA[1], sC, ctx->comm}) TPST_HIP(ctx, hipStreamSynchronize(s2));
         sp.store(tr);
         return TPST_OK;

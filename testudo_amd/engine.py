@@ -147,8 +147,16 @@ class Context:
         self.check(self.lib.tpst_join_stream(self.h, self._torch_stream(self.device)), "tpst_join_stream")
 
     def g1_msm_dev(self, d_bases: int, d_scalars: int, n: int, d_out: int):
+        """Stream-ordered device MSM: later work on the library stream sees d_out."""
         self.check(self.lib.tpst_g1_msm_dev(self.h, C.c_void_p(d_bases), C.c_void_p(d_scalars), n,
                                             C.c_void_p(d_out)), "tpst_g1_msm_dev")
+
+    def g1_msm_dev_async(self, d_bases: int, d_scalars: int, n: int, d_out: int):
+        """Pipelined device MSM (tpst_g1_msm_dev_async): consecutive calls overlap.
+        The buffers must stay alive and untouched until synchronize() /
+        lib_to_torch() or the next call of another entry point."""
+        self.check(self.lib.tpst_g1_msm_dev_async(self.h, C.c_void_p(d_bases), C.c_void_p(d_scalars), n,
+                                                  C.c_void_p(d_out)), "tpst_g1_msm_dev_async")
 
     def g1_msm_xyzz_dev(self, d_bases: int, d_scalars: int, n: int, d_out: int):
         """One rank's share of a split MSM: the raw XYZZ sum (24 u64, Montgomery) at d_out."""
