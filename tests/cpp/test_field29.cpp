@@ -2,7 +2,8 @@
 // (tests/test_field29.py): per input line "a b" (field.h Montgomery words,
 // 12 x u32 hex, possibly unreduced below 64 p) print
 //   mul, sqr, add, sub, to_std(from_std(a)), inv(a),
-//   mul_sum(a, b, a, a) = ab + a^2, mul_sub(a, b, b, b) = ab - b^2  for reduced a, b
+//   mul_sum(a, b, a, a) = ab + a^2, mul_sub(a, b, b, b) = ab - b^2,
+//   pack377(a) (= a 2^377 mod p as a plain integer), unpack377(pack377(a))  for reduced a, b
 //   the wave engine's stage product / square               for wide a, b
 #include <cstdio>
 #include <cstring>
@@ -41,6 +42,10 @@ int main() {
       put(inv(a));
       put(to_std(mul_sum(x, y, x, x)));
       put(to_std(mul_sub(x, y, y, y)));
+      Fq w;  // the accumulation kernels' packed bucket format and back
+      pack377(x, w.v);
+      put(w);
+      put(to_std(unpack377(w.v)));
     }
   }
   return 0;

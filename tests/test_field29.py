@@ -2,7 +2,8 @@
 the wave engine's products) checked on the host against Python integers:
 Montgomery product / square / add / sub, the one-reduction sum of two
 products (mul_sum / mul_sub), the conversions from and to
-field.h's layout (R = 2^384 <-> 2^377), the binary-GCD inverse, and the wave
+field.h's layout (R = 2^384 <-> 2^377), the packed bucket format (pack377 /
+unpack377: the R = 2^377 value's bits in 12 words), the binary-GCD inverse, and the wave
 engine's stage product on unreduced operands (a form of weight w is < w p;
 the engine feeds products with w_x w_y <= 64, squares with w <= 8)."""
 import os
@@ -44,9 +45,10 @@ def test_field29_ops_and_inverse(exe):
     vals += [(rng.randrange(P), rng.randrange(P)) for _ in range(2000)]
     out = _run(exe, [(0, a * R % P, b * R % P) for a, b in vals])
     for k, (a, b) in enumerate(vals):
-        got = [_parse(out[8 * k + j]) for j in range(8)]
+        got = [_parse(out[10 * k + j]) for j in range(10)]
         exp = [a * b % P * R % P, a * a % P * R % P, (a + b) % P * R % P, (a - b) % P * R % P, a * R % P,
-               (pow(a, -1, P) * R % P) if a else 0, (a * b + a * a) % P * R % P, (a * b - b * b) % P * R % P]
+               (pow(a, -1, P) * R % P) if a else 0, (a * b + a * a) % P * R % P, (a * b - b * b) % P * R % P,
+               a * (1 << 377) % P, a * R % P]
         assert got == exp, (a, b)
 
 

@@ -104,4 +104,38 @@ __device__ __forceinline__ void store_acc(Xyzz<F>* p, size_t i, const Xyzz<typen
   store_xyzz(p, i, AccField<F>::out(v));
 }
 
+// Buckets, parked pieces and block partials of the accumulation kernels
+// (written and read only by msm.hip's accumulation / fixup / first reduction
+// kernels): for G1 the accumulation field's own Montgomery values packed bit
+// for bit (field29.h pack377; 12 words per coordinate like field.h, so buffer
+// sizes and the all-zero infinity are unchanged).  The accumulation loops
+// store a bucket every few mixed adds, and the conversion to field.h
+// (to_std: ~190 VALU per coordinate, run by the whole wave whenever one lane
+// ends a bucket) was ~6 % of K2's and ~10 % of K1's issue slots.  G2 keeps
+// field.h's layout.
+template <class F>
+__device__ __forceinline__ Xyzz<typename AccField<F>::T> load_pk(const Xyzz<F>* p, size_t i) {
+  return load_acc(p, i);
+}
+template <class F>
+__device__ __forceinline__ void store_pk(Xyzz<F>* p, size_t i, const Xyzz<typename AccField<F>::T>& v) {
+  store_acc(p, i, v);
+}
+#if TPST_ACC29
+template <>
+__device__ __forceinline__ Xyzz<Fq29> load_pk<Fq>(const Xyzz<Fq>* p, size_t i) {
+  const Xyzz<Fq> w = load_xyzz(p, i);
+  return {unpack377(w.X.v), unpack377(w.Y.v), unpack377(w.ZZ.v), unpack377(w.ZZZ.v)};
+}
+template <>
+__device__ __forceinline__ void store_pk<Fq>(Xyzz<Fq>* p, size_t i, const Xyzz<Fq29>& v) {
+  Xyzz<Fq> w;
+  pack377(v.X, w.X.v);
+  pack377(v.Y, w.Y.v);
+  pack377(v.ZZ, w.ZZ.v);
+  pack377(v.ZZZ, w.ZZZ.v);
+  store_xyzz(p, i, w);
+}
+#endif
+
 }  // namespace tpst

@@ -264,6 +264,39 @@ TPST_HD uint32_t bits29(const uint32_t* w, int s) {
 #endif
 }
 
+// The accumulation kernels' internal bucket / piece format: the radix-2^29
+// Montgomery value itself (x 2^377, canonical, < p < 2^377) with its 377 bits
+// regrouped into 12 u32 words -- field.h's footprint, but no modular
+// conversion either way (to_std / from_std cost a quotient estimate, 12 limb
+// products and a conditional subtraction per coordinate; this is ~2 bit
+// operations per word)
+TPST_HD void pack377(const Fq29& a, uint32_t* w) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    const int s = 32 * i, j = s / 29, o = s % 29;
+    uint32_t v = a.v[j] >> o;
+    if (j + 1 < r29::N) v |= a.v[j + 1] << (29 - o);
+    if (j + 2 < r29::N && 58 - o < 32) v |= a.v[j + 2] << (58 - o);
+    w[i] = v;
+  }
+}
+
+TPST_HD Fq29 unpack377(const uint32_t* w) {
+  Fq29 r;
+#pragma unroll
+  for (int j = 0; j < r29::N; j++) {
+    const int s = 29 * j, q = s >> 5, o = s & 31;
+    const uint32_t lo = w[q];
+    const uint32_t hi = q + 1 < 12 ? w[q + 1] : 0u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    r.v[j] = __builtin_amdgcn_alignbit(hi, lo, (uint32_t)o) & r29::M;
+#else
+    r.v[j] = (uint32_t)((((uint64_t)hi << 32) | lo) >> o) & r29::M;
+#endif
+  }
+  return r;
+}
+
 // field.h Montgomery (x 2^384, 12 x u32) -> x 2^377 in radix 2^29:
 // (a + k p) / 2^7 < p for a < p; for an unreduced a < 64 p (a wave-engine
 // form) the sum carries into a 13th word and the result is < 1.5 p < 2^377

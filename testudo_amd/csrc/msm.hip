@@ -645,9 +645,9 @@ __global__ void __launch_bounds__(ACC_BLOCK, MINW)
           if (bend[key] <= c1) {  // the bucket ends in this chunk
             // began here: complete; began earlier: the chunk's first segment
             if (bstart[key] >= c0)
-              store_xyzz(buckets, key, A::out(acc));
+              store_pk(buckets, key, acc);
             else
-              store_xyzz(part, t, A::out(acc));
+              store_pk(part, t, acc);
             acc = Xyzz<C>::inf();
           } else {  // continues: the chunk's last segment (e + 1 == c1)
             tail_key = key;
@@ -658,7 +658,7 @@ __global__ void __launch_bounds__(ACC_BLOCK, MINW)
       pt = pt_n;
     }
     if (tail_key < sent && bstart[tail_key] < c0) {  // spans the whole chunk
-      store_xyzz(part, t, A::out(acc));
+      store_pk(part, t, acc);
       tail_key = sent;
     }
   }
@@ -668,11 +668,11 @@ __global__ void __launch_bounds__(ACC_BLOCK, MINW)
   const size_t t1 = ((size_t)bend[tail_key] - 1) >> lg;  // chunk of the bucket's last entry
   const size_t tb = (size_t)blockIdx.x * ACC_BLOCK + (ACC_BLOCK - 1);
   const size_t stop = t1 < tb ? t1 : tb;
-  for (size_t u = t + 1; u <= stop; u++) acc = add(acc, load_acc(part, u));
+  for (size_t u = t + 1; u <= stop; u++) acc = add(acc, load_pk(part, u));
   if (t1 <= tb)
-    store_acc(buckets, tail_key, acc);
+    store_pk(buckets, tail_key, acc);
   else
-    store_acc(bpart, blockIdx.x, acc);
+    store_pk(bpart, blockIdx.x, acc);
 }
 
 // k_bucket_acc_chunk over K1's record table (REC29) with the next record
@@ -680,6 +680,12 @@ __global__ void __launch_bounds__(ACC_BLOCK, MINW)
 // per step land lane i's 16-byte pieces at stage[buf][j][i] while the current
 // mixed add runs; the loop runs to the wave's longest chunk (every lane
 // issues every staging load), then the same tail / owner walk
+#ifndef TPST_K1_NBUF
+#define TPST_K1_NBUF 2
+#endif
+#ifndef TPST_K1_MINW
+#define TPST_K1_MINW 2
+#endif
 template <int MINW>
 __global__ void __launch_bounds__(ACC_BLOCK, MINW)
     k_bucket_acc_chunk_lds(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals, size_t m_all,
@@ -688,7 +694,8 @@ __global__ void __launch_bounds__(ACC_BLOCK, MINW)
                            Xyzz<Fq>* __restrict__ buckets, Xyzz<Fq>* __restrict__ part,
                            Xyzz<Fq>* __restrict__ bpart) {
   constexpr int NP = 7;  // the first 112 bytes of a 128-byte record
-  __shared__ uint4 stage[2][NP][ACC_BLOCK];
+  constexpr int NBUF = TPST_K1_NBUF;  // 1: refilled once the current record's ds_reads returned
+  __shared__ uint4 stage[NBUF][NP][ACC_BLOCK];
   using A = AccField<Fq>;
   using C = typename A::T;
   const int lane = threadIdx.x;
@@ -740,16 +747,17 @@ __global__ void __launch_bounds__(ACC_BLOCK, MINW)
       key_n = keys[e + 1];
       if (key_n < sent) val_n = vals[e + 1];
     }
-    const Affine<C> pt = stage_read((int)(s & 1), val);
-    stage_load((int)((s + 1) & 1), val_n, key_n < sent);
+    const Affine<C> pt = stage_read(NBUF == 1 ? 0 : (int)(s & 1), val);
+    if constexpr (NBUF == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // pt read out of the buffer
+    stage_load(NBUF == 1 ? 0 : (int)((s + 1) & 1), val_n, key_n < sent);
     if (live && key < sent) {
       acc = add_affine(acc, pt);
       if (key_n != key) {
         if (bend[key] <= c1) {  // the bucket ends in this chunk
           if (bstart[key] >= c0)
-            store_xyzz(buckets, key, A::out(acc));
+            store_pk(buckets, key, acc);
           else
-            store_xyzz(part, t, A::out(acc));
+            store_pk(part, t, acc);
           acc = Xyzz<C>::inf();
         } else {  // continues: the chunk's last segment
           tail_key = key;
@@ -762,7 +770,7 @@ __global__ void __launch_bounds__(ACC_BLOCK, MINW)
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no staging load outstanding
   if (tail_key < sent && bstart[tail_key] < c0) {  // spans the whole chunk
-    store_xyzz(part, t, A::out(acc));
+    store_pk(part, t, acc);
     tail_key = sent;
   }
   __threadfence_block();
@@ -771,11 +779,11 @@ __global__ void __launch_bounds__(ACC_BLOCK, MINW)
   const size_t t1 = ((size_t)bend[tail_key] - 1) >> lg;  // chunk of the bucket's last entry
   const size_t tb = (size_t)blockIdx.x * ACC_BLOCK + (ACC_BLOCK - 1);
   const size_t stop = t1 < tb ? t1 : tb;
-  for (size_t u = t + 1; u <= stop; u++) acc = add(acc, load_acc(part, u));
+  for (size_t u = t + 1; u <= stop; u++) acc = add(acc, load_pk(part, u));
   if (t1 <= tb)
-    store_acc(buckets, tail_key, acc);
+    store_pk(buckets, tail_key, acc);
   else
-    store_acc(bpart, blockIdx.x, acc);
+    store_pk(bpart, blockIdx.x, acc);
 }
 
 // buckets crossing a workgroup boundary: thread B finishes the bucket holding
@@ -796,9 +804,9 @@ __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
   const uint32_t key = keys[e];
   if (key >= sent || keys[e - 1] != key || ((size_t)bstart[key] >> lb) != B) return;
   const size_t t1 = ((size_t)bend[key] - 1) >> lg;
-  Xyzz<C> acc = load_acc(bpart, B);
-  for (size_t u = (B + 1) << ACC_BLOCK_LG; u <= t1; u++) acc = add(acc, load_acc(part, u));
-  store_acc(buckets, key, acc);
+  Xyzz<C> acc = load_pk(bpart, B);
+  for (size_t u = (B + 1) << ACC_BLOCK_LG; u <= t1; u++) acc = add(acc, load_pk(part, u));
+  store_pk(buckets, key, acc);
 }
 
 // Short-chunk accumulation for the variable-base MSM (32-entry chunks over
@@ -848,9 +856,9 @@ __global__ void __launch_bounds__(64, MINW)
         const bool starts = bstart[key] >= c0;
         const bool ends = bend[key] <= c1;
         if (starts && ends)
-          store_xyzz(buckets, key, A::out(acc));
+          store_pk(buckets, key, acc);
         else
-          store_xyzz(part, 2 * t + (starts ? 1 : 0), A::out(acc));
+          store_pk(part, 2 * t + (starts ? 1 : 0), acc);
         acc = Xyzz<C>::inf();
       }
     }
@@ -866,6 +874,12 @@ __global__ void __launch_bounds__(64, MINW)
 // point back with six ds_read_b128.  Frees the prefetched point's VGPRs
 // (occupancy) and moves the gathers off the register file.  The default for
 // G1 (TPST_ACC_LDS=0: k_bucket_acc_short's register prefetch).
+#ifndef TPST_K2_NBUF
+#define TPST_K2_NBUF 2
+#endif
+#ifndef TPST_K2_MINW
+#define TPST_K2_MINW 2  // waves per SIMD the register allocation targets (G1 records)
+#endif
 template <int MINW, bool REC29>
 __global__ void __launch_bounds__(64, MINW)
     k_bucket_acc_short_lds(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
@@ -876,7 +890,10 @@ __global__ void __launch_bounds__(64, MINW)
   // double-buffered points, piece-major: 96-byte field.h points or the
   // first 112 bytes of a 128-byte record (REC29)
   constexpr int NP = REC29 ? 7 : 6;
-  __shared__ uint4 stage[2][NP][64];
+  // NBUF = 1: one staging buffer, refilled once the current point's ds_reads
+  // have returned (half the LDS per wave)
+  constexpr int NBUF = TPST_K2_NBUF;
+  __shared__ uint4 stage[NBUF][NP][64];
   using A = AccField<Fq>;
   using C = typename A::T;
   const int lane = threadIdx.x;
@@ -939,17 +956,18 @@ __global__ void __launch_bounds__(64, MINW)
       key_n = keys[e + 1];
       if (key_n < sent) val_n = vals[e + 1];
     }
-    const Affine<C> pt = stage_read((int)(s & 1), val);
-    stage_load((int)((s + 1) & 1), val_n, key_n < sent);
+    const Affine<C> pt = stage_read(NBUF == 1 ? 0 : (int)(s & 1), val);
+    if constexpr (NBUF == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // pt read out of the buffer
+    stage_load(NBUF == 1 ? 0 : (int)((s + 1) & 1), val_n, key_n < sent);
     if (live && key < sent) {
       acc = add_affine(acc, pt);
       if (key_n != key) {
         const bool starts = bstart[key] >= c0;
         const bool ends = bend[key] <= c1;
         if (starts && ends)
-          store_xyzz(buckets, key, A::out(acc));
+          store_pk(buckets, key, acc);
         else
-          store_xyzz(part, 2 * t + (starts ? 1 : 0), A::out(acc));
+          store_pk(part, 2 * t + (starts ? 1 : 0), acc);
         acc = Xyzz<C>::inf();
       }
     }
@@ -1011,6 +1029,16 @@ static __global__ void __launch_bounds__(64, 2)
   }
 }
 
+// bucket-array input of a reduction kernel: the accumulation's packed format
+// (PK) or a reduction's own output
+template <bool PK, class F>
+__device__ __forceinline__ Xyzz<typename AccField<F>::T> load_in(const Xyzz<F>* p, size_t i) {
+  if constexpr (PK)
+    return load_pk(p, i);
+  else
+    return load_acc(p, i);
+}
+
 // Buckets spanning more than LONG_PARTS chunks (many equal digits: small or
 // boolean scalars put most entries of a window into one bucket) are not
 // walked by one lane of the fixups below -- 2^20 entries of one bucket would
@@ -1043,15 +1071,15 @@ __global__ void __launch_bounds__(LONG_THREADS) k_bucket_fixup_long(const uint32
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
     const uint32_t b = ll.list[i];
     const size_t t0 = (size_t)bstart[b] >> lg, t1 = (size_t)(bend[b] - 1) >> lg;
-    Xyzz<C> acc = tid == 0 ? load_acc(part, 2 * t0 + 1) : Xyzz<C>::inf();
-    for (size_t t = t0 + 1 + tid; t <= t1; t += LONG_THREADS) acc = add(acc, load_acc(part, 2 * t));
+    Xyzz<C> acc = tid == 0 ? load_pk(part, 2 * t0 + 1) : Xyzz<C>::inf();
+    for (size_t t = t0 + 1 + tid; t <= t1; t += LONG_THREADS) acc = add(acc, load_pk(part, 2 * t));
     sh[tid] = acc;
     __syncthreads();
     for (uint32_t h = LONG_THREADS / 2; h > 0; h >>= 1) {
       if (tid < h) sh[tid] = add(sh[tid], sh[tid + h]);
       __syncthreads();
     }
-    if (tid == 0) store_acc(buckets, b, sh[0]);
+    if (tid == 0) store_pk(buckets, b, sh[0]);
     __syncthreads();
   }
 }
@@ -1097,9 +1125,9 @@ __global__ void __launch_bounds__(64, (sizeof(F) > 48 ? 1 : 2))
     ll.push((uint32_t)b);
     return;
   }
-  Xyzz<C> acc = load_acc(part, 2 * t0 + 1);
-  for (size_t t = t0 + 1; t <= t1; t++) acc = add(acc, load_acc(part, 2 * t));
-  store_acc(buckets, b, acc);
+  Xyzz<C> acc = load_pk(part, 2 * t0 + 1);
+  for (size_t t = t0 + 1; t <= t1; t++) acc = add(acc, load_pk(part, 2 * t));
+  store_pk(buckets, b, acc);
 }
 
 // the same fixup, one quad of lanes per bucket (coop.h: 4 product latencies
@@ -1122,16 +1150,16 @@ __global__ void __launch_bounds__(64) k_bucket_fixup_quad(const uint32_t* __rest
     if (qi == 0) ll.push((uint32_t)b);
     return;
   }
-  Xyzz<C> acc = load_acc(part, 2 * t0 + 1);
-  for (size_t t = t0 + 1; t <= t1; t++) acc = add_quad(acc, load_acc(part, 2 * t), qi);
-  if (qi == 0) store_acc(buckets, b, acc);
+  Xyzz<C> acc = load_pk(part, 2 * t0 + 1);
+  for (size_t t = t0 + 1; t <= t1; t++) acc = add_quad(acc, load_pk(part, 2 * t), qi);
+  if (qi == 0) store_pk(buckets, b, acc);
 }
 
 // segment t of group g: sum_{b in seg} (b+1) * S_b with b the bucket index
 // inside the group (bucket b holds digit value b+1): running sums over the L
 // buckets plus (segment offset) * (segment sum).  One quad of lanes per
 // segment (coop.h): 4 / 3 product latencies per addition / doubling.
-template <class F>
+template <class F, bool PK>
 __global__ void __launch_bounds__(64) k_seg_reduce_quad(const Xyzz<F>* __restrict__ buckets, uint32_t nb, uint32_t L,
                                                         size_t nseg, Xyzz<F>* __restrict__ seg_out, int prio = 0) {
   using C = typename AccField<F>::T;
@@ -1145,7 +1173,7 @@ __global__ void __launch_bounds__(64) k_seg_reduce_quad(const Xyzz<F>* __restric
   const size_t base = g * nb + (size_t)k * L;
   Xyzz<C> acc = Xyzz<C>::inf(), sum = Xyzz<C>::inf();
   for (int b = (int)L - 1; b >= 0; b--) {
-    acc = add_quad(acc, load_acc(buckets, base + b), qi);
+    acc = add_quad(acc, load_in<PK>(buckets, base + b), qi);
     sum = add_quad(sum, acc, qi);
   }
   const uint32_t s0 = k * L;
@@ -1157,7 +1185,7 @@ __global__ void __launch_bounds__(64) k_seg_reduce_quad(const Xyzz<F>* __restric
 // segments to fill the chip (the 4096-row commit at 2^24: 262 144 segments)
 // the quad-cooperative form only adds exchange overhead to a throughput-bound
 // pass
-template <class F>
+template <class F, bool PK>
 __global__ void __launch_bounds__(64) k_seg_reduce_lane(const Xyzz<F>* __restrict__ buckets, uint32_t nb, uint32_t L,
                                                         size_t nseg, Xyzz<F>* __restrict__ seg_out) {
   using C = typename AccField<F>::T;
@@ -1169,7 +1197,7 @@ __global__ void __launch_bounds__(64) k_seg_reduce_lane(const Xyzz<F>* __restric
   const size_t base = g * nb + (size_t)k * L;
   Xyzz<C> acc = Xyzz<C>::inf(), sum = Xyzz<C>::inf();
   for (int b = (int)L - 1; b >= 0; b--) {
-    acc = add(acc, load_acc(buckets, base + b));
+    acc = add(acc, load_in<PK>(buckets, base + b));
     sum = add(sum, acc);
   }
   const uint32_t s0 = k * L;
@@ -1274,6 +1302,7 @@ __global__ void __launch_bounds__(64) k_xyzz_to_affine_wave(const Xyzz<F>* __res
 // (k_xyzz_to_affine_wave); above it one lone-lane inverse per point
 constexpr size_t INV_WAVE_MAX = 4096;
 
+#ifndef TPST_MSM_LAB  // tools/lab: the kernels above only, instantiated there
 template <class F>
 hipError_t points_to_mont(hipStream_t s, const uint32_t* d_in, uint32_t* d_out, size_t n) {
   if (!n) return hipSuccess;
@@ -1320,15 +1349,22 @@ static size_t reduce_scratch(size_t groups, uint32_t nb) {
 
 template <class F>
 static hipError_t reduce_buckets(Arena& ar, hipStream_t s, const Xyzz<F>* d_buckets, size_t groups, uint32_t nb,
-                                 Xyzz<F>* d_group_out, int prio = 0) {
+                                 Xyzz<F>* d_group_out, int prio = 0, bool pk = true) {
   const uint32_t L = reduce_seg_len(groups, nb);
   const uint32_t S = nb / L;
   const size_t nseg = groups * S;
   Xyzz<F>* seg = ar.take<Xyzz<F>>(nseg);
-  if (std::is_same<F, Fq>::value && nseg >= ((size_t)1 << 18))
-    k_seg_reduce_lane<F><<<grid_for(nseg, 64), 64, 0, s>>>(d_buckets, nb, L, nseg, seg);
-  else
-    k_seg_reduce_quad<F><<<grid_for(4 * nseg, 64), 64, 0, s>>>(d_buckets, nb, L, nseg, seg, prio);
+  // d_buckets: the accumulation's bucket format (pk) or a reduction's output
+  if (std::is_same<F, Fq>::value && nseg >= ((size_t)1 << 18)) {
+    if (pk)
+      k_seg_reduce_lane<F, true><<<grid_for(nseg, 64), 64, 0, s>>>(d_buckets, nb, L, nseg, seg);
+    else
+      k_seg_reduce_lane<F, false><<<grid_for(nseg, 64), 64, 0, s>>>(d_buckets, nb, L, nseg, seg);
+  } else if (pk) {
+    k_seg_reduce_quad<F, true><<<grid_for(4 * nseg, 64), 64, 0, s>>>(d_buckets, nb, L, nseg, seg, prio);
+  } else {
+    k_seg_reduce_quad<F, false><<<grid_for(4 * nseg, 64), 64, 0, s>>>(d_buckets, nb, L, nseg, seg, prio);
+  }
   TPST_TRY(hipGetLastError());
   if (S >= 256 && S % 64 == 0) {  // two-pass tree: 64 -> 1, then per group
     Xyzz<F>* mid = ar.take<Xyzz<F>>(nseg / 64);
@@ -1347,7 +1383,7 @@ static hipError_t reduce_buckets(Arena& ar, hipStream_t s, const Xyzz<F>* d_buck
 // Level 1: segments of L1 buckets -> S_k = sum_{b in seg} (b - k L1 + 1) X_b and
 // T_k = sum_{b in seg} X_b; then sum_b (b+1) X_b = sum_k S_k + L1 sum_k k T_k,
 // the second sum being the same weighted reduction over Tn_{k-1} = T_k.
-template <class F>
+template <class F, bool PK = true>
 __global__ void __launch_bounds__(64) k_seg_run_quad(const Xyzz<F>* __restrict__ buckets, uint32_t nb, uint32_t L,
                                                      size_t nseg, Xyzz<F>* __restrict__ S_out,
                                                      Xyzz<F>* __restrict__ Tn, int prio = 0) {
@@ -1362,7 +1398,7 @@ __global__ void __launch_bounds__(64) k_seg_run_quad(const Xyzz<F>* __restrict__
   const size_t base = g * nb + (size_t)k * L;
   Xyzz<C> acc = Xyzz<C>::inf(), sum = Xyzz<C>::inf();
   for (int b = (int)L - 1; b >= 0; b--) {
-    acc = add_quad(acc, load_acc(buckets, base + b), qi);
+    acc = add_quad(acc, load_in<PK>(buckets, base + b), qi);
     sum = add_quad(sum, acc, qi);
   }
   if (qi == 0) {
@@ -1373,7 +1409,7 @@ __global__ void __launch_bounds__(64) k_seg_run_quad(const Xyzz<F>* __restrict__
 
 // k_seg_run_quad with one lane per segment (throughput shape: >= 2^18
 // segments, e.g. the 2^24 commit's 4096 rows x 128 segments)
-template <class F>
+template <class F, bool PK = true>
 __global__ void __launch_bounds__(64) k_seg_run_lane(const Xyzz<F>* __restrict__ buckets, uint32_t nb, uint32_t L,
                                                      size_t nseg, Xyzz<F>* __restrict__ S_out,
                                                      Xyzz<F>* __restrict__ Tn) {
@@ -1386,7 +1422,7 @@ __global__ void __launch_bounds__(64) k_seg_run_lane(const Xyzz<F>* __restrict__
   const size_t base = g * nb + (size_t)k * L;
   Xyzz<C> acc = Xyzz<C>::inf(), sum = Xyzz<C>::inf();
   for (int b = (int)L - 1; b >= 0; b--) {
-    acc = add(acc, load_acc(buckets, base + b));
+    acc = add(acc, load_in<PK>(buckets, base + b));
     sum = add(sum, acc);
   }
   store_acc(S_out, t, sum);
@@ -1449,7 +1485,7 @@ static hipError_t reduce_buckets2(Arena& ar, hipStream_t s, const Xyzz<F>* d_buc
   else
     k_seg_run_quad<F><<<grid_for(4 * nseg, 64), 64, 0, s>>>(d_buckets, nb, L1, nseg, Sk, Tn, prio);
   TPST_TRY(hipGetLastError());
-  TPST_TRY(reduce_buckets<F>(ar, s, Tn, groups, S1, R, prio));
+  TPST_TRY(reduce_buckets<F>(ar, s, Tn, groups, S1, R, prio, false));  // Tn: a reduction's output
   TPST_TRY(sum_groups<F>(ar, s, Sk, groups, S1, SS, prio));
   k_lift_add_quad<F><<<grid_for(4 * groups, 64), 64, 0, s>>>(SS, R, RED2_LG, groups, d_group_out, prio);
   return hipGetLastError();
@@ -1663,7 +1699,7 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
       }();
       const unsigned grid = grid_for(gchunks, 64);
       if (lds && rec29)
-        k_bucket_acc_short_lds<2, true><<<grid, 64, 0, bulk>>>(keys, vals, range, wlo, whi, sent, bstart, bend, gb,
+        k_bucket_acc_short_lds<TPST_K2_MINW, true><<<grid, 64, 0, bulk>>>(keys, vals, range, wlo, whi, sent, bstart, bend, gb,
                                                                 nullptr, gnb, lg, buckets, part);
       else if (lds)
         k_bucket_acc_short_lds<2, false><<<grid, 64, 0, bulk>>>(keys, vals, range, wlo, whi, sent, bstart, bend,
@@ -2159,7 +2195,7 @@ hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint3
   pf->begin(ST_BUCKET_ACC, s);
   // the LDS-staged gathers (2^24 commit 68.7-69.3 -> 68.6-68.8 ms against
   // k_bucket_acc_chunk<Fq, 2, true>'s register prefetch, profiles/r05/l)
-  k_bucket_acc_chunk_lds<2><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys, entries, m, nullptr, (uint32_t)nbk, bstart, bend,
+  k_bucket_acc_chunk_lds<TPST_K1_MINW><<<(unsigned)nblk, ACC_BLOCK, 0, s>>>(keys, entries, m, nullptr, (uint32_t)nbk, bstart, bend,
                                                                   t.d_table, lg, buckets, part, bpart);
   TPST_TRY(hipGetLastError());
   k_bucket_fixup<Fq><<<grid_for(nblk, 64), 64, 0, s>>>(keys, m, nullptr, (uint32_t)nbk, bstart, bend, lg, nblk,
@@ -2191,5 +2227,6 @@ template hipError_t points_to_mont<Fq2>(hipStream_t, const uint32_t*, uint32_t*,
 template hipError_t affine_from_mont<Fq2>(hipStream_t, const uint32_t*, uint32_t*, size_t);
 template hipError_t xyzz_to_affine_canonical<Fq2>(hipStream_t, const Xyzz<Fq2>*, uint32_t*, size_t);
 #endif
+#endif  // TPST_MSM_LAB
 
 }  // namespace tpst

@@ -8,6 +8,8 @@
 #   pmc     PMC passes (FETCH_SIZE, WRITE_SIZE, VALU, stall counters) on the MSM bench
 #   k1pmc   PMC passes (FETCH_SIZE, WRITE_SIZE, VALU) on the 2^24 commit (K1)
 #   solo    per-rank latency of the sharded opening (tools/shard_open_solo.py, W = 2/4/8)
+#   valu    VALU slots / busy / divergence PMC pass of K2 (MSM bench) and K1 (2^24 commit)
+#   icache  instruction-cache PMC pass of the MSM bench
 #   list    rocprofv3 -L (available counters)
 # Every GPU step runs under its own time limit; the first failure ends the script.
 set -o pipefail
@@ -42,6 +44,16 @@ for step in "$@"; do
       timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_BUSY_CYCLES --output-format csv -d $OUT/pmc_stall -o run -- python3 $SHORT > $OUT/pmc_stall.log 2>&1 || exit 1
       cd $R && python tools/pmc_summary.py $OUT/pmc_bucket_acc_short.json $OUT/pmc_fetch $OUT/pmc_write $OUT/pmc_valu $OUT/prof_msm > $OUT/pmc_summary.log 2>&1
       cd $R && python tools/pmc_stall.py $OUT/pmc_stall.json $OUT/pmc_stall > $OUT/pmc_stall_summary.log 2>&1 ;;
+    valu)
+      cd /tmp
+      timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_INT32 SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_valu2 -o run -- python3 $SHORT > $OUT/pmc_valu2.log 2>&1 || exit 1
+      cd $R && python tools/pmc_valu.py $OUT/pmc_valu_k2.json $OUT/pmc_valu2 k_bucket_acc_short 3 k_mb_fq29 > $OUT/pmc_valu_k2.log 2>&1
+      cd /tmp
+      timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_INT32 SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $OUT/k1_valu2 -o run -- python3 $K1 > $OUT/k1_valu2.log 2>&1 || exit 1
+      cd $R && python tools/pmc_valu.py $OUT/pmc_valu_k1.json $OUT/k1_valu2 k_bucket_acc_chunk_lds 1 > $OUT/pmc_valu_k1.log 2>&1 ;;
+    icache)
+      cd /tmp
+      timeout -s KILL 120 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQ_IFETCH --output-format csv -d $OUT/pmc_icache -o run -- python3 $SHORT > $OUT/pmc_icache.log 2>&1 || exit 1 ;;
     k1pmc)
       cd /tmp
       timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/k1_fetch -o run -- python3 $K1 > $OUT/k1_fetch.log 2>&1 || exit 1
