@@ -56,10 +56,20 @@ BYTES_PER_PAIR = 128           # 32 B scalar + 96 B affine base
 LIMB_PRODUCTS_PER_FQ_MUL = 325
 MB_FQMUL_KIND = 12  # tpst_microbench kind of that product (kind 0: field.h's 12 x 32-bit product)
 SEED = 0x7E57D0
-PMC_FILE = os.path.join(ROOT, "profiles", "r05", "final", "pmc_bucket_acc_short.json")
-PMC_FILE_K1 = os.path.join(ROOT, "profiles", "r05", "final", "pmc_bucket_acc_chunk_2p24.json")
-if not os.path.exists(PMC_FILE):  # the latest round that has one
-    PMC_FILE = os.path.join(ROOT, "profiles", "r03", "pmc_bucket_acc_short.json")
+def _latest(*rel):
+    """The newest round's copy of a committed profile file (profiles/r06 first)."""
+    for r in ("r06", "r05/final", "r03"):
+        f = os.path.join(ROOT, "profiles", r, *rel)
+        if os.path.exists(f):
+            return f
+    return os.path.join(ROOT, "profiles", "r06", *rel)
+
+
+PMC_FILE = _latest("pmc_bucket_acc_short.json")
+PMC_FILE_K1 = _latest("pmc_bucket_acc_chunk_2p24.json")
+# VALU issue-slot passes (tools/pmc_valu.py): SQ_INSTS_VALU + SQ_INSTS_VALU_INT64
+PMC_VALU_K2 = _latest("pmc_valu_k2.json")
+PMC_VALU_K1 = _latest("pmc_valu_k1.json")
 
 
 def parse():
@@ -122,6 +132,31 @@ def fq_mults_per_madd(pmc=None):
     if pmc and pmc.get("fq_mul_equiv_per_madd"):
         return float(pmc["fq_mul_equiv_per_madd"])
     return 12.0
+
+
+def valu_slots(path, kernel_ms, rates):
+    """VALU issue-slot fraction of an accumulation kernel from its committed
+    PMC pass (tools/pmc_valu.py: SQ_INSTS_VALU + SQ_INSTS_VALU_INT64 slots per
+    launch group, v_mad_u64_u32 counting two) over this run's kernel time,
+    against the live-measured v_add_u32 issue rate (one slot per instruction)."""
+    if not os.path.exists(path):
+        return {}
+    try:
+        d = json.load(open(path))
+    except ValueError:
+        return {}
+    slots = d.get("issue_slots")
+    if not slots or not kernel_ms:
+        return {}
+    rate = slots / (kernel_ms * 1e-3)
+    return {"valu_slots_per_group": slots, "valu_int64_frac": round(d.get("int64_frac_of_valu") or 0.0, 4),
+            "valu_slot_frac": round(rate / rates["v_add_u32"], 4),
+            "valu_busy_frac_pmc": round(d["valu_busy_frac"], 4) if d.get("valu_busy_frac") else None,
+            "valu_utilization_pmc": round(d["valu_utilization"], 4) if d.get("valu_utilization") else None,
+            "valu_slots_source": os.path.relpath(path, ROOT),
+            "valu_slot_note": ("slots = SQ_INSTS_VALU + SQ_INSTS_VALU_INT64 (v_mad_u64_u32 issues over two slots) "
+                               "per launch group of the PMC pass / this run's kernel time, over the measured "
+                               "v_add_u32 chip issue rate")}
 
 
 def issue_rates(ctx):
@@ -338,10 +373,12 @@ def main():
                if pmc and pmc.get("fq_mul_equiv_per_madd") else "formula (8M + 2S + adds)"}
     if pmc and pmc.get("valu_insts_per_launch"):
         rate = pmc["valu_insts_per_launch"] / (acc_avg_ms * 1e-3)
-        compute.update({"valu_wave_insts_per_launch": pmc["valu_insts_per_launch"],
+        compute.update({"valu_wave_insts_per_msm": pmc["valu_insts_per_launch"],
                         "valu_issue_per_s": rate, "valu_issue_peak_per_s": rates["v_add_u32"],
                         "valu_issue_peak_source": "v_add_u32 chip issue rate, measured",
-                        "valu_issue_frac": round(rate / rates["v_add_u32"], 4)})
+                        "valu_issue_frac": round(rate / rates["v_add_u32"], 4),
+                        "valu_issue_frac_note": "instructions, not issue slots (v_mad_u64_u32 = 2 slots)"})
+    compute.update(valu_slots(PMC_VALU_K2, acc_avg_ms, rates))
 
     result = {
         "metric": METRIC,
@@ -362,7 +399,8 @@ def main():
                    "parallelism": "independent MSM per rank" if world > 1 else "1 GPU"},
         "parity_ok": parity_ok,
         "latency_ms_single_call": round(latency_ms, 4),
-        "pipelining": ("consecutive tpst_g1_msm_dev calls overlap on three library streams with three arenas: "
+        "pipelining": ("consecutive tpst_g1_msm_dev_async calls (the pipelined entry point; tpst_g1_msm_dev is "
+                       "the stream-ordered one) overlap on three library streams with three arenas: "
                        "call i+1's scalar decomposition and sort run under call i's bucket accumulation, its "
                        "accumulation under call i's last-window-group tail (fixup, bucket reduction, window chain, "
                        "affine output); ms_per_step is the steady state, latency_ms_single_call one call "
@@ -371,11 +409,17 @@ def main():
         "roofline": {"bound": "valu-int32", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                      "traffic_source": (os.path.relpath(PMC_FILE, ROOT) if pmc else None),
-                     "kernel": "k_bucket_acc_short_lds<2, true> (G1, 128-B records staged through LDS; 3 window-group launches per MSM)", "alg_bytes_per_launch": alg_bytes,
-                     "kernel_avg_ms": round(acc_avg_ms, 4),
-                     "note": "HBM column secondary: the kernel is bound by 32-bit integer VALU issue"},
+                     "kernel": "k_bucket_acc_short_lds (G1, 128-B records staged through LDS; 3 window-group launches per MSM)",
+                     "alg_bytes_per_msm": alg_bytes, "kernel_ms_per_msm": round(acc_avg_ms, 4), "launches_per_msm": 3,
+                     "note": ("per MSM = the sum over its 3 window-group launches (bytes and time alike, so achieved "
+                              "is the per-launch ratio); HBM column secondary: the kernel is bound by 32-bit integer "
+                              "VALU issue (compute.valu_slot_frac)")},
         "compute": compute,
     }
+    if world > 1 and os.environ.get("TPST_BENCH_SHARED_GPU") == "1":
+        result["rehearsal"] = ("%d ranks sharing %d GPU(s) over gloo (TPST_BENCH_SHARED_GPU=1): a correctness "
+                               "rehearsal of the multi-rank legs; the timings are NOT scaling numbers"
+                               % (world, max(1, torch.cuda.device_count())))
     if split is not None:
         result["msm_split"] = split
     if sharded20 is not None:
@@ -698,13 +742,18 @@ def sharded_leg(ctx, log_n, dist, dev, reps=5):
                 pmc = json.load(open(PMC_FILE_K1))
             except ValueError:
                 pmc = None
-        res["roofline_k1"] = {"bound": "valu-int32 / random gathers", "kernel": "k_bucket_acc_chunk_lds<2> + fixup",
+        # the PMC files hold the one-GPU 2^24 commit (4096 rows): quoted only
+        # when this rank accumulates the same rows
+        same = pmc is not None and world == 1 and log_n == 24
+        res["roofline_k1"] = {"bound": "valu-int32 / random gathers", "kernel": "k_bucket_acc_chunk_lds + fixup",
                               "achieved": round(alg / acc_s / 1e9, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(alg / acc_s / 1e9 / HBM_PEAK_GBS, 6), "alg_bytes_per_launch": alg,
                               "kernel_ms": round(k1["bucket_acc"], 4),
-                              "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
-                              "traffic_source": os.path.relpath(PMC_FILE_K1, ROOT) if pmc else None,
-                              "gather_bytes_per_launch": pmc.get("gather_bytes_per_launch") if pmc else None}
+                              "traffic": pmc.get("hbm_bytes_per_launch") if same else None,
+                              "traffic_source": os.path.relpath(PMC_FILE_K1, ROOT) if same else None,
+                              "gather_bytes_per_launch": pmc.get("gather_bytes_per_launch") if same else None}
+        if world == 1 and log_n == 24:
+            res["roofline_k1"].update(valu_slots(PMC_VALU_K1, k1["bucket_acc"], issue_rates(ctx)))
     return res
 
 

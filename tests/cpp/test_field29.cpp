@@ -3,7 +3,8 @@
 // 12 x u32 hex, possibly unreduced below 64 p) print
 //   mul, sqr, add, sub, to_std(from_std(a)), inv(a),
 //   mul_sum(a, b, a, a) = ab + a^2, mul_sub(a, b, b, b) = ab - b^2,
-//   pack377(a) (= a 2^377 mod p as a plain integer), unpack377(pack377(a))  for reduced a, b
+//   pack377(a) (= a 2^377 mod p as a plain integer), unpack377(pack377(a)),
+//   cneg(a, 1) = -a, cneg(a, 0) = a  for reduced a, b
 //   the wave engine's stage product / square               for wide a, b
 #include <cstdio>
 #include <cstring>
@@ -46,6 +47,8 @@ int main() {
       pack377(x, w.v);
       put(w);
       put(to_std(unpack377(w.v)));
+      put(to_std(cneg(x, true)));
+      put(to_std(cneg(x, false)));
     }
   }
   return 0;

@@ -45,10 +45,10 @@ def test_field29_ops_and_inverse(exe):
     vals += [(rng.randrange(P), rng.randrange(P)) for _ in range(2000)]
     out = _run(exe, [(0, a * R % P, b * R % P) for a, b in vals])
     for k, (a, b) in enumerate(vals):
-        got = [_parse(out[10 * k + j]) for j in range(10)]
+        got = [_parse(out[12 * k + j]) for j in range(12)]
         exp = [a * b % P * R % P, a * a % P * R % P, (a + b) % P * R % P, (a - b) % P * R % P, a * R % P,
                (pow(a, -1, P) * R % P) if a else 0, (a * b + a * a) % P * R % P, (a * b - b * b) % P * R % P,
-               a * (1 << 377) % P, a * R % P]
+               a * (1 << 377) % P, a * R % P, (-a) % P * R % P, a * R % P]
         assert got == exp, (a, b)
 
 

@@ -129,6 +129,26 @@ TPST_HD Fq29 sub(const Fq29& a, const Fq29& b) {
 }
 
 TPST_HD Fq29 neg(const Fq29& a) { return sub(Fq29::zero(), a); }
+
+// c ? -a : a for canonical a: p - a in one borrow pass (a = 0 stays 0) -- the
+// sign of a gathered point in the accumulation loops, where neg's second pass
+// (the conditional add of p) is dead weight
+TPST_HD Fq29 cneg(const Fq29& a, bool c) {
+  Fq29 r;
+  int32_t br = 0;
+  uint32_t nz = 0;
+#pragma unroll
+  for (int i = 0; i < r29::N; i++) {
+    const int32_t d = (int32_t)r29::P[i] - (int32_t)a.v[i] + br;
+    r.v[i] = (uint32_t)d & r29::M;
+    br = d >> 29;
+    nz |= a.v[i];
+  }
+  const bool take = c && nz != 0;
+#pragma unroll
+  for (int i = 0; i < r29::N; i++) r.v[i] = take ? r.v[i] : a.v[i];
+  return r;
+}
 TPST_HD Fq29 mul3(const Fq29& a) { return add(dbl(a), a); }
 
 // Montgomery product a b 2^-377 mod p, product scanning: column k gathers its

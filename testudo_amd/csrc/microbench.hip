@@ -25,7 +25,9 @@ __global__ void k_mb_fqmul(int iters, uint32_t* out) {
 
 // ---- single-instruction issue rates: 8 independent chains per lane -------
 // kind 6: v_mad_u64_u32, 7: v_mad_u32_u24, 8: v_mul_lo_u32, 9: v_add_u32,
-// 10: v_fma_f64, 11: v_mul_hi_u32 (iters x 4 x 8 instructions per lane)
+// 10: v_fma_f64, 11: v_mul_hi_u32 (iters x 4 x 8 instructions per lane);
+// kinds 112..115 (tpst_microbench): 12 v_lshl_add_u64, 13 v_lshrrev_b64,
+// 14 v_alignbit_b32, 15 v_add3_u32
 template <int K>
 __global__ void k_mb_insn(int iters, uint32_t* out) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -56,6 +58,14 @@ __global__ void k_mb_insn(int iters, uint32_t* out) {
           asm volatile("v_add_u32 %0, %0, %1" : "+v"(a32[j]) : "v"(x));
         } else if constexpr (K == 10) {
           asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(f[j]) : "v"(fx), "v"(fy));
+        } else if constexpr (K == 12) {  // the column carry add of the radix-2^29 product
+          asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(a64[j]) : "v"(a64[(j + 1) & 7]));
+        } else if constexpr (K == 13) {  // the column shift acc >>= 29
+          asm volatile("v_lshrrev_b64 %0, 29, %0" : "+v"(a64[j]));
+        } else if constexpr (K == 14) {
+          asm volatile("v_alignbit_b32 %0, %0, %1, 29" : "+v"(a32[j]) : "v"(x));
+        } else if constexpr (K == 15) {
+          asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a32[j]) : "v"(x), "v"(y));
         } else {
           asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a32[j]) : "v"(x));
         }
@@ -474,6 +484,14 @@ extern "C" int tpst_microbench(tpst_ctx* ctx, int kind, size_t threads, int iter
     k_mb_inv_wave<<<grid_for(threads, 64), 64, 0, ctx->stream>>>(iters, d);
   else if (kind == 13)
     k_mb_madd29<<<grid, bs, 0, ctx->stream>>>(iters, d);
+  else if (kind == 112)
+    k_mb_insn<12><<<grid, bs, 0, ctx->stream>>>(iters, d);
+  else if (kind == 113)
+    k_mb_insn<13><<<grid, bs, 0, ctx->stream>>>(iters, d);
+  else if (kind == 114)
+    k_mb_insn<14><<<grid, bs, 0, ctx->stream>>>(iters, d);
+  else if (kind == 115)
+    k_mb_insn<15><<<grid, bs, 0, ctx->stream>>>(iters, d);
   else if (kind >= 16 && kind < 16 + wave::N_OPS) {
     const int op = kind - 16;
     const size_t lds = (((wave::OP_LEN[op] + 3) & ~3u) + (size_t)(wave::N_CONSTS + 64 + 4 * 48) * wave::SLOT) * 4;

@@ -579,7 +579,7 @@ __device__ __forceinline__ Affine<Fq29> fetch_rec29(const uint32_t* table, uint3
     p.x.v[i] = w[i];
     p.y.v[i] = w[r29::N + i];
   }
-  if (v >> 31) p.y = neg(p.y);
+  p.y = cneg(p.y, (v >> 31) != 0);
   return p;
 }
 
@@ -729,7 +729,7 @@ __global__ void __launch_bounds__(ACC_BLOCK, MINW)
       p.x.v[i] = w[i];
       p.y.v[i] = w[r29::N + i];
     }
-    if (v >> 31) p.y = neg(p.y);
+    p.y = cneg(p.y, (v >> 31) != 0);
     return p;
   };
   uint32_t tail_key = sent;
@@ -934,7 +934,7 @@ __global__ void __launch_bounds__(64, MINW)
         p.x.v[i] = w[i];
         p.y.v[i] = w[r29::N + i];
       }
-      if (v >> 31) p.y = neg(p.y);
+      p.y = cneg(p.y, (v >> 31) != 0);
       return p;
     } else {
       Affine<Fq> p = {Fq::from_limbs(w), Fq::from_limbs(w + 12)};
@@ -1471,16 +1471,21 @@ static size_t reduce2_scratch(size_t groups, uint32_t nb) {
          Arena::need(groups * S1 / 64 + 1, sizeof(Xyzz<F>)) + 2 * Arena::need(groups, sizeof(Xyzz<F>));
 }
 
+#ifndef TPST_RED2_LANE
+#define TPST_RED2_LANE 1
+#endif
+// lane_ok: a throughput reduction (under other accumulation work) -- one lane
+// per segment costs fewer VALU issue slots per addition than a quad
 template <class F>
 static hipError_t reduce_buckets2(Arena& ar, hipStream_t s, const Xyzz<F>* d_buckets, size_t groups, uint32_t nb,
-                                  Xyzz<F>* d_group_out, int prio) {
+                                  Xyzz<F>* d_group_out, int prio, bool lane_ok = false) {
   const uint32_t L1 = 1u << RED2_LG, S1 = nb / L1;
   const size_t nseg = groups * S1;
   Xyzz<F>* Sk = ar.take<Xyzz<F>>(nseg);
   Xyzz<F>* Tn = ar.take<Xyzz<F>>(nseg);
   Xyzz<F>* R = ar.take<Xyzz<F>>(groups);
   Xyzz<F>* SS = ar.take<Xyzz<F>>(groups);
-  if (std::is_same<F, Fq>::value && nseg >= ((size_t)1 << 18))
+  if (std::is_same<F, Fq>::value && (nseg >= ((size_t)1 << 18) || (TPST_RED2_LANE && lane_ok)))
     k_seg_run_lane<F><<<grid_for(nseg, 64), 64, 0, s>>>(d_buckets, nb, L1, nseg, Sk, Tn);
   else
     k_seg_run_quad<F><<<grid_for(4 * nseg, 64), 64, 0, s>>>(d_buckets, nb, L1, nseg, Sk, Tn, prio);
@@ -1733,7 +1738,7 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
     TPST_TRY(hipGetLastError());
     if (g == 0) break;
     if (red2_ok(nb))
-      TPST_TRY(reduce_buckets2<F>(ar, a, buckets + b0, (size_t)(whi - wlo), nb, win + wlo, RED_PRIO));
+      TPST_TRY(reduce_buckets2<F>(ar, a, buckets + b0, (size_t)(whi - wlo), nb, win + wlo, RED_PRIO, true));
     else
       TPST_TRY(reduce_buckets<F>(ar, a, buckets + b0, (size_t)(whi - wlo), nb, win + wlo, RED_PRIO));
     k_window_chain<F><<<1, 64, 0, a>>>(win, wlo, whi, c, nullptr, 0, contrib + g);

@@ -50,7 +50,7 @@ def main():
         "fetch_size_kb_per_msm": f_kb, "write_size_kb_per_msm": w_kb,
         "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE as reported; KB = 1024 B",
         "hbm_bytes_per_launch": (2 * f_kb + w_kb) * 1024.0,
-        "hbm_bytes_note": "per MSM (all window-group launches of one call), the unit of kernel_avg_ms",
+        "hbm_bytes_note": "per MSM (all window-group launches of one call), the unit of bench.py kernel_ms_per_msm",
         "valu_insts_per_launch": per_msm(valu),
         "per_grid_avg_fetch_kb": {str(g): avg(v) for g, v in fetch.items()},
         "note": "FETCH counts fabric requests incl. Infinity-Cache hits: bases gathered once per window entry",
