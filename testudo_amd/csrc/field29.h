@@ -177,11 +177,11 @@ TPST_HD Fq29 mul(const Fq29& a, const Fq29& b) {
     }
     if (k < N) {
       m[k] = (0u - (uint32_t)acc) & r29::M;
-      acc += m[k];
+      acc = (acc + r29::M) >> 29;  // = (acc + m_k) / 2^29 = ceil(acc / 2^29): independent of m_k
     } else {
       t[k - N] = (uint32_t)acc & r29::M;
+      acc >>= 29;
     }
-    acc >>= 29;
   }
   t[N - 1] = (uint32_t)acc;  // < 2^30: t < 2p
   Fq29 r;
@@ -215,11 +215,11 @@ TPST_HD Fq29 mul_sum(const Fq29& a, const Fq29& b, const Fq29& c, const Fq29& d)
     }
     if (k < N) {
       m[k] = (0u - (uint32_t)acc) & r29::M;
-      acc += m[k];
+      acc = (acc + r29::M) >> 29;  // = (acc + m_k) / 2^29 = ceil(acc / 2^29): independent of m_k
     } else {
       t[k - N] = (uint32_t)acc & r29::M;
+      acc >>= 29;
     }
-    acc >>= 29;
   }
   t[N - 1] = (uint32_t)acc;  // < 2^31: t < 2.7 p
   Fq29 r;
@@ -230,8 +230,25 @@ TPST_HD Fq29 mul_sum(const Fq29& a, const Fq29& b, const Fq29& c, const Fq29& d)
   return r;
 }
 
-// a b - c d for canonical operands: one reduction (mul_sum with p - d)
-TPST_HD Fq29 mul_sub(const Fq29& a, const Fq29& b, const Fq29& c, const Fq29& d) { return mul_sum(a, b, c, neg(d)); }
+// p - a in one borrow pass for a <= p (p - 0 = p is fine as a mul_sum
+// operand: its limbs are 29-bit and p = 0 mod p)
+TPST_HD Fq29 p_minus(const Fq29& a) {
+  Fq29 r;
+  int32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < r29::N; i++) {
+    const int32_t d = (int32_t)r29::P[i] - (int32_t)a.v[i] + br;
+    r.v[i] = (uint32_t)d & r29::M;
+    br = d >> 29;
+  }
+  return r;
+}
+
+// a b - c d for canonical operands: one reduction (mul_sum with p - d; the
+// sum stays < 2.7 p with d = p too)
+TPST_HD Fq29 mul_sub(const Fq29& a, const Fq29& b, const Fq29& c, const Fq29& d) {
+  return mul_sum(a, b, c, p_minus(d));
+}
 
 // square: cross products a_i a_j (i < j) once, doubled per column
 TPST_HD Fq29 sqr(const Fq29& a) {
@@ -255,11 +272,11 @@ TPST_HD Fq29 sqr(const Fq29& a) {
     }
     if (k < N) {
       m[k] = (0u - (uint32_t)acc) & r29::M;
-      acc += m[k];
+      acc = (acc + r29::M) >> 29;  // = (acc + m_k) / 2^29 = ceil(acc / 2^29): independent of m_k
     } else {
       t[k - N] = (uint32_t)acc & r29::M;
+      acc >>= 29;
     }
-    acc >>= 29;
   }
   t[N - 1] = (uint32_t)acc;
   Fq29 r;

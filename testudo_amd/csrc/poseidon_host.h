@@ -45,10 +45,18 @@ const HostP64& hp64() {
   return h;
 }
 
+// (host pass only: a HIP device pass defines __x86_64__ too)
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+#define TPST_HOST_ADX 1
+#include "host_mont_adx.inc"
+#else
+#define TPST_HOST_ADX 0
+#endif
+
 // no-carry CIOS (p's top word < 2^62: the running value fits 6 words + the
 // carry word of each row), fully unrolled over the 6 words of b
 template <bool LAZY = false>
-Fq hmul(const Fq& a, const Fq& b) {
+Fq hmul_cxx(const Fq& a, const Fq& b) {
   typedef unsigned __int128 u128;
   const HostP64& P = hp64();
   uint64_t x[6], y[6];
@@ -176,7 +184,7 @@ __attribute__((always_inline)) inline void mac12(uint64_t* t, const uint64_t* x,
 // are added unreduced (3 p^2 < p R) and reduced once, so an MDS row costs
 // three multiplications and one REDC instead of three of each
 template <bool LAZY = false>
-Fq hmul3(const Fq& a0, const Fq& b0, const Fq& a1, const Fq& b1, const Fq& a2, const Fq& b2) {
+Fq hmul3_cxx(const Fq& a0, const Fq& b0, const Fq& a1, const Fq& b1, const Fq& a2, const Fq& b2) {
   uint64_t t[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, x[6], y[6];
   memcpy(x, a0.v, 48);
   memcpy(y, b0.v, 48);
@@ -193,7 +201,7 @@ Fq hmul3(const Fq& a0, const Fq& b0, const Fq& a1, const Fq& b1, const Fq& a2, c
 // Montgomery square: the 15 cross products once, doubled, plus the 6
 // squares, then the REDC -- the S-box's x^2, x^4, x^8, x^16
 template <bool LAZY = false>
-Fq hsqr(const Fq& a) {
+Fq hsqr_cxx(const Fq& a) {
   typedef unsigned __int128 u128;
   uint64_t x[6];
   memcpy(x, a.v, 48);
@@ -276,6 +284,23 @@ inline Fq hadd_lazy(const Fq& a, const Fq& b) {
   return out;
 }
 
+// a + b without reduction (the sum < 2^384)
+inline Fq hadd_raw(const Fq& a, const Fq& b) {
+  typedef unsigned __int128 u128;
+  uint64_t x[6], y[6], t[6];
+  memcpy(x, a.v, 48);
+  memcpy(y, b.v, 48);
+  u128 c = 0;
+  for (int j = 0; j < 6; j++) {
+    c += (u128)x[j] + y[j];
+    t[j] = (uint64_t)c;
+    c >>= 64;
+  }
+  Fq out;
+  memcpy(out.v, t, 48);
+  return out;
+}
+
 // x < 2p -> canonical
 inline Fq hcanon(const Fq& a) {
   typedef unsigned __int128 u128;
@@ -291,6 +316,76 @@ inline Fq hcanon(const Fq& a) {
   Fq out;
   memcpy(out.v, br ? t : r, 48);
   return out;
+}
+
+// t - m if t >= m (6 words; t < 2^384)
+inline Fq sub_if_ge(const Fq& a, const uint64_t* m) {
+  typedef unsigned __int128 u128;
+  uint64_t t[6], r[6];
+  memcpy(t, a.v, 48);
+  u128 br = 0;
+  for (int j = 0; j < 6; j++) {
+    const u128 d = (u128)t[j] - m[j] - (uint64_t)br;
+    r[j] = (uint64_t)d;
+    br = (d >> 64) & 1;
+  }
+  Fq out;
+  memcpy(out.v, br ? t : r, 48);
+  return out;
+}
+
+// The products the transcript's permutations run on: MULX / ADCX / ADOX
+// assembly (host_mont_adx.inc, generated by tools/gen_mont_adx.py) where the
+// host CPU has BMI2 + ADX -- 2.3x faster than the __int128 CIOS above
+// (tests/cpp/test_mont_adx.cpp: 58 vs 136 ns on the build container) -- else
+// the C++ forms.  Every MIPP round's Poseidon absorption of t_l / t_r sits on
+// the opening's critical path (~13 permutations of ~500 products).
+inline bool host_adx() {
+#if TPST_HOST_ADX
+  // (__builtin_cpu_init first: a shared library's code may run before the
+  // runtime's own CPU-model constructor has)
+  static const bool ok = [] {
+    __builtin_cpu_init();
+    return __builtin_cpu_supports("adx") && __builtin_cpu_supports("bmi2");
+  }();
+  return ok;
+#else
+  return false;
+#endif
+}
+
+template <bool LAZY = false>
+Fq hmul(const Fq& a, const Fq& b) {
+#if TPST_HOST_ADX
+  if (host_adx()) {  // < a b / R + p < 1.03 p for a, b < 2p
+    Fq r;
+    mont_mul_adx(reinterpret_cast<uint64_t*>(r.v), reinterpret_cast<const uint64_t*>(a.v),
+                 reinterpret_cast<const uint64_t*>(b.v), hp64().p, hp64().inv);
+    return LAZY ? r : hcanon(r);
+  }
+#endif
+  return hmul_cxx<LAZY>(a, b);
+}
+
+template <bool LAZY = false>
+Fq hsqr(const Fq& a) {
+  if (host_adx()) return hmul<LAZY>(a, a);
+  return hsqr_cxx<LAZY>(a);
+}
+
+// the sum of the three products: each < 1.03 p from the ADX product, the sum
+// < 3.1 p, brought below 2p (LAZY) or below p
+template <bool LAZY = false>
+Fq hmul3(const Fq& a0, const Fq& b0, const Fq& a1, const Fq& b1, const Fq& a2, const Fq& b2) {
+  if (host_adx()) {
+    const Fq s = hadd_raw(hadd_raw(hmul<true>(a0, b0), hmul<true>(a1, b1)), hmul<true>(a2, b2));
+    uint64_t p2[6];
+    const HostP64& P = hp64();
+    for (int j = 0; j < 6; j++) p2[j] = (P.p[j] << 1) | (j ? P.p[j - 1] >> 63 : 0);
+    const Fq r = sub_if_ge(s, p2);  // < 2p
+    return LAZY ? r : hcanon(r);
+  }
+  return hmul3_cxx<LAZY>(a0, b0, a1, b1, a2, b2);
 }
 
 // x^17 (alpha = 17), lazy: x < 2p in, < 2p out

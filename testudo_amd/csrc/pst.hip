@@ -1,5 +1,6 @@
 // sqrt-PST protocol kernels for gfx950 (see pst_kernels.h).
 #include "device_util.h"
+#include "inv_wave.h"
 #include "pst_kernels.h"
 #include <cstdlib>
 
@@ -209,10 +210,27 @@ __global__ void __launch_bounds__(64, 1) k_xyzz_to_affine_mont(const Xyzz<F>* __
 // (one inverse per wave by Montgomery's batch trick across the lanes was
 // measured within noise for the h vector of the opening: not kept)
 
+// one wave per point, the wave-cooperative inverse (inv_wave.h): the
+// latency-bound conversions of the opening (the h vector each round before
+// its G2 preparation, <= C / 2 points; the gathered a^(r1))
+template <class F>
+__global__ void __launch_bounds__(64) k_xyzz_to_affine_mont_wave(const Xyzz<F>* __restrict__ in,
+                                                                 uint32_t* __restrict__ out, size_t n) {
+  const size_t i = blockIdx.x;
+  if (i >= n) return;
+  const Affine<F> a = to_affine_w(load_xyzz(in, i));
+  if (threadIdx.x == 0) store_affine(out, i, a);
+}
+
+constexpr size_t MONT_WAVE_MAX = 4096;
+
 template <class F>
 hipError_t xyzz_to_affine_mont(hipStream_t s, const Xyzz<F>* d_in, uint32_t* d_out, size_t n) {
   if (!n) return hipSuccess;
-  k_xyzz_to_affine_mont<F><<<grid_for(n, 64), 64, 0, s>>>(d_in, d_out, n);
+  if (n <= MONT_WAVE_MAX)
+    k_xyzz_to_affine_mont_wave<F><<<(unsigned)n, 64, 0, s>>>(d_in, d_out, n);
+  else
+    k_xyzz_to_affine_mont<F><<<grid_for(n, 64), 64, 0, s>>>(d_in, d_out, n);
   return hipGetLastError();
 }
 

@@ -92,5 +92,6 @@ int main() {
          " (check %llx)\n",
          (t1 - t0) / N * 1e-3, (t2 - t1) / N * 1e-3, (t4 - t3) / M, (t5 - t4) / M, (t6 - t5) / M, (t7 - t6) / M,
          (unsigned long long)(a.v[0] ^ ref[0].v[0]));
+  printf("host products: %s\n", host_adx() ? "MULX/ADCX/ADOX assembly" : "C++ __int128");
   return 0;
 }
