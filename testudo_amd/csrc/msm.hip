@@ -1738,7 +1738,10 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
     TPST_TRY(hipGetLastError());
     if (g == 0) break;
     if (red2_ok(nb))
-      TPST_TRY(reduce_buckets2<F>(ar, a, buckets + b0, (size_t)(whi - wlo), nb, win + wlo, RED_PRIO, true));
+      // lane form (fewer issue slots) for the groups with slack; the group
+      // before the last keeps the quads: its tail ends right after the last
+      // group's in a lone call
+      TPST_TRY(reduce_buckets2<F>(ar, a, buckets + b0, (size_t)(whi - wlo), nb, win + wlo, RED_PRIO, g >= 2));
     else
       TPST_TRY(reduce_buckets<F>(ar, a, buckets + b0, (size_t)(whi - wlo), nb, win + wlo, RED_PRIO));
     k_window_chain<F><<<1, 64, 0, a>>>(win, wlo, whi, c, nullptr, 0, contrib + g);
@@ -1747,7 +1750,15 @@ hipError_t msm_var(Arena& ar, hipStream_t s, const uint32_t* d_bases, const uint
   }
   const int w1 = wb[1];  // group 0 = windows [0, w1)
   pf->begin(ST_REDUCE, t0);
-  TPST_TRY(reduce_buckets<F>(ar, t0, buckets, (size_t)w1, nb, win));  // the latency-bound short-segment one
+#ifndef TPST_G0_RED2
+#define TPST_G0_RED2 0  // 1: the two-level form for the last group (slower: 285-290 vs 295 Mscalar/s, a lone call 5.5 vs 5.1 ms, profiles/r06/ab_g0_red2.jsonl)
+#endif
+  // the last group's reduction is the call's tail: the two-level form (no
+  // per-segment scalar multiplications; quads) or the short-segment one
+  if (TPST_G0_RED2 && red2_ok(nb))
+    TPST_TRY(reduce_buckets2<F>(ar, t0, buckets, (size_t)w1, nb, win, 0, false));
+  else
+    TPST_TRY(reduce_buckets<F>(ar, t0, buckets, (size_t)w1, nb, win));
   pf->end(ST_REDUCE, t0);
   pf->begin(ST_COMBINE, t0);
   for (int g = 1; g < NG; g++) TPST_TRY(hipStreamWaitEvent(t0, ar.aux_ev[2 * g + 1], 0));

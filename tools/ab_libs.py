@@ -23,6 +23,7 @@ def run(label, path):
                        env=env, timeout=300)
     mb = [json.loads(x) for x in m.stdout.splitlines() if x.startswith("{")]
     return {"label": label, "value": d.get("value"), "ms_per_step": d.get("ms_per_step"),
+            "latency_ms": d.get("latency_ms_single_call"),
             "stages": d.get("stages_ms_per_step"), "mb": {x["op"]: [x["chip_G_per_s"], x["lone_wave_us"]] for x in mb}}
 
 
