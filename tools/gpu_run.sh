@@ -59,7 +59,10 @@ for step in "$@"; do
       timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/k1_fetch -o run -- python3 $K1 > $OUT/k1_fetch.log 2>&1 || exit 1
       timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/k1_write -o run -- python3 $K1 > $OUT/k1_write.log 2>&1 || exit 1
       timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES --output-format csv -d $OUT/k1_valu -o run -- python3 $K1 > $OUT/k1_valu.log 2>&1 || exit 1
-      cd $R && python tools/pmc_k1.py $OUT/pmc_bucket_acc_chunk_2p24.json $OUT/k1_fetch $OUT/k1_write $OUT/k1_valu $OUT/prof_open24 > $OUT/pmc_k1.log 2>&1 ;;
+      cd $R && python tools/pmc_k1.py $OUT/pmc_bucket_acc_chunk_2p24.json $OUT/k1_fetch $OUT/k1_write $OUT/k1_valu $OUT/prof_open24 > $OUT/pmc_k1.log 2>&1
+      cd /tmp
+      timeout -s KILL 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_BUSY_CYCLES --output-format csv -d $OUT/k1_stall -o run -- python3 $K1 > $OUT/k1_stall.log 2>&1 || exit 1
+      cd $R && python tools/pmc_stall.py $OUT/pmc_stall_k1.json $OUT/k1_stall k_bucket_acc_chunk_lds > $OUT/pmc_stall_k1_summary.log 2>&1 ;;
     solo)
       cd $R && for w in 2 4 8; do timeout -k 10 300 python -u tools/shard_open_solo.py 24 $w 5 >> $OUT/shard_open_solo.jsonl 2>> $OUT/shard_open_solo.err || exit 1; done
       cd $R && timeout -k 10 300 python -u tools/shard_open_solo.py 20 8 5 >> $OUT/shard_open_solo.jsonl 2>> $OUT/shard_open_solo.err || exit 1 ;;
