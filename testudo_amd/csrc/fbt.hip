@@ -191,18 +191,28 @@ __global__ void __launch_bounds__(64) k_fbt_partial_quad(const uint32_t* __restr
     }
     int carry = 0;
     for (int w = 0; w < wb; w++) fbt_digit(s, w, carry);
+    // the next lookup is in flight during the current addition; the phi
+    // chunks sum the lookups of T and map the sum once (phi(sum T_j) =
+    // sum phi(T_j), phi(X, Y, ZZ, ZZZ) = (beta X, Y, ZZ, ZZZ))
+    auto look = [&](int w, int d) { return load_affine<F>(table, (k * nw + w) * FBT_M + (d < 0 ? -d : d) - 1); };
+    int dn = fbt_digit(s, wb, carry);
+    Affine<F> nx;
+    if (dn) nx = look(wb, dn);
     for (int j = 0; j < 8; j++) {
-      const int w = wb + j;
-      const int d = fbt_digit(s, w, carry);
+      const Affine<F> cur = nx;
+      const int d = dn;
+      if (j + 1 < 8) {
+        dn = fbt_digit(s, wb + j + 1, carry);
+        if (dn) nx = look(wb + j + 1, dn);
+      }
       if (d) {
-        Affine<F> ts = load_affine<F>(table, (k * nw + w) * FBT_M + (d < 0 ? -d : d) - 1);
-        if constexpr (sizeof(F) == sizeof(Fq)) {
-          if (phi) ts.x = mul(ts.x, Fq::from_limbs(params::G1_BETA));
-        }
-        Affine<C> t = A::in(ts);
+        Affine<C> t = A::in(cur);
         if (d < 0) t = neg(t);
         acc = add_affine_quad(acc, t, qi);
       }
+    }
+    if constexpr (sizeof(F) == sizeof(Fq)) {
+      if (phi) acc.X = mul(acc.X, A::in(Affine<F>{Fq::from_limbs(params::G1_BETA), Fq::zero()}).x);
     }
   }
   if (qi == 0) store_acc(partial, i, acc);

@@ -1124,7 +1124,8 @@ static int open_streams(tpst_ctx* ctx, size_t n_events, size_t pinned_bytes, boo
   // the row-sharded opening's collectives, in one issue order on every rank
   if (comm && !ctx->comm) TPST_HIP(ctx, hipStreamCreateWithPriority(&ctx->comm, hipStreamNonBlocking, greatest));
   // the per-round h preparation of the opening (its own hardware queue: on
-  // stream A it delayed the next round's t; 2^20 open 13.0 -> 11.4 ms)
+  // stream A it delayed the next round's t; 2^20 open 13.0 -> 11.4 ms; at
+  // the least priority 11.05 -> 11.30 ms, profiles/r06/ab/ab_open_c_prio.txt)
   if (!ctx->side_c) TPST_HIP(ctx, hipStreamCreateWithPriority(&ctx->side_c, hipStreamNonBlocking, greatest));
   while (ctx->events.size() < n_events) {
     hipEvent_t e;
@@ -1601,11 +1602,44 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
       Ca = len;
     }
 
-    // -- B: y fold by the previous challenge, cross MSMs u_l / u_r
-    // (u_l = a[:s]^y[s:], u_r = a[s:]^y[:s], on the comm_list table); B is
-    // enqueued first: its comms_u gate the transcript, and the look-ahead
-    // enqueue below costs the host tens of launches
     uint8_t* dn_r = pin + dn_round + (size_t)r * DN_ROUND;
+    // -- A: t_l / t_r of this round, enqueued before B from round 1 on (the
+    // combination gates the odd rounds and needs only the upload, while B's
+    // table MSM costs the host tens of microseconds to enqueue; 2^20 open
+    // 11.40 -> 11.25 ms, 2^24 25.5 -> 24.9 ms, profiles/r06/ab/ab_open_order_prio.txt)
+    auto enqueue_a = [&]() -> int {
+      if (r == 0) {  // direct: the rotated comm_list (affine) against h^(0)
+        if (loc) {  // this rank's pairs (a_i, h_{s+i}), (a_{s+i}, h_i), i = rho mod W
+          TPST_HIP(ctx, affine_rot(sA, A.u(), P.u(), Cl, 24));
+          arA.reset();
+          TPST_HIP(ctx, arA.reserve(multi_pairing_scratch(2, s / W)));
+          const Slot sl = slot(2 * sizeof(Fq12));
+          TPST_HIP(ctx, multi_pairing_prepared(arA, sA, P.u(), H0l, L0l, 2, s / W, (Fq12*)sl.send, false, s / W, 0));
+          if (int rc = gather(sA, sl, 2 * sizeof(Fq12))) return rc;
+          TPST_HIP(ctx, gt_prod_final(sA, (const Fq12*)sl.recv, W, 2, (Fq12*)gts.p));
+        } else {
+          TPST_HIP(ctx, affine_rot(sA, A.u(), P.u(), C, 24));
+          arA.reset();
+          TPST_HIP(ctx, arA.reserve(multi_pairing_scratch(2, s)));
+          TPST_HIP(ctx, multi_pairing_prepared(arA, sA, P.u(), H0, L0, 2, s, (Fq12*)gts.p, true, s, 0));
+        }
+      } else {  // round r-1's look-ahead products, combined with c_{r-1}
+        TPST_HIP(ctx, hipStreamWaitEvent(sA, ev_la(r - 1), 0));
+        TPST_HIP(ctx, mipp_combine_tab(sA, (Fq12*)SqT[(r - 1) & 1].p, ddig, (Fq12*)SqG[(r - 1) & 1].p,
+                                       (Fq12*)SqM.p, (Fq12*)gts.p));
+      }
+      TPST_HIP(ctx, fq12_from_mont(sA, (Fq12*)gts.p, canA.u(), 2));
+      TPST_HIP(ctx, hipMemcpyAsync(dn_r + 2 * X1, canA.p, 1152, hipMemcpyDeviceToHost, sA));
+      TPST_HIP(ctx, hipEventRecord(ev_a(r), sA));
+      return TPST_OK;
+    };
+    const bool a_first = r > 0;
+    if (a_first)
+      if (int rc = enqueue_a()) return rc;
+    // -- B: y fold by the previous challenge, cross MSMs u_l / u_r
+    // (u_l = a[:s]^y[s:], u_r = a[s:]^y[:s], on the comm_list table); B goes
+    // before the look-ahead: its comms_u gate the transcript, and the
+    // look-ahead enqueue below costs the host tens of launches
     TPST_HIP(ctx, hipStreamWaitEvent(sB, ev_up(r), 0));
     if (r > 0) TPST_HIP(ctx, compress_fr(sB, Y.u(), len, dcp));  // y_l + c' y_r (mipp.rs:124-136)
     {  // (round 0 as two variable-base K2 MSMs over comm_list, skipping the
@@ -1634,31 +1668,8 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
     TPST_HIP(ctx, hipMemcpyAsync(dn_r, xb.p, 2 * X1, hipMemcpyDeviceToHost, sB));
     TPST_HIP(ctx, hipEventRecord(ev_b(r), sB));
     const double hb = open_trace() ? host_us() : 0.0;
-    // -- A: t_l / t_r of this round
-    if (r == 0) {  // direct: the rotated comm_list (affine) against h^(0)
-      if (loc) {  // this rank's pairs (a_i, h_{s+i}), (a_{s+i}, h_i), i = rho mod W
-        TPST_HIP(ctx, affine_rot(sA, A.u(), P.u(), Cl, 24));
-        arA.reset();
-        TPST_HIP(ctx, arA.reserve(multi_pairing_scratch(2, s / W)));
-        const Slot sl = slot(2 * sizeof(Fq12));
-        TPST_HIP(ctx, multi_pairing_prepared(arA, sA, P.u(), H0l, L0l, 2, s / W, (Fq12*)sl.send, false, s / W, 0));
-        if (int rc = gather(sA, sl, 2 * sizeof(Fq12))) return rc;
-        TPST_HIP(ctx, gt_prod_final(sA, (const Fq12*)sl.recv, W, 2, (Fq12*)gts.p));
-      } else {
-        TPST_HIP(ctx, affine_rot(sA, A.u(), P.u(), C, 24));
-        arA.reset();
-        TPST_HIP(ctx, arA.reserve(multi_pairing_scratch(2, s)));
-        TPST_HIP(ctx, multi_pairing_prepared(arA, sA, P.u(), H0, L0, 2, s, (Fq12*)gts.p, true, s, 0));
-      }
-    } else {  // round r-1's look-ahead products, combined with c_{r-1}
-      TPST_HIP(ctx, hipStreamWaitEvent(sA, ev_la(r - 1), 0));
-      TPST_HIP(ctx, mipp_combine_tab(sA, (Fq12*)SqT[(r - 1) & 1].p, ddig, (Fq12*)SqG[(r - 1) & 1].p,
-                                     (Fq12*)SqM.p, (Fq12*)gts.p));
-    }
-    TPST_HIP(ctx, fq12_from_mont(sA, (Fq12*)gts.p, canA.u(), 2));
-    TPST_HIP(ctx, hipMemcpyAsync(dn_r + 2 * X1, canA.p, 1152, hipMemcpyDeviceToHost, sA));
-    TPST_HIP(ctx, hipEventRecord(ev_a(r), sA));
-
+    if (!a_first)
+      if (int rc = enqueue_a()) return rc;
     const double ha = open_trace() ? host_us() : 0.0;
     // -- D: look-ahead products of this round's vectors for round r+1
     if (len >= 4) {
