@@ -148,6 +148,15 @@ struct DevBuf {
     return b ? hipMalloc(&p, b) : hipSuccess;
   }
   uint32_t* u() const { return (uint32_t*)p; }
+  // grow-only: keep the buffer when it is large enough
+  hipError_t grow(size_t b) { return (p && bytes >= b) ? hipSuccess : alloc(b); }
+};
+
+// the opening's device buffers, kept across openings (grow-only): ~40
+// hipMalloc / hipFree pairs per call cost the host ~0.4 ms
+struct OpenBufs {
+  DevBuf up, A, P, Y, chiC, ScA, ScB, ScC, ScD[2], xa, xb, xd, xh, xp, xl[2], LAo[2], Hb[3], Lb[3], gts, canA, canC,
+      canD, pstA, pstB, Wall, Wiall, SqT[2], SqG[2], SqM, chis_own, tLoc, A1x, A1, tA1, Hbl[3], Lbl[3];
 };
 
 }  // namespace
@@ -180,6 +189,7 @@ struct SrsState {
   // canonical row commitments; consumed by the next opening of them
   std::vector<uint64_t> t_A_key;
   std::vector<uint64_t> flat;     // canonical export
+  OpenBufs ob;                    // the opening's device buffers (grow-only)
   ~SrsState() { batch_tables_free(tables); }
 };
 
@@ -699,10 +709,12 @@ extern "C" int tpst_poly_commit(tpst_ctx* ctx, tpst_poly* p, uint64_t* comms, ui
   if (int rc = poly_need_full(ctx, p)) return rc;
   TPST_HIP(ctx, hipSetDevice(ctx->device));
   const size_t C = (size_t)1 << p->m_col;
-  DevBuf cm, tt, out;
-  TPST_HIP(ctx, cm.alloc(C * 96));
-  TPST_HIP(ctx, tt.alloc(sizeof(Fq12)));
-  TPST_HIP(ctx, out.alloc(C * 96 + 576));
+  ctx->io.reset();  // (grow-only: no per-call hipMalloc / hipFree)
+  TPST_HIP(ctx, ctx->io.reserve(Arena::need(C * 24, 4) + Arena::need(1, sizeof(Fq12)) +
+                                Arena::need(C * 24 + 144, 4) + 512));
+  uint32_t* cm = ctx->io.take<uint32_t>(C * 24);
+  Fq12* tt = ctx->io.take<Fq12>(1);
+  uint32_t* out = ctx->io.take<uint32_t>(C * 24 + 144);
   // the table build runs beside the IPP (2^20: commit + open 21.7 -> 21.2
   // ms); at C = 4096 it outlasts the IPP by ~2 ms but leaves the opening's
   // first round free of it.  TPST_COMMIT_TABLE=0: the opening builds it
@@ -711,13 +723,13 @@ extern "C" int tpst_poly_commit(tpst_ctx* ctx, tpst_poly* p, uint64_t* comms, ui
     return e ? atoi(e) : -1;
   }();
   const bool prebuild = table_env != 0;
-  int rc = poly_commit_dev(ctx, p, cm.u(), (Fq12*)tt.p, prebuild);
+  int rc = poly_commit_dev(ctx, p, cm, tt, prebuild);
   if (rc) return rc;
   hipStream_t s = ctx->stream;
-  TPST_HIP(ctx, affine_from_mont<Fq>(s, cm.u(), out.u(), C));
-  TPST_HIP(ctx, fq12_from_mont(s, (Fq12*)tt.p, out.u() + 24 * C, 1));
-  TPST_HIP(ctx, hipMemcpyAsync(comms, out.p, C * 96, hipMemcpyDeviceToHost, s));
-  TPST_HIP(ctx, hipMemcpyAsync(T, out.u() + 24 * C, 576, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, affine_from_mont<Fq>(s, cm, out, C));
+  TPST_HIP(ctx, fq12_from_mont(s, tt, out + 24 * C, 1));
+  TPST_HIP(ctx, hipMemcpyAsync(comms, out, C * 96, hipMemcpyDeviceToHost, s));
+  TPST_HIP(ctx, hipMemcpyAsync(T, out + 24 * C, 576, hipMemcpyDeviceToHost, s));
   TPST_HIP(ctx, hipStreamSynchronize(s));
   if (prebuild) srs_of(ctx)->t_A_key.assign(comms, comms + 12 * C);
   return TPST_OK;
@@ -1281,7 +1293,8 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
   const size_t dn_fh = dn_final + X1, dn_ph = dn_fh + X2, dn_pst = dn_ph + (size_t)m * 96;
   const size_t dn_bytes = X1 + (size_t)m * DN_ROUND + X1 + X2 + (size_t)m * 96 + (size_t)k * 192;
   const size_t n_ev = 8 + 6 * (size_t)m + (shd ? 8 * (size_t)m + 8 : 0);
-  if (int rc = open_streams(ctx, n_ev, up_bytes + dn_bytes, shd)) return rc;
+  const size_t cm_off = up_bytes + dn_bytes;  // comm_list staging (unsharded form)
+  if (int rc = open_streams(ctx, n_ev, cm_off + (shd ? 0 : C * 96), shd)) return rc;
   uint8_t* pin = (uint8_t*)ctx->pinned;
   // five streams: A (critical), B (cross terms), two look-ahead streams for
   // alternating rounds (consecutive look-aheads overlap, each taking longer
@@ -1358,56 +1371,56 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
   // ---- device buffers (allocated before any stream runs: no hipFree mid-open)
   const size_t Ch = C > 1 ? C / 2 : 1;
   const size_t Ca0 = shd ? Cl : C;  // a-side bases resident: own rows or all
-  DevBuf up, A, P, Y, chiC, ScA, ScB, ScC, ScD[2], xa, xb, xd, xh, xp, xl[2], LAo[2], Hb[3], Lb[3], gts, canA, canC,
-      canD, pstA, pstB, Wall, Wiall, SqT[2], SqG[2], SqM, chis_own, tLoc, A1x, A1, tA1, Hbl[3], Lbl[3];
-  TPST_HIP(ctx, up.alloc(up_bytes));
-  TPST_HIP(ctx, Wall.alloc(2 * C * 32));  // round r's 2^r fold weights at offset 2^r - 1
-  TPST_HIP(ctx, Wiall.alloc(2 * C * 32));
-  TPST_HIP(ctx, A.alloc(Ca0 * 96));
-  TPST_HIP(ctx, P.alloc(Ca0 * 96));
-  TPST_HIP(ctx, Y.alloc(C * 32));
-  TPST_HIP(ctx, chiC.alloc(C * 32));
-  TPST_HIP(ctx, ScA.alloc(2 * C * 32));
-  TPST_HIP(ctx, ScB.alloc(C * 32));
-  TPST_HIP(ctx, ScC.alloc(C * 32));
-  TPST_HIP(ctx, xa.alloc(C * sizeof(Xyzz<Fq>)));
-  TPST_HIP(ctx, xb.alloc(2 * sizeof(Xyzz<Fq>)));
-  TPST_HIP(ctx, xd.alloc((k + 1) * sizeof(Xyzz<Fq2>)));
-  TPST_HIP(ctx, xh.alloc(C * sizeof(Xyzz<Fq2>)));
-  TPST_HIP(ctx, xp.alloc(((size_t)m + 1) * sizeof(Xyzz<Fq>)));
+  auto& [up, A, P, Y, chiC, ScA, ScB, ScC, ScD, xa, xb, xd, xh, xp, xl, LAo, Hb, Lb, gts, canA, canC, canD, pstA, pstB,
+         Wall, Wiall, SqT, SqG, SqM, chis_own, tLoc, A1x, A1, tA1, Hbl, Lbl] = st->ob;
+  TPST_HIP(ctx, up.grow(up_bytes));
+  TPST_HIP(ctx, Wall.grow(2 * C * 32));  // round r's 2^r fold weights at offset 2^r - 1
+  TPST_HIP(ctx, Wiall.grow(2 * C * 32));
+  TPST_HIP(ctx, A.grow(Ca0 * 96));
+  TPST_HIP(ctx, P.grow(Ca0 * 96));
+  TPST_HIP(ctx, Y.grow(C * 32));
+  TPST_HIP(ctx, chiC.grow(C * 32));
+  TPST_HIP(ctx, ScA.grow(2 * C * 32));
+  TPST_HIP(ctx, ScB.grow(C * 32));
+  TPST_HIP(ctx, ScC.grow(C * 32));
+  TPST_HIP(ctx, xa.grow(C * sizeof(Xyzz<Fq>)));
+  TPST_HIP(ctx, xb.grow(2 * sizeof(Xyzz<Fq>)));
+  TPST_HIP(ctx, xd.grow((k + 1) * sizeof(Xyzz<Fq2>)));
+  TPST_HIP(ctx, xh.grow(C * sizeof(Xyzz<Fq2>)));
+  TPST_HIP(ctx, xp.grow(((size_t)m + 1) * sizeof(Xyzz<Fq>)));
   for (int i = 0; i < 3; i++) {  // prepared h^(r) in slot r % 3
-    TPST_HIP(ctx, Hb[i].alloc(Ch * 192));
-    TPST_HIP(ctx, Lb[i].alloc(Ch * N_LINE_COEFFS * sizeof(LineCoeff)));
+    TPST_HIP(ctx, Hb[i].grow(Ch * 192));
+    TPST_HIP(ctx, Lb[i].grow(Ch * N_LINE_COEFFS * sizeof(LineCoeff)));
     if (shd) {
-      TPST_HIP(ctx, Hbl[i].alloc((Ch / W ? Ch / W : 1) * 192));
-      TPST_HIP(ctx, Lbl[i].alloc((Ch / W ? Ch / W : 1) * N_LINE_COEFFS * sizeof(LineCoeff)));
+      TPST_HIP(ctx, Hbl[i].grow((Ch / W ? Ch / W : 1) * 192));
+      TPST_HIP(ctx, Lbl[i].grow((Ch / W ? Ch / W : 1) * N_LINE_COEFFS * sizeof(LineCoeff)));
     }
   }
-  TPST_HIP(ctx, gts.alloc(2 * sizeof(Fq12)));
+  TPST_HIP(ctx, gts.grow(2 * sizeof(Fq12)));
   for (int i = 0; i < 2; i++) {
-    TPST_HIP(ctx, ScD[i].alloc(8 * C * 32));
-    TPST_HIP(ctx, xl[i].alloc(C * sizeof(Xyzz<Fq>)));
-    TPST_HIP(ctx, LAo[i].alloc(8 * sizeof(Fq12)));
+    TPST_HIP(ctx, ScD[i].grow(8 * C * 32));
+    TPST_HIP(ctx, xl[i].grow(C * sizeof(Xyzz<Fq>)));
+    TPST_HIP(ctx, LAo[i].grow(8 * sizeof(Fq12)));
     // sized for either engine (RNS form: rns::RES_WORDS u32 per Fq12)
-    TPST_HIP(ctx, SqT[i].alloc(4 * 64 * MIPP_TAB_F12_BYTES));
-    TPST_HIP(ctx, SqG[i].alloc(2 * 10 * MIPP_TAB_F12_BYTES));
+    TPST_HIP(ctx, SqT[i].grow(4 * 64 * MIPP_TAB_F12_BYTES));
+    TPST_HIP(ctx, SqG[i].grow(2 * 10 * MIPP_TAB_F12_BYTES));
   }
-  TPST_HIP(ctx, SqM.alloc(128 * MIPP_TAB_F12_BYTES));
-  TPST_HIP(ctx, canA.alloc(2 * 576));
-  TPST_HIP(ctx, canC.alloc((size_t)(m + 1) * 192));
-  TPST_HIP(ctx, canD.alloc(96 + (size_t)k * 192));
-  TPST_HIP(ctx, pstA.alloc(pst_open_scratch_words(st, m) * 4));
-  TPST_HIP(ctx, pstB.alloc(pst_open_scratch_words(st, k) * 4));
+  TPST_HIP(ctx, SqM.grow(128 * MIPP_TAB_F12_BYTES));
+  TPST_HIP(ctx, canA.grow(2 * 576));
+  TPST_HIP(ctx, canC.grow((size_t)(m + 1) * 192));
+  TPST_HIP(ctx, canD.grow(96 + (size_t)k * 192));
+  TPST_HIP(ctx, pstA.grow(pst_open_scratch_words(st, m) * 4));
+  TPST_HIP(ctx, pstB.grow(pst_open_scratch_words(st, k) * 4));
   if (!shd && st->t_A_n < C) {
     TPST_HIP(ctx, st->t_A.alloc(fbt_words<Fq>(C) * 4));
     st->t_A_n = C;
   }
   if (shd) {
-    TPST_HIP(ctx, tLoc.alloc(fbt_words<Fq>(Cl) * 4));
+    TPST_HIP(ctx, tLoc.grow(fbt_words<Fq>(Cl) * 4));
     const size_t len1 = C >> r1;
-    TPST_HIP(ctx, A1x.alloc(len1 * X1));
-    TPST_HIP(ctx, A1.alloc(len1 * 96));
-    TPST_HIP(ctx, tA1.alloc(fbt_words<Fq>(len1) * 4));
+    TPST_HIP(ctx, A1x.grow(len1 * X1));
+    TPST_HIP(ctx, A1.grow(len1 * 96));
+    TPST_HIP(ctx, tA1.grow(fbt_words<Fq>(len1) * 4));
   }
   {  // G2 preparation scratch: the prepared h^(r) (global: <= C / 2 points, a rank's: <= C / 2W)
     size_t mx = 0;
@@ -1463,7 +1476,8 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
     TPST_HIP(ctx, hipMemcpyAsync(A.p, own.data(), Cl * 96, hipMemcpyHostToDevice, sA));
     TPST_HIP(ctx, hipStreamSynchronize(sA));  // `own` is pageable and local
   } else {
-    TPST_HIP(ctx, hipMemcpyAsync(A.p, comms, C * 96, hipMemcpyHostToDevice, sA));  // pageable: staged by HIP
+    memcpy(pin + cm_off, comms, C * 96);  // pinned: an asynchronous copy, not HIP's pageable staging
+    TPST_HIP(ctx, hipMemcpyAsync(A.p, pin + cm_off, C * 96, hipMemcpyHostToDevice, sA));
   }
   TPST_HIP(ctx, points_to_mont<Fq>(sA, A.u(), A.u(), Ca0));
   const uint32_t* chis = nullptr;
@@ -1566,7 +1580,9 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
     uint32_t* dW = Wall.u() + 8 * (nW - 1);
     uint32_t* dWi = Wiall.u() + 8 * (nW - 1);
     TPST_HIP(ctx, hipEventRecord(ev_up(r), sB));
-    TPST_HIP(ctx, hipStreamWaitEvent(sA, ev_up(r), 0));
+    // (round 0's A and D work -- the direct t and the first look-ahead --
+    // needs no upload: they do not wait behind B's U MSM)
+    if (r > 0) TPST_HIP(ctx, hipStreamWaitEvent(sA, ev_up(r), 0));
 
     if (shd && r == r1) {
       // -- hand-over: a^(r1) (len = 2W positions) folded by the owners of its
@@ -1675,7 +1691,7 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
     if (len >= 4) {
       hipStream_t sD = sLA[r & 1];
       Arena& arD = *arLA[r & 1];
-      TPST_HIP(ctx, hipStreamWaitEvent(sD, ev_up(r), 0));
+      if (r > 0) TPST_HIP(ctx, hipStreamWaitEvent(sD, ev_up(r), 0));
       if (ev_t1) TPST_HIP(ctx, hipStreamWaitEvent(sD, ev_t1, 0));
       const size_t ln = loc ? len / W : len;  // positions this rank pairs
       arD.reset();
