@@ -140,8 +140,78 @@ __device__ __forceinline__ int fbt_digit(const uint32_t* s, int w, int& carry) {
   return carry ? d - 16 : d;
 }
 
-// quad of lanes (coop.h) per (group, member, chunk): sum of the 8 lookups of
-// windows [8 chunk, 8 chunk + 8)
+// quad of lanes (coop.h): sum of the lookups of windows [8 ch + j0, 8 ch +
+// j0 + nj) of member m of group g in scalar set q
+template <class F>
+__device__ __forceinline__ Xyzz<typename AccField<F>::T> fbt_lookups(const uint32_t* __restrict__ table,
+                                                                      const uint32_t* __restrict__ scal,
+                                                                      const FbGroups& gr, size_t q, size_t g, size_t m,
+                                                                      int ch, int j0, int nj, int qi) {
+  using A = AccField<F>;
+  using C = typename A::T;
+  size_t k;
+  if (gr.d_seg) {
+    const size_t lo = gr.d_seg[g], hi = gr.d_seg[g + 1];
+    if (m >= hi - lo) return Xyzz<C>::inf();
+    k = lo + m;
+  } else {
+    k = (m / gr.D) * gr.L + g * gr.D + m % gr.D;
+  }
+  Xyzz<C> acc = Xyzz<C>::inf();
+  uint32_t s[8];
+  const uint4* sp = reinterpret_cast<const uint4*>(scal + 8 * (k + q * gr.set_stride));
+  const uint4 a = sp[0], b = sp[1];
+  s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w;
+  s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
+  // GLV table: chunks 0-3 take k1's windows from T, chunks 4-7 k2's from
+  // phi(T) = (beta x, y)
+  int wb = 8 * ch, nw = FBT_W;
+  bool phi = false;
+  if constexpr (sizeof(F) == sizeof(Fq)) {
+    if (gr.glv) {
+      uint32_t k1[4], k2[4];
+      glv_split(s, k1, k2);
+      phi = ch >= 4;
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        s[t] = phi ? k2[t] : k1[t];
+        s[4 + t] = 0;
+      }
+      wb = 8 * (ch & 3);
+      nw = FBT_WG;
+    }
+  }
+  wb += j0;
+  int carry = 0;
+  for (int w = 0; w < wb; w++) fbt_digit(s, w, carry);
+  // the next lookup is in flight during the current addition; the phi
+  // chunks sum the lookups of T and map the sum once (phi(sum T_j) =
+  // sum phi(T_j), phi(X, Y, ZZ, ZZZ) = (beta X, Y, ZZ, ZZZ))
+  auto look = [&](int w, int d) { return load_affine<F>(table, (k * nw + w) * FBT_M + (d < 0 ? -d : d) - 1); };
+  int dn = fbt_digit(s, wb, carry);
+  Affine<F> nx;
+  if (dn) nx = look(wb, dn);
+  for (int j = 0; j < nj; j++) {
+    const Affine<F> cur = nx;
+    const int d = dn;
+    if (j + 1 < nj) {
+      dn = fbt_digit(s, wb + j + 1, carry);
+      if (dn) nx = look(wb + j + 1, dn);
+    }
+    if (d) {
+      Affine<C> t = A::in(cur);
+      if (d < 0) t = neg(t);
+      acc = add_affine_quad(acc, t, qi);
+    }
+  }
+  if constexpr (sizeof(F) == sizeof(Fq)) {
+    if (phi) acc.X = mul(acc.X, A::in(Affine<F>{Fq::from_limbs(params::G1_BETA), Fq::zero()}).x);
+  }
+  return acc;
+}
+
+// quad of lanes per (group, member, chunk): sum of the 8 lookups of windows
+// [8 chunk, 8 chunk + 8)
 template <class F>
 __global__ void __launch_bounds__(64) k_fbt_partial_quad(const uint32_t* __restrict__ table,
                                                          const uint32_t* __restrict__ scal, FbGroups gr,
@@ -153,93 +223,75 @@ __global__ void __launch_bounds__(64) k_fbt_partial_quad(const uint32_t* __restr
   const size_t per_set = gr.groups * gr.members;
   const size_t qgm = i >> 3, q = qgm / per_set, gm = qgm % per_set;
   const size_t g = gm / gr.members, m = gm % gr.members;
-  size_t k;
-  bool valid = true;
-  if (gr.d_seg) {
-    const size_t lo = gr.d_seg[g], hi = gr.d_seg[g + 1];
-    valid = m < hi - lo;
-    k = lo + m;
-  } else {
-    k = (m / gr.D) * gr.L + g * gr.D + m % gr.D;
-  }
-  using A = AccField<F>;
-  using C = typename A::T;
-  Xyzz<C> acc = Xyzz<C>::inf();
-  if (valid) {
-    uint32_t s[8];
-    const uint4* sp = reinterpret_cast<const uint4*>(scal + 8 * (k + q * gr.set_stride));
-    const uint4 a = sp[0], b = sp[1];
-    s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w;
-    s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
-    // GLV table: chunks 0-3 take k1's windows from T, chunks 4-7 k2's from
-    // phi(T) = (beta x, y)
-    int wb = 8 * ch, nw = FBT_W;
-    bool phi = false;
-    if constexpr (sizeof(F) == sizeof(Fq)) {
-      if (gr.glv) {
-        uint32_t k1[4], k2[4];
-        glv_split(s, k1, k2);
-        phi = ch >= 4;
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-          s[t] = phi ? k2[t] : k1[t];
-          s[4 + t] = 0;
-        }
-        wb = 8 * (ch & 3);
-        nw = FBT_WG;
-      }
-    }
-    int carry = 0;
-    for (int w = 0; w < wb; w++) fbt_digit(s, w, carry);
-    // the next lookup is in flight during the current addition; the phi
-    // chunks sum the lookups of T and map the sum once (phi(sum T_j) =
-    // sum phi(T_j), phi(X, Y, ZZ, ZZZ) = (beta X, Y, ZZ, ZZZ))
-    auto look = [&](int w, int d) { return load_affine<F>(table, (k * nw + w) * FBT_M + (d < 0 ? -d : d) - 1); };
-    int dn = fbt_digit(s, wb, carry);
-    Affine<F> nx;
-    if (dn) nx = look(wb, dn);
-    for (int j = 0; j < 8; j++) {
-      const Affine<F> cur = nx;
-      const int d = dn;
-      if (j + 1 < 8) {
-        dn = fbt_digit(s, wb + j + 1, carry);
-        if (dn) nx = look(wb + j + 1, dn);
-      }
-      if (d) {
-        Affine<C> t = A::in(cur);
-        if (d < 0) t = neg(t);
-        acc = add_affine_quad(acc, t, qi);
-      }
-    }
-    if constexpr (sizeof(F) == sizeof(Fq)) {
-      if (phi) acc.X = mul(acc.X, A::in(Affine<F>{Fq::from_limbs(params::G1_BETA), Fq::zero()}).x);
-    }
-  }
+  const auto acc = fbt_lookups<F>(table, scal, gr, q, g, m, ch, 0, 8, qi);
   if (qi == 0) store_acc(partial, i, acc);
 }
 
-// out[seg * parts + part] = sum of in[seg * seg_len + part * per .. + per),
-// BS / 4 quads per block
-template <class F, int BS>
-__global__ void __launch_bounds__(BS) k_seg_sum_quad(const Xyzz<F>* __restrict__ in, size_t seg_len, size_t per,
-                                                     size_t parts, Xyzz<F>* __restrict__ out) {
-  using C = typename AccField<F>::T;
-  constexpr int Q = BS / 4;
-  __shared__ Xyzz<C> sh[Q];
-  const int quad = threadIdx.x >> 2, qi = threadIdx.x & 3;
-  const size_t seg = blockIdx.x / parts, part = blockIdx.x % parts;
-  const size_t lo = part * per, hi = lo + per < seg_len ? lo + per : seg_len;
-  Xyzz<C> acc = Xyzz<C>::inf();
-  for (size_t j = lo + quad; j < hi; j += Q) acc = add_quad(acc, load_acc(in, seg * seg_len + j), qi);
-  if (qi == 0) sh[quad] = acc;
-  __syncthreads();
-  for (int h = Q / 2; h > 0; h >>= 1) {
-    if (quad < h) {
+// pairwise tree over the quads [0, n) of a block, n <= the block's quads:
+// sh[0] ends with the sum (n > 0)
+template <class C>
+__device__ __forceinline__ void quad_tree(Xyzz<C>* sh, int n, int quad, int qi) {
+  int h = 1;
+  while (h < n) h <<= 1;
+  for (h >>= 1; h > 0; h >>= 1) {
+    if (quad < h && quad + h < n) {
       const Xyzz<C> v = add_quad(sh[quad], sh[quad + h], qi);
       if (qi == 0) sh[quad] = v;
     }
     __syncthreads();
   }
+}
+
+// workgroup size: four waves, one per SIMD (two waves per SIMD doubled every
+// addition's latency: 2^24 open 24.0 -> 26.8 ms)
+template <class F>
+constexpr int fbt_block() { return 256; }
+
+// one workgroup per (set, group) of few members: quad u sums the lpq lookups
+// of unit u = (member, chunk, sub-chunk), then a tree in LDS -- lpq + log2
+// (units) serial additions in one launch instead of 8 + the two-launch
+// segmented tree
+template <class F>
+__global__ void __launch_bounds__(fbt_block<F>()) k_fbt_small_quad(const uint32_t* __restrict__ table,
+                                                                   const uint32_t* __restrict__ scal, FbGroups gr,
+                                                                   int lpq, Xyzz<F>* __restrict__ out) {
+  using C = typename AccField<F>::T;
+  __shared__ Xyzz<C> sh[fbt_block<F>() / 4];
+  const int quad = threadIdx.x >> 2, qi = threadIdx.x & 3;
+  const size_t q = blockIdx.x / gr.groups, g = blockIdx.x % gr.groups;
+  const int spc = 8 / lpq;  // units per chunk
+  const int units = (int)gr.members * 8 * spc;
+  Xyzz<C> acc = Xyzz<C>::inf();
+  if (quad < units) {
+    const int m = quad / (8 * spc), ch = (quad / spc) & 7, sub = quad % spc;
+    acc = fbt_lookups<F>(table, scal, gr, q, g, m, ch, sub * lpq, lpq, qi);
+  }
+  if (qi == 0) sh[quad] = acc;
+  __syncthreads();
+  quad_tree(sh, units, quad, qi);
+  if (threadIdx.x == 0) store_acc(out, blockIdx.x, sh[0]);
+}
+
+// out[seg * parts + part] = sum of in[seg * seg_len + part * per .. + per):
+// each quad sums its strided elements, then a tree over the quads in use
+template <class F>
+__global__ void __launch_bounds__(fbt_block<F>()) k_seg_sum_quad(const Xyzz<F>* __restrict__ in, size_t seg_len,
+                                                                 size_t per, size_t parts, Xyzz<F>* __restrict__ out) {
+  using C = typename AccField<F>::T;
+  constexpr int Q = fbt_block<F>() / 4;
+  __shared__ Xyzz<C> sh[Q];
+  const int quad = threadIdx.x >> 2, qi = threadIdx.x & 3;
+  const size_t seg = blockIdx.x / parts, part = blockIdx.x % parts;
+  const size_t lo = part * per, hi = lo + per < seg_len ? lo + per : seg_len;
+  Xyzz<C> acc = Xyzz<C>::inf();
+  size_t j = lo + quad;
+  if (j < hi) {
+    acc = load_acc(in, seg * seg_len + j);
+    for (j += Q; j < hi; j += Q) acc = add_quad(acc, load_acc(in, seg * seg_len + j), qi);
+  }
+  if (qi == 0) sh[quad] = acc;
+  __syncthreads();
+  quad_tree(sh, (int)(hi - lo < (size_t)Q ? hi - lo : (size_t)Q), quad, qi);
   if (threadIdx.x == 0) store_acc(out, blockIdx.x, sh[0]);
 }
 
@@ -247,9 +299,15 @@ template <class F>
 hipError_t fbt_msm(Arena& ar, hipStream_t s, const uint32_t* d_table, const uint32_t* d_scalars, const FbGroups& g,
                    Xyzz<F>* d_out) {
   if (!g.groups || !g.sets) return hipSuccess;
-  constexpr int BS = 128;  // 32 quads per partial sum
-  constexpr size_t R = 4;  // serial additions per quad before the tree
+  constexpr int BS = fbt_block<F>();
+  constexpr size_t Q = BS / 4;  // quads per block
   const size_t G = g.groups * g.sets;
+  if (!g.d_seg && g.members && g.members * 8 <= Q) {  // few members: one launch
+    int lpq = 1;
+    while (g.members * 8 * (8 / lpq) > Q) lpq <<= 1;
+    k_fbt_small_quad<F><<<(unsigned)G, BS, 0, s>>>(d_table, d_scalars, g, lpq, d_out);
+    return hipGetLastError();
+  }
   size_t len = g.members * 8;
   const size_t np = G * (len ? len : 1);
   ar.reset();
@@ -264,10 +322,12 @@ hipError_t fbt_msm(Arena& ar, hipStream_t s, const uint32_t* d_table, const uint
     TPST_TRY(hipGetLastError());
   }
   while (len > 1) {
-    const size_t per = BS / 4 * R;
+    // four serial additions per quad before the tree, one when a block holds
+    // the whole segment
+    const size_t per = len <= Q ? Q : 4 * Q;
     const size_t parts = (len + per - 1) / per;
     Xyzz<F>* dst = parts == 1 ? d_out : b;
-    k_seg_sum_quad<F, BS><<<(unsigned)(G * parts), BS, 0, s>>>(a, len, per, parts, dst);
+    k_seg_sum_quad<F><<<(unsigned)(G * parts), BS, 0, s>>>(a, len, per, parts, dst);
     TPST_TRY(hipGetLastError());
     if (parts == 1) return hipSuccess;
     len = parts;
