@@ -1872,9 +1872,12 @@ int msm_window_bits(size_t n) {
 }
 
 int batch_window_bits(size_t N) {
+  // rows of 1024 / 2048 scalars: 11-bit windows (2^20 commit 7.35 -> 7.05 ms
+  // against 10; 12 -> 13 at 4096 was slower, 65.2 -> 65.8 ms:
+  // profiles/r06/ab/ab_k1_window.txt)
   int lg = bit_length(N ? N - 1 : 0);
   if (lg >= 12) return 12;
-  if (lg >= 10) return 10;
+  if (lg >= 10) return 11;
   if (lg >= 6) return 7;
   return 4;
 }
