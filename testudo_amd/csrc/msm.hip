@@ -2015,11 +2015,12 @@ constexpr int SB_SPT = 4;                 // scalars per thread: N <= 4096
 constexpr uint32_t SB_NB = 2048;          // buckets per row (c <= 12)
 constexpr uint32_t SB_STAGE = 15 * 1024;  // staged entries per pass (120 KB)
 
-// WC > 0 (c = 12, W = WC = 22: the commit's row MSMs): the window loop is
-// unrolled, so every digit is a funnel shift at a constant bit offset; with a
-// runtime W the offset is runtime and the word select a chain of conditional
-// moves over the scalar's 8 words (x 7 passes over every digit of the row)
-template <int WC>
+// WC > 0 (c = CC, W = WC: the commit's row MSMs, 12 / 22 at 2^24 and 11 /
+// 24 at 2^20): the window loop is unrolled, so every digit is a funnel shift
+// at a constant bit offset; with a runtime W the offset is runtime and the
+// word select a chain of conditional moves over the scalar's 8 words (x 7
+// passes over every digit of the row; 2^20 sort 172 -> 95 us)
+template <int WC, int CC = 12>
 __global__ void __launch_bounds__(SB_THREADS) k_batch_sort_staged(const uint32_t* __restrict__ scalars, size_t rows,
                                                                  size_t N, size_t row_stride, size_t col_stride, int c,
                                                                  int W, uint32_t* __restrict__ keys,
@@ -2049,7 +2050,7 @@ __global__ void __launch_bounds__(SB_THREADS) k_batch_sort_staged(const uint32_t
     if constexpr (WC > 0) {
 #pragma unroll
       for (int w = 0; w < WC; w++) {
-        const int d = signed_digit(sc, 8, w, 12, WC, carry);
+        const int d = signed_digit(sc, 8, w, CC, WC, carry);
         if (d) atomicAdd(&cur[abs(d) - 1], 1u);
       }
     } else {
@@ -2146,7 +2147,7 @@ __global__ void __launch_bounds__(SB_THREADS) k_batch_sort_staged(const uint32_t
       uint32_t carry = 0;
       if constexpr (WC > 0) {
 #pragma unroll
-        for (int w = 0; w < WC; w++) place(signed_digit(sc, 8, w, 12, WC, carry), w, j);
+        for (int w = 0; w < WC; w++) place(signed_digit(sc, 8, w, CC, WC, carry), w, j);
       } else {
         for (int w = 0; w < W; w++) place(signed_digit(sc, 8, w, c, W, carry), w, j);
       }
@@ -2201,8 +2202,11 @@ hipError_t msm_batch(Arena& ar, hipStream_t s, const BatchTables& t, const uint3
   if (!pf) pf = &dummy;
   pf->begin(ST_BATCH_SORT, s);
   if (N <= (size_t)SB_THREADS * SB_SPT && c == 12 && W == 22)
-    k_batch_sort_staged<22><<<nrow_blk, SB_THREADS, 0, s>>>(d_scalars, rows, N, row_stride, col_stride, c, W, keys,
-                                                             entries, bstart, bend, reinterpret_cast<uint4*>(buckets));
+    k_batch_sort_staged<22, 12><<<nrow_blk, SB_THREADS, 0, s>>>(d_scalars, rows, N, row_stride, col_stride, c, W, keys,
+                                                                 entries, bstart, bend, reinterpret_cast<uint4*>(buckets));
+  else if (N <= (size_t)SB_THREADS * SB_SPT && c == 11 && W == 24)
+    k_batch_sort_staged<24, 11><<<nrow_blk, SB_THREADS, 0, s>>>(d_scalars, rows, N, row_stride, col_stride, c, W, keys,
+                                                                 entries, bstart, bend, reinterpret_cast<uint4*>(buckets));
   else if (N <= (size_t)SB_THREADS * SB_SPT && nb <= SB_NB)
     k_batch_sort_staged<0><<<nrow_blk, SB_THREADS, 0, s>>>(d_scalars, rows, N, row_stride, col_stride, c, W, keys,
                                                             entries, bstart, bend, reinterpret_cast<uint4*>(buckets));

@@ -654,6 +654,18 @@ extern "C" int tpst_poly_eval(tpst_ctx* ctx, tpst_poly* p, const uint64_t* point
 // commit (sqrt_pst.rs:117-149): K1 row MSMs + IPP T = prod e(C_i, h_i)
 static int open_streams(tpst_ctx* ctx, size_t n_events, size_t pinned_bytes, bool comm = false);
 
+// the context's pinned host staging (grow-only; the opening's per-round
+// transfers, the commit's outputs)
+static int ensure_pinned(tpst_ctx* ctx, size_t bytes) {
+  if (ctx->pinned_cap >= bytes) return TPST_OK;
+  if (ctx->pinned) TPST_HIP(ctx, hipHostFree(ctx->pinned));
+  ctx->pinned = nullptr;
+  ctx->pinned_cap = 0;
+  TPST_HIP(ctx, hipHostMalloc(&ctx->pinned, bytes, hipHostMallocDefault));
+  ctx->pinned_cap = bytes;
+  return TPST_OK;
+}
+
 // prebuild (tpst_poly_commit): also build the opening's fold table over the
 // row commitments on a side stream while the IPP runs (TPST_COMMIT_TABLE=0 /
 // 1 forces it off / on)
@@ -728,9 +740,12 @@ extern "C" int tpst_poly_commit(tpst_ctx* ctx, tpst_poly* p, uint64_t* comms, ui
   hipStream_t s = ctx->stream;
   TPST_HIP(ctx, affine_from_mont<Fq>(s, cm, out, C));
   TPST_HIP(ctx, fq12_from_mont(s, tt, out + 24 * C, 1));
-  TPST_HIP(ctx, hipMemcpyAsync(comms, out, C * 96, hipMemcpyDeviceToHost, s));
-  TPST_HIP(ctx, hipMemcpyAsync(T, out + 24 * C, 576, hipMemcpyDeviceToHost, s));
+  // one asynchronous copy into pinned staging (not two pageable ones)
+  if (int rc2 = ensure_pinned(ctx, C * 96 + 576)) return rc2;
+  TPST_HIP(ctx, hipMemcpyAsync(ctx->pinned, out, C * 96 + 576, hipMemcpyDeviceToHost, s));
   TPST_HIP(ctx, hipStreamSynchronize(s));
+  memcpy(comms, ctx->pinned, C * 96);
+  memcpy(T, (const uint8_t*)ctx->pinned + C * 96, 576);
   if (prebuild) srs_of(ctx)->t_A_key.assign(comms, comms + 12 * C);
   return TPST_OK;
 }
@@ -1144,14 +1159,7 @@ static int open_streams(tpst_ctx* ctx, size_t n_events, size_t pinned_bytes, boo
     TPST_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     ctx->events.push_back(e);
   }
-  if (ctx->pinned_cap < pinned_bytes) {
-    if (ctx->pinned) TPST_HIP(ctx, hipHostFree(ctx->pinned));
-    ctx->pinned = nullptr;
-    ctx->pinned_cap = 0;
-    TPST_HIP(ctx, hipHostMalloc(&ctx->pinned, pinned_bytes, hipHostMallocDefault));
-    ctx->pinned_cap = pinned_bytes;
-  }
-  return TPST_OK;
+  return ensure_pinned(ctx, pinned_bytes);
 }
 
 // Polynomial::open (sqrt_pst.rs:168-230) with MippProof::prove (mipp.rs:31-153).
