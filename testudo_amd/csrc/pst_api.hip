@@ -1300,9 +1300,15 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
   const size_t dn_U = up_bytes, dn_round = dn_U + X1, dn_final = dn_round + (size_t)m * DN_ROUND;
   const size_t dn_fh = dn_final + X1, dn_ph = dn_fh + X2, dn_pst = dn_ph + (size_t)m * 96;
   const size_t dn_bytes = X1 + (size_t)m * DN_ROUND + X1 + X2 + (size_t)m * 96 + (size_t)k * 192;
-  const size_t n_ev = 8 + 6 * (size_t)m + (shd ? 8 * (size_t)m + 8 : 0);
+  const size_t n_ev = 9 + 6 * (size_t)m + (shd ? 8 * (size_t)m + 8 : 0);
+  // unsharded rebase: in round rb = 4, a^(4) (C / 16 points) is tabulated
+  // (as the sharded hand-over does) on the otherwise idle comm stream, and the
+  // later rounds fold 2^(r - 4) of its points instead of C / len row
+  // commitments (2^24 open 24.4 -> 23.0 ms, 2^20 10.4 -> 10.2 ms; rebasing at
+  // len 16 / 64 at 2^24 gained less: profiles/r06/ab/ab_open_rebase.txt)
+  const int rb = !shd && m >= 8 ? 4 : -1;
   const size_t cm_off = up_bytes + dn_bytes;  // comm_list staging (unsharded form)
-  if (int rc = open_streams(ctx, n_ev, cm_off + (shd ? 0 : C * 96), shd)) return rc;
+  if (int rc = open_streams(ctx, n_ev, cm_off + (shd ? 0 : C * 96), shd || rb >= 0)) return rc;
   uint8_t* pin = (uint8_t*)ctx->pinned;
   // five streams: A (critical), B (cross terms), two look-ahead streams for
   // alternating rounds (consecutive look-aheads overlap, each taking longer
@@ -1321,14 +1327,14 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
   Arena &arA = ctx->arena, &arB = ctx->arena_side[0], &arC = ctx->arena2;
   Arena* arLA[2] = {&ctx->arena_side[1], &ctx->arena_side[2]};
   hipEvent_t* ev = ctx->events.data();
-  enum { EV_PRE, EV_TABLE, EV_U, EV_FINAL_UP, EV_B_DONE, EV_C_DONE, EV_D_DONE, EV_A_DONE };
-  auto ev_up = [&](int r) { return ev[8 + 6 * r]; };
-  auto ev_a = [&](int r) { return ev[8 + 6 * r + 1]; };
-  auto ev_b = [&](int r) { return ev[8 + 6 * r + 2]; };
-  auto ev_c = [&](int r) { return ev[8 + 6 * r + 3]; };
-  auto ev_la = [&](int r) { return ev[8 + 6 * r + 4]; };
-  auto ev_cl = [&](int r) { return ev[8 + 6 * r + 5]; };  // the rank's own h positions prepared
-  hipEvent_t* xev = ev + 8 + 6 * m;                         // exchange events (sharded form)
+  enum { EV_PRE, EV_TABLE, EV_U, EV_FINAL_UP, EV_B_DONE, EV_C_DONE, EV_D_DONE, EV_A_DONE, EV_REBASE };
+  auto ev_up = [&](int r) { return ev[9 + 6 * r]; };
+  auto ev_a = [&](int r) { return ev[9 + 6 * r + 1]; };
+  auto ev_b = [&](int r) { return ev[9 + 6 * r + 2]; };
+  auto ev_c = [&](int r) { return ev[9 + 6 * r + 3]; };
+  auto ev_la = [&](int r) { return ev[9 + 6 * r + 4]; };
+  auto ev_cl = [&](int r) { return ev[9 + 6 * r + 5]; };  // the rank's own h positions prepared
+  hipEvent_t* xev = ev + 9 + 6 * m;                         // exchange events (sharded form)
   int last_c = -1;  // the last odd round that issued h work "C"
   // the prepared h the look-ahead of round r pairs against (see above)
   auto la_src = [](int r) { return r <= 1 ? 0 : r - 1; };
@@ -1423,9 +1429,9 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
     TPST_HIP(ctx, st->t_A.alloc(fbt_words<Fq>(C) * 4));
     st->t_A_n = C;
   }
-  if (shd) {
-    TPST_HIP(ctx, tLoc.grow(fbt_words<Fq>(Cl) * 4));
-    const size_t len1 = C >> r1;
+  if (shd) TPST_HIP(ctx, tLoc.grow(fbt_words<Fq>(Cl) * 4));
+  if (shd || rb >= 0) {
+    const size_t len1 = C >> (shd ? r1 : rb);
     TPST_HIP(ctx, A1x.grow(len1 * X1));
     TPST_HIP(ctx, A1.grow(len1 * 96));
     TPST_HIP(ctx, tA1.grow(fbt_words<Fq>(len1) * 4));
@@ -1592,6 +1598,11 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
     // needs no upload: they do not wait behind B's U MSM)
     if (r > 0) TPST_HIP(ctx, hipStreamWaitEvent(sA, ev_up(r), 0));
 
+    if (rb >= 0 && r == rb + 1) {  // the rebase table from here on (B waits for it; D, A do below)
+      tA = tA1.u();
+      Ca = C >> rb;
+      TPST_HIP(ctx, hipStreamWaitEvent(sB, ev_t1, 0));
+    }
     if (shd && r == r1) {
       // -- hand-over: a^(r1) (len = 2W positions) folded by the owners of its
       // positions, gathered; rank 0 tabulates it and continues alone
@@ -1795,6 +1806,24 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
       last_c = r;
     }
 
+    if (r == rb) {  // the rebase (see rb above), consumed from round rb + 1 on
+      const hipStream_t sR = ctx->comm;
+      TPST_HIP(ctx, hipStreamWaitEvent(sR, ev_up(r), 0));
+      TPST_HIP(ctx, hipStreamWaitEvent(sR, ev[EV_TABLE], 0));
+      TPST_HIP(ctx, mipp_scalars(sR, dW, nullptr, len, 0, C, ScA.u()));
+      FbGroups g;
+      g.groups = len;
+      g.members = C / len;
+      g.L = len;
+      g.D = 1;
+      g.glv = true;
+      TPST_HIP(ctx, fbt_msm<Fq>(ctx->io, sR, tA, ScA.u(), g, (Xyzz<Fq>*)A1x.p));
+      TPST_HIP(ctx, xyzz_to_affine_mont<Fq>(sR, (const Xyzz<Fq>*)A1x.p, A1.u(), len));
+      TPST_HIP(ctx, fbt_build<Fq>(ctx->io, sR, A1.u(), len, tA1.u(), true));
+      ev_t1 = ev[EV_REBASE];
+      TPST_HIP(ctx, hipEventRecord(ev_t1, sR));
+    }
+
     // -- host: transcript (mipp.rs:56, 97-101) and the challenge
     if (!have_U) {
       TPST_HIP(ctx, hipEventSynchronize(ev[EV_U]));
@@ -1921,7 +1950,7 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
     pf.end(ST_SQRT_OPEN, sA);
   }
   for (hipStream_t s2 : {sA, sB, sLA[0], sLA[1], sC}) TPST_HIP(ctx, hipStreamSynchronize(s2));
-  if (shd) TPST_HIP(ctx, hipStreamSynchronize(ctx->comm));
+  if (shd || rb >= 0) TPST_HIP(ctx, hipStreamSynchronize(ctx->comm));
   xyzz_to_canonical_host<Fq>(pin + dn_final, 1, proof->final_a);
   xyzz_to_canonical_host<Fq2>(pin + dn_fh, 1, proof->final_h);
   if (m > 0) memcpy(proof->pst_proof_h, pin + dn_ph, (size_t)m * 96);
