@@ -3,6 +3,7 @@
 #include "coop.h"
 #include "fbt.h"
 #include "glv.h"
+#include <cstdlib>
 
 namespace tpst {
 
@@ -302,7 +303,11 @@ hipError_t fbt_msm(Arena& ar, hipStream_t s, const uint32_t* d_table, const uint
   constexpr int BS = fbt_block<F>();
   constexpr size_t Q = BS / 4;  // quads per block
   const size_t G = g.groups * g.sets;
-  if (!g.d_seg && g.members && g.members * 8 <= Q) {  // few members: one launch
+  // few members in few groups: one launch (latency-bound shapes; with many
+  // groups the tree levels' idle quads cost throughput: 2^24's first h fold,
+  // 2048 groups of 2 members, 3.2 ms in one launch; 2^24 open 22.85 -> 22.45
+  // ms with the cap, profiles/r06/ab/ab_fbt_small.txt)
+  if (!g.d_seg && g.members && g.members * 8 <= Q && G <= 256) {
     int lpq = 1;
     while (g.members * 8 * (8 / lpq) > Q) lpq <<= 1;
     k_fbt_small_quad<F><<<(unsigned)G, BS, 0, s>>>(d_table, d_scalars, g, lpq, d_out);
