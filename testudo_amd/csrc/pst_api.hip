@@ -1315,8 +1315,8 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
   // than a round) and C, the h preparation, at the greatest priority.  h^(r)
   // (G2 fold + G2Prepared lines) is prepared in every round r >= 1 that a
   // look-ahead needs: look-ahead r pairs E = 2^(r - s) fold sets of a^(r)
-  // against the prepared h^(s), s = r - 1 (prepared one round earlier: E = 2),
-  // s = 0 for r <= 1.  Preparing at odd rounds only (s = r - 2 / r - 3, E =
+  // against the prepared h^(s), s = r - 1 (prepared one round earlier: E = 2;
+  // in round 1 itself for r = 1: E = 1), s = 0 for r = 0.  Preparing at odd rounds only (s = r - 2 / r - 3, E =
   // 4 / 8) paired two to four times as many pairs; C on stream A delayed the
   // next round's t (2^24 open 26.6 -> 25.5 ms, 2^20 13.0 -> 11.4 ms with both,
   // profiles/r05/i).  The epilogue's final h fold runs on the first look-ahead
@@ -1337,7 +1337,10 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
   hipEvent_t* xev = ev + 9 + 6 * m;                         // exchange events (sharded form)
   int last_c = -1;  // the last odd round that issued h work "C"
   // the prepared h the look-ahead of round r pairs against (see above)
-  auto la_src = [](int r) { return r <= 1 ? 0 : r - 1; };
+  // look-ahead 1 pairs h^(1), prepared by C in round 1 (enqueued before D
+  // there), with E = 1 instead of h^(0) with E = 2: half the pairs (2^24 open
+  // 22.9 -> 22.5 ms, profiles/r06/ab/ab_open_la1.txt)
+  auto la_src = [](int r) { return r == 0 ? 0 : r - 1; };
   // which odd rounds prepare h: for a look-ahead on the rank's own positions
   // (local, sharded rounds) or on every position (global)
   std::vector<char> need_loc(m + 1, 0), need_glob(m + 1, 0);
@@ -1706,6 +1709,48 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
     if (!a_first)
       if (int rc = enqueue_a()) return rc;
     const double ha = open_trace() ? host_us() : 0.0;
+    auto enqueue_c = [&]() -> int {
+      // -- C: h^(r) prepared for the look-ahead of round r+1: at this rank's
+      // positions (sharded look-aheads) and / or at all
+      const bool c_glob = need_glob[r];
+      if (need_loc[r] || c_glob) {
+        TPST_HIP(ctx, hipStreamWaitEvent(sC, ev_up(r), 0));
+        if (r >= 3) TPST_HIP(ctx, hipStreamWaitEvent(sC, ev_la(r - 2), 0));  // last reader of h^(r-3)'s slot
+      }
+      if (need_loc[r]) {
+        const size_t ln = len / W;
+        TPST_HIP(ctx, mipp_scalars(sC, dWi, nullptr, len, 0, Cl, ScC.u(), W, rho));
+        FbGroups g;
+        g.groups = ln;
+        g.members = C / len;
+        g.L = ln;
+        g.D = 1;
+        TPST_HIP(ctx, fbt_msm<Fq2>(arC, sC, tHl, ScC.u(), g, (Xyzz<Fq2>*)xh.p));
+        TPST_HIP(ctx, xyzz_to_affine_mont<Fq2>(sC, (Xyzz<Fq2>*)xh.p, Hbl[r % 3].u(), ln));
+        TPST_HIP(ctx, g2_prepare_batch(sC, Hbl[r % 3].u(), ln, (LineCoeff*)Lbl[r % 3].p,
+                                       st->prep_scratch.u()));
+        TPST_HIP(ctx, hipEventRecord(ev_cl(r), sC));
+        last_c = r;
+      }
+      if (c_glob) {
+        TPST_HIP(ctx, mipp_scalars(sC, dWi, nullptr, len, 0, C, ScC.u()));
+        FbGroups g;
+        g.groups = len;
+        g.members = C / len;
+        g.L = len;
+        g.D = 1;
+        TPST_HIP(ctx, fbt_msm<Fq2>(arC, sC, tH, ScC.u(), g, (Xyzz<Fq2>*)xh.p));
+        TPST_HIP(ctx, xyzz_to_affine_mont<Fq2>(sC, (Xyzz<Fq2>*)xh.p, Hb[r % 3].u(), len));
+        TPST_HIP(ctx, g2_prepare_batch(sC, Hb[r % 3].u(), len, (LineCoeff*)Lb[r % 3].p,
+                                       st->prep_scratch.u()));
+        TPST_HIP(ctx, hipEventRecord(ev_c(r), sC));
+        last_c = r;
+      }
+      return TPST_OK;
+    };
+    const bool c_first = r == 1;  // look-ahead 1 pairs this round's h
+    if (c_first)
+      if (int rc = enqueue_c()) return rc;
     // -- D: look-ahead products of this round's vectors for round r+1
     if (len >= 4) {
       hipStream_t sD = sLA[r & 1];
@@ -1769,42 +1814,8 @@ static int poly_open(tpst_ctx* ctx, tpst_poly* p, tpst_transcript* tr, int n, co
       if (int rc = pst_q()) return rc;
 
     const double hp = open_trace() ? host_us() : 0.0;
-    // -- C: h^(r) prepared for the look-ahead of round r+1: at this rank's
-    // positions (sharded look-aheads) and / or at all
-    const bool c_glob = need_glob[r];
-    if (need_loc[r] || c_glob) {
-      TPST_HIP(ctx, hipStreamWaitEvent(sC, ev_up(r), 0));
-      if (r >= 3) TPST_HIP(ctx, hipStreamWaitEvent(sC, ev_la(r - 2), 0));  // last reader of h^(r-3)'s slot
-    }
-    if (need_loc[r]) {
-      const size_t ln = len / W;
-      TPST_HIP(ctx, mipp_scalars(sC, dWi, nullptr, len, 0, Cl, ScC.u(), W, rho));
-      FbGroups g;
-      g.groups = ln;
-      g.members = C / len;
-      g.L = ln;
-      g.D = 1;
-      TPST_HIP(ctx, fbt_msm<Fq2>(arC, sC, tHl, ScC.u(), g, (Xyzz<Fq2>*)xh.p));
-      TPST_HIP(ctx, xyzz_to_affine_mont<Fq2>(sC, (Xyzz<Fq2>*)xh.p, Hbl[r % 3].u(), ln));
-      TPST_HIP(ctx, g2_prepare_batch(sC, Hbl[r % 3].u(), ln, (LineCoeff*)Lbl[r % 3].p,
-                                     st->prep_scratch.u()));
-      TPST_HIP(ctx, hipEventRecord(ev_cl(r), sC));
-      last_c = r;
-    }
-    if (c_glob) {
-      TPST_HIP(ctx, mipp_scalars(sC, dWi, nullptr, len, 0, C, ScC.u()));
-      FbGroups g;
-      g.groups = len;
-      g.members = C / len;
-      g.L = len;
-      g.D = 1;
-      TPST_HIP(ctx, fbt_msm<Fq2>(arC, sC, tH, ScC.u(), g, (Xyzz<Fq2>*)xh.p));
-      TPST_HIP(ctx, xyzz_to_affine_mont<Fq2>(sC, (Xyzz<Fq2>*)xh.p, Hb[r % 3].u(), len));
-      TPST_HIP(ctx, g2_prepare_batch(sC, Hb[r % 3].u(), len, (LineCoeff*)Lb[r % 3].p,
-                                     st->prep_scratch.u()));
-      TPST_HIP(ctx, hipEventRecord(ev_c(r), sC));
-      last_c = r;
-    }
+    if (!c_first)
+      if (int rc = enqueue_c()) return rc;
 
     if (r == rb) {  // the rebase (see rb above), consumed from round rb + 1 on
       const hipStream_t sR = ctx->comm;
